@@ -1,0 +1,219 @@
+"""Benchmark: train interactions/s, MF-BPR dim=64, MovieLens-20M-shaped, 1 -> 8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one pass of the hot path over one batch of B = 8192 positives per
+GPU (weak scaling), each with n = 5 negatives drawn bit-exactly from the CPython
+MT19937 stream, the BPR loss on the neg.view(n, B) pairing, backward, and a dense
+coupled-L2 Adam update of every row of the four BilinearNet tables (the
+reference's semantics: implicit.py:347-364, spotlight/optimizers.py:10-16).
+Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
+
+Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
+max over ranks of the timed wall time.  `roofline` is for the dominant kernel
+(rg_mf_apply, the dense optimizer pass), timed with HIP events on the stream it
+is launched on; `cpu_baseline` times the CPU restatement (oracle/, the
+reference's algorithm incl. its random.choices sampler) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "train interactions/sec, MF-BPR dim=64 MovieLens-20M, 1→8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+
+def algorithmic_bytes(U, I, d, B, n):
+    """gathers + ids + dense Adam (read+write p, m, v) per step."""
+    gather = B * (1 + n) * 2 * (4 * d + 4)
+    ids = B * (16 + 24 * n)
+    adam = 6 * (U + I) * (4 * d + 4)
+    return gather, ids, adam
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=8192, help="positives per GPU per step")
+    ap.add_argument("--neg", type=int, default=5)
+    ap.add_argument("--loss", default="bpr")
+    ap.add_argument("--optim", default="adam")
+    ap.add_argument("--zipf", type=float, default=1.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(data, d, B, n, loss, budget_s):
+    """Time the oracle's CPU restatement (torch-CPU math + CPython random.choices over
+    a list of tuples, as implicit.py:352) on a bounded number of full-size steps."""
+    from oracle import mf as omf
+    from oracle import rng as orng
+    torch.manual_seed(0)
+    U, I = data.num_users, data.num_items
+    tabs = omf.init_tables(U, I, d)
+    random.seed(0)
+    t0 = time.time()
+    o = omf.MFOracle(*tabs, data.pool_u, data.pool_i, orng.state_from_python(random.getstate()), loss=loss,
+                     optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, python_sampler=True)
+    setup = time.time() - t0
+    pu = torch.from_numpy(data.train_u)
+    pi = torch.from_numpy(data.train_i)
+    o.step(pu[:B], pi[:B])          # warm-up
+    steps, t0 = 0, time.time()
+    while True:
+        s = (steps + 1) * B
+        o.step(pu[s:s + B], pi[s:s + B])
+        steps += 1
+        el = time.time() - t0
+        if el >= budget_s or steps >= 200:
+            break
+    return {"value": steps * B / el, "unit": "interactions/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{steps} full steps (B={B}, n={n}, d={d}, {loss}, Adam over U={U} I={I}, "
+                      f"pool {len(data.pool_u)}) after 1 warm-up step, {el:.1f} s timed "
+                      f"(+{setup:.1f} s pool/tuple setup untimed)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    from recommendation_gans_amd import build as rg_build
+    from recommendation_gans_amd.mf_engine import MFEngine
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    from oracle import rng as orng  # noqa: F401  (state glue only; not on the timed path)
+
+    if not os.path.exists(rg_build.LIB):
+        rg_build.build()
+    d, B, n = args.dim, args.batch, args.neg
+    data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
+    U, I = data.num_users, data.num_items
+    torch.manual_seed(0)                               # mf_spotlight.py:37
+    Uw = torch.empty(U, d).normal_(0, 1.0 / d)         # ScaledEmbedding (layers.py:35)
+    Iw = torch.empty(I, d).normal_(0, 1.0 / d)
+    random.seed(0)
+    mt = np.asarray(random.getstate()[1], dtype=np.uint32)
+    eng = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), data.pool_u, data.pool_i, mt, loss=args.loss,
+                   optimizer=args.optim, lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev,
+                   rank=rank, world_size=world, prefetch=not args.no_prefetch)
+    tu = torch.from_numpy(data.train_u).to(dev)
+    ti = torch.from_numpy(data.train_i).to(dev)
+    gb = B * world
+    nbatches = len(data.train_u) // gb
+    # per-batch plans: the epoch order is fixed for the whole fit (implicit.py:262), so
+    # they are built once, before timing (like the reference's own data preparation)
+    nplan = min(nbatches, args.warmup + args.steps)
+    plans = [eng.make_plan(ti[g * gb + rank * B:g * gb + rank * B + B]) for g in range(nplan)]
+
+    def batch(s):
+        g = s % nbatches
+        lo = g * gb + rank * B
+        return tu[lo:lo + B], ti[lo:lo + B], plans[g % nplan]
+
+    if world > 1:
+        def allreduce(t):
+            dist.all_reduce(t)
+
+        def step(s, ev=None):
+            u, i, p = batch(s)
+            return eng.train_step_dp(u, i, gb, allreduce, plan=p)
+    else:
+        # step inputs (ids + plan pointers) built before timing; each call also hands the
+        # NEXT step's input to the native stepper, which generates its words ahead
+        inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + 1)]
+
+        def step(s, ev=None):
+            return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if world == 1 else None
+    if evs:   # torch creates the HIP event lazily on its first record
+        for a, b_ in evs:
+            a.record()
+            b_.record()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s, evs[s] if evs else None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss_last = float(eng.loss_out[0])
+
+    if rank == 0:
+        value = args.steps * B * world / el
+        gather, ids, adam = algorithmic_bytes(U, I, d, B, n)
+        out = {"metric": METRIC, "value": value, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": f"synthetic ML-20M-shaped: U={U} I={I}, {len(data.train_u)} train positives "
+                       f"(lognormal users, Zipf({args.zipf}) items, 81/9/10 time split), "
+                       f"pool {len(data.pool_u)} uniform pairs; tables N(0,1/d) init",
+               "config": {"workload": f"MF-{args.loss.upper()} ML-20M-shaped, embedding_dim={d}, "
+                                      f"batch {B}/GPU, {n} negatives, {args.optim} (coupled L2 1e-5) over all rows",
+                          "global_batch": gb, "embedding_dim": d, "parallelism": f"dp{world}"}}
+        step_bytes = gather + ids + adam
+        out["step_roofline"] = {"bytes_per_step": step_bytes,
+                                "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
+                                "frac": step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS}
+        if evs:
+            from recommendation_gans_amd import _lib
+            ms = [_lib.elapsed_ms(a, b) for a, b in evs]
+            avg = float(np.mean(ms)) * 1e-3
+            ach = adam / avg / 1e9
+            out["roofline"] = {"bound": "hbm", "kernel": "rg_mf_apply (mf_apply_kernel)", "achieved": ach,
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                               "traffic": None, "algorithmic_bytes_per_launch": adam,
+                               "avg_launch_us": avg * 1e6}
+            pmc = os.path.join(ROOT, "profiles", "pmc_apply.json")
+            if os.path.exists(pmc):
+                p = json.load(open(pmc))
+                if p.get("dim") == d and p.get("batch") == B:
+                    out["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
+        out["final_loss"] = loss_last
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

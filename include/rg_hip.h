@@ -1,0 +1,267 @@
+/*
+ * rg_hip.h -- C-ABI of librg_hip.so, the MI355X (gfx950) hot path of the
+ * recommendation_Gans embedding-training loop.
+ *
+ * Conventions
+ *   - Every pointer named *_dev / inside the structs is a DEVICE pointer owned by
+ *     the caller (PyTorch's caching allocator); the library allocates no device
+ *     memory.  Host pointers are marked "host".
+ *   - Every call is stream-ordered on `stream` (a hipStream_t passed as void*),
+ *     never synchronises the host, and returns RG_OK (0) or a negative status;
+ *     rg_last_error() then holds a thread-local message.
+ *   - No torch types cross this boundary.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference checkout):
+ *   rg_mt_generate      random.choices' MT19937 stream      implicit.py:352, :370
+ *   rg_mf_pairs         BilinearNet.forward x2 + loss + autograd
+ *                                                          implicit.py:348-361,
+ *                                                          spotlight/factorization/representations.py:62-91,
+ *                                                          spotlight/losses.py:20-172
+ *   rg_mf_apply         optimizer.step() over every row     implicit.py:363,
+ *                                                          spotlight/optimizers.py:4-22
+ *   rg_mf_grads /       the same step split around an RCCL all-reduce of the
+ *   rg_mf_apply_dense   gradient (data parallel; no reference counterpart)
+ *   rg_mf_scores        BilinearNet.forward (eval / predict)
+ *                                                          implicit.py:368, :412
+ *   rg_loss_finalize    loss.item() of run_val_iteration    implicit.py:366-379
+ */
+#ifndef RG_HIP_H
+#define RG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_OK 0
+#define RG_E_ARG (-1)      /* invalid argument / unsupported shape */
+#define RG_E_LAUNCH (-2)   /* HIP launch or runtime error */
+
+/* capacity of the per-row contribution list (rows touched more often spill into
+ * the overflow accumulators hot_grad / hot_bias_grad) */
+#define RG_MF_LIST_CAP 8
+/* maximum negatives per positive handled by the fused pair kernel */
+#define RG_MF_MAX_NEG 8
+
+enum rg_loss_kind {
+    RG_LOSS_POINTWISE = 0,       /* spotlight/losses.py:20   BCE(pos,1) + BCE(neg,0) */
+    RG_LOSS_BPR = 1,             /* spotlight/losses.py:59   mean(1 - sigmoid(pos - neg)), neg.view(n,B) */
+    RG_LOSS_HINGE = 2,           /* spotlight/losses.py:99   mean(clamp(neg - pos + 1, 0)), neg.view(n,B) */
+    RG_LOSS_ADAPTIVE_HINGE = 3   /* spotlight/losses.py:133  hinge against max over ALL negatives */
+};
+
+enum rg_opt_kind {
+    RG_OPT_ADAM = 0,   /* torch.optim.Adam, coupled L2 (optimizers.py:10-16) */
+    RG_OPT_SGD = 1,    /* torch.optim.SGD, momentum 0     (optimizers.py:4-8)   */
+    RG_OPT_RMSPROP = 2 /* torch.optim.RMSprop, centered=False, momentum 0 (optimizers.py:18-22) */
+};
+
+/* The four BilinearNet tables (fp32, row-major, rows contiguous) plus optimizer
+ * state.  Updates are written to the *_out tables (ping-pong): the pull-style
+ * gradient gather reads the pre-step rows of the OTHER table while rows are
+ * being updated, so *_out must not alias the inputs. */
+typedef struct rg_mf_tables {
+    const float *user_w, *item_w;   /* [num_users, dim], [num_items, dim] */
+    const float *user_b, *item_b;   /* [num_users], [num_items] */
+    float *user_w_out, *item_w_out, *user_b_out, *item_b_out;
+    float *user_w_m, *user_w_v, *item_w_m, *item_w_v;   /* Adam m/v; RMSprop uses *_v */
+    float *user_b_m, *user_b_v, *item_b_m, *item_b_v;
+    int64_t num_users, num_items;
+    int32_t dim;                    /* 1..256 */
+    int32_t pad_;
+} rg_mf_tables_t;
+
+/* One training step's positives and negatives, for the caller's rank.
+ * Negative draw j (0 <= j < n_neg * global_cols) belongs to column j % global_cols
+ * and negative slot j / global_cols (the reference's flat draw order viewed as
+ * (n, B) -- SURVEY §0.1); this rank owns columns [col_offset, col_offset + cols).
+ * rg_mf_prepare fills `pairs` with the (user, item) ids of every pair in
+ * processing order (position s = column, or plan_perm[s] with a plan): row 0 the
+ * positives, row 1 + k negative slot k.  rg_mf_pairs reads only `pairs` (plus
+ * words/pool for the adaptive hinge's max). */
+typedef struct rg_mf_batch {
+    const int64_t *pos_user, *pos_item;  /* [n_pos] this rank's positives (column order) */
+    int64_t n_pos;          /* <= cols; < cols only on the last partial batch */
+    int64_t cols;           /* this rank's columns (batch_size) */
+    int64_t col_offset;     /* first global column owned by this rank */
+    int64_t global_cols;    /* batch_size * world_size */
+    int64_t global_pos;     /* positives in the whole (global) batch */
+    const uint32_t *words;  /* raw MT19937 words of this step (rg_mt_generate): draw j uses [2j], [2j+1] */
+    const int32_t *pool;    /* negative pool as int32 (user, item) pairs [pool_len] */
+    int64_t pool_len;
+    int32_t n_neg;          /* negatives per positive, 1..RG_MF_MAX_NEG */
+    int32_t loss;           /* enum rg_loss_kind */
+    int32_t *pairs;         /* [(1 + n_neg) * cols * 2] int32 (user, item), see above */
+} rg_mf_batch_t;
+
+/* Caller-owned scratch.  row_count, hot_grad and hot_bias_grad must be zero
+ * before the first step; the library leaves them zero after every
+ * rg_mf_pairs + rg_mf_apply/rg_mf_grads pair.
+ *
+ * Optional per-batch plan (all plan_* null: no plan).  Positives are processed in
+ * item-sorted column order and the item-side gradient of the positives is reduced
+ * per pair-kernel block into partial rows (plain stores, fixed order) instead of
+ * per-row lists + atomics -- the Zipf-hot items.  With U = rg_mf_plan_units_per_block(dim):
+ *   plan_perm[s]          column processed at position s (a permutation of [0, cols)),
+ *                         positives (column < n_pos) sorted by item, then the rest
+ *   plan_pos_slot[s]      partial slot of position s: consecutive positions with the same
+ *                         item inside one block of U positions share a slot; slots are
+ *                         numbered in position order
+ *   plan_item_slot_off[i] item i's slots are [off[i], off[i+1])  (num_items + 1 entries)
+ * part_row / part_bias: [slots * dim] / [slots] partial sums (slots <= cols). */
+typedef struct rg_mf_work {
+    int32_t *row_count;      /* [num_users + num_items] */
+    int32_t *row_list;       /* [(num_users + num_items) * RG_MF_LIST_CAP * 2] {other row, dz bits} */
+    float *hot_grad;         /* [(num_users + num_items) * dim] overflow accumulators */
+    float *hot_bias_grad;    /* [num_users + num_items] */
+    float *loss_partials;    /* [rg_mf_partials_len(cols, dim)] */
+    float *scores;           /* [cols]  (adaptive hinge only) */
+    uint64_t *max_key;       /* [1] (adaptive hinge only) */
+    int32_t *active_count;   /* [1] (adaptive hinge only) */
+    const int32_t *plan_perm, *plan_pos_slot, *plan_item_slot_off;
+    float *part_row, *part_bias;
+} rg_mf_work_t;
+
+/* Loss reduction requested from rg_mf_apply / rg_mf_grads:
+ * *out = sum(partials[:,0]) * inv_a + sum(partials[:,1]) * inv_b. */
+typedef struct rg_mf_loss {
+    int64_t n_partials;
+    double inv_a, inv_b;
+    float *out;
+} rg_mf_loss_t;
+
+typedef struct rg_opt {
+    int32_t kind;            /* enum rg_opt_kind */
+    float lr, beta1, beta2, eps, weight_decay, alpha;
+    /* 1 - beta1, 1 - beta2, 1 - alpha evaluated in double on the host (as the
+     * Python optimizer does) and rounded once; fp32 (1 - 0.999f) would differ by 1.3e-5 */
+    float one_minus_beta1, one_minus_beta2, one_minus_alpha;
+    float step_size;         /* Adam: lr / (1 - beta1^t)  (host, double -> float) */
+    float bias_correction2_sqrt;  /* Adam: sqrt(1 - beta2^t) */
+} rg_opt_t;
+
+/* Extra words rg_mt_generate may write past nwords (the output buffer must hold
+ * nwords + RG_MT_PAD words). */
+#define RG_MT_PAD 1280
+
+/* MT19937 stream: advances `state_dev` (624 words + position, the layout of
+ * CPython's random.getstate()[1]) by `nwords` and writes the RAW (untempered)
+ * state words; output k, tempered, is the k-th genrand_uint32() CPython would
+ * return.  If state_before_dev is non-null, the state on entry is copied there
+ * first.  Runs as ONE workgroup (the recurrence is sequential). */
+int rg_mt_generate(void *stream, uint32_t *state_dev, uint32_t *out_words_dev,
+                   int64_t nwords, uint32_t *state_before_dev);
+
+/* Number of float loss partials rg_mf_pairs writes for `cols` columns. */
+int64_t rg_mf_partials_len(int64_t cols, int32_t dim);
+
+/* Positions per pair-kernel block, the block size a batch plan is built for. */
+int64_t rg_mf_plan_units_per_block(int32_t dim);
+
+/* Resolve the step's pairs: positives permuted to processing order and every
+ * negative draw -> pool index (CPython random.choices arithmetic) -> (user, item).
+ * Fully parallel; depends only on the words, the pool, the plan and the ids, so it
+ * can run ahead on another stream. */
+int rg_mf_prepare(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work);
+
+/* Forward of all pairs of the step, the loss terms, dL/dz, and the per-row
+ * contribution lists (+ planned partials) consumed by rg_mf_apply / rg_mf_grads.
+ * backward = 0 computes the loss only (validation, implicit.py:366). */
+int rg_mf_pairs(void *stream, const rg_mf_tables_t *tables, const rg_mf_batch_t *batch,
+                rg_mf_work_t *work, int32_t backward);
+
+/* Rows are numbered users [0, U) then items [U, U + I); [row_begin, row_end)
+ * selects the rows a call touches (row_end < 0: all).  Item rows run first. */
+
+/* Gradient gather (pull from the contribution lists) + optimizer update of EVERY
+ * row in the range (coupled weight decay touches all rows).  loss: optional. */
+int rg_mf_apply(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
+                int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss);
+
+/* Pull the DATA gradient (no weight decay) of the rows in range into the flat
+ * buffer grad_dev = [n*dim row grads | n bias grads | loss], n = row_end - row_begin
+ * (the loss slot is written when loss->out is non-null).  Resets the lists like
+ * rg_mf_apply.  The caller all-reduces grad_dev across ranks (RCCL). */
+int rg_mf_grads(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, float *grad_dev,
+                int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss);
+
+/* Optimizer update of the rows in range from a (summed) flat gradient
+ * (+ weight_decay * p).  loss_out_dev (optional) receives grad_dev's loss slot. */
+int rg_mf_apply_dense(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
+                      int64_t row_begin, int64_t row_end, float *loss_out_dev);
+
+/* loss = sum(partials[:,0]) * inv_a + sum(partials[:,1]) * inv_b  (one block). */
+int rg_loss_finalize(void *stream, const float *partials_dev, int64_t n_partials,
+                     double inv_a, double inv_b, float *loss_out_dev);
+
+/* Scores sigmoid(<U[u],I[i]> + ub[u] + ib[i]) for n pairs (ids int64). */
+int rg_mf_scores(void *stream, const float *user_w, const float *item_w,
+                 const float *user_b, const float *item_b, int32_t dim,
+                 const int64_t *users, const int64_t *items, int64_t n, float *out);
+
+/* ------------------------------------------------------------------------------
+ * Native step runtime (rg_stepper.cpp): one call per training step enqueues
+ *   side stream:  rg_mt_generate + rg_mf_prepare of the NEXT step (generated ahead)
+ *   main stream:  rg_mf_pairs -> rg_mf_apply of the current step
+ * Replaces the loop body implicit.py:290-298 / run_train_iteration :347-364.
+ * ---------------------------------------------------------------------------- */
+typedef struct rg_mf_stepper_config {
+    rg_mf_tables_t tables[2];       /* tables[k]: reads set k, writes set 1 - k */
+    rg_mf_work_t work;              /* plan_* fields are set per step */
+    uint32_t *mt_state, *mt_state_before;   /* [625] each */
+    uint32_t *words[2];             /* [2 * n_neg * global_cols + RG_MT_PAD] each */
+    int32_t *pairs[2];              /* [(1 + n_neg) * cols * 2] each */
+    const int32_t *pool;
+    int64_t pool_len;
+    int32_t n_neg, loss;
+    int64_t cols, col_offset, global_cols;
+    rg_opt_t opt;                   /* kind + fp32 hyper-parameters */
+    double lr_d, beta1_d, beta2_d;  /* the same as Python floats (Adam bias corrections) */
+    int64_t step;                   /* optimizer steps already taken */
+    int64_t n_partials;
+    int32_t current_set, pad_;
+} rg_mf_stepper_config_t;
+
+typedef struct rg_mf_step_in {
+    const int64_t *pos_user, *pos_item;
+    int64_t n_pos, global_pos;
+    const int32_t *plan_perm, *plan_pos_slot, *plan_item_slot_off;   /* optional plan */
+} rg_mf_step_in_t;
+
+void *rg_mf_stepper_create(const rg_mf_stepper_config_t *config);
+int rg_mf_stepper_destroy(void *stepper);
+/* One fused training step on `stream`; `next` (optional) = the following step's
+ * inputs, whose words and pairs are produced ahead on the side stream.  Optional
+ * events (hipEvent_t) are recorded around rg_mf_apply. */
+int rg_mf_stepper_train(void *stepper, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
+                        float *loss_out_dev, void *ev_apply_begin, void *ev_apply_end);
+/* Words + pairs of `cur` for an external consumer on `stream` (validation, split
+ * data-parallel steps); *batch_out / *work_out are ready for rg_mf_pairs.
+ * Follow the consumer's launch with rg_mf_stepper_release. */
+int rg_mf_stepper_acquire(void *stepper, void *stream, const rg_mf_step_in_t *cur, rg_mf_batch_t *batch_out,
+                          rg_mf_work_t *work_out);
+int rg_mf_stepper_release(void *stepper, void *stream);
+/* Optimizer scalars for optimizer step `step` (1-based). */
+int rg_mf_stepper_opt(void *stepper, int64_t step, rg_opt_t *opt_out);
+int rg_mf_stepper_state(void *stepper, int32_t *current_set, int64_t *step);
+/* After an external update: flip the ping-pong sets and count optimizer steps. */
+int rg_mf_stepper_advance(void *stepper, int32_t flip_sets, int64_t steps);
+/* direction 0: copy the MT state after the last consumed word to host_state[625];
+ * 1: load host_state into the device state (drops words generated ahead).  Synchronises. */
+int rg_mf_stepper_sync_mt(void *stepper, uint32_t *host_state, int32_t direction);
+
+/* Milliseconds between two timing events (hipEvent_t) recorded on a stream. */
+int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms);
+
+/* Thread-local description of the last error. */
+const char *rg_last_error(void);
+
+/* Library build identification (gfx target, ABI version). */
+const char *rg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RG_HIP_H */

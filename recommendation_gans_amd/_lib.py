@@ -1,0 +1,179 @@
+"""ctypes binding of librg_hip.so (include/rg_hip.h).
+
+There is deliberately no CPU fallback: if the library is missing or cannot be
+loaded, every entry point raises ``RuntimeError``.  ``torch`` is imported
+before the library so that the HIP runtime torch ships (SONAME
+libamdhip64.so.7) is the one librg_hip.so binds to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "librg_hip.so")
+
+RG_OK = 0
+RG_MF_LIST_CAP = 8
+RG_MF_MAX_NEG = 8
+RG_MT_PAD = 1280
+
+LOSS_KINDS = {"pointwise": 0, "bpr": 1, "hinge": 2, "adaptive_hinge": 3}
+OPT_KINDS = {"adam": 0, "sgd": 1, "rms": 2}
+
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class MFTables(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "user_w", "item_w", "user_b", "item_b",
+        "user_w_out", "item_w_out", "user_b_out", "item_b_out",
+        "user_w_m", "user_w_v", "item_w_m", "item_w_v",
+        "user_b_m", "user_b_v", "item_b_m", "item_b_v")] + [
+        ("num_users", ctypes.c_int64), ("num_items", ctypes.c_int64),
+        ("dim", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class MFBatch(ctypes.Structure):
+    _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p),
+                ("n_pos", ctypes.c_int64), ("cols", ctypes.c_int64), ("col_offset", ctypes.c_int64),
+                ("global_cols", ctypes.c_int64), ("global_pos", ctypes.c_int64),
+                ("words", ctypes.c_void_p), ("pool", ctypes.c_void_p), ("pool_len", ctypes.c_int64),
+                ("n_neg", ctypes.c_int32), ("loss", ctypes.c_int32), ("pairs", ctypes.c_void_p)]
+
+
+class MFWork(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "row_count", "row_list", "hot_grad", "hot_bias_grad", "loss_partials", "scores",
+        "max_key", "active_count", "plan_perm", "plan_pos_slot", "plan_item_slot_off",
+        "part_row", "part_bias")]
+
+
+class MFLoss(ctypes.Structure):
+    _fields_ = [("n_partials", ctypes.c_int64), ("inv_a", ctypes.c_double), ("inv_b", ctypes.c_double),
+                ("out", ctypes.c_void_p)]
+
+
+class Opt(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("alpha", ctypes.c_float), ("one_minus_beta1", ctypes.c_float),
+                ("one_minus_beta2", ctypes.c_float), ("one_minus_alpha", ctypes.c_float),
+                ("step_size", ctypes.c_float),
+                ("bias_correction2_sqrt", ctypes.c_float)]
+
+
+class MFStepperConfig(ctypes.Structure):
+    _fields_ = [("tables", MFTables * 2), ("work", MFWork), ("mt_state", ctypes.c_void_p),
+                ("mt_state_before", ctypes.c_void_p), ("words", ctypes.c_void_p * 2), ("pairs", ctypes.c_void_p * 2),
+                ("pool", ctypes.c_void_p), ("pool_len", ctypes.c_int64), ("n_neg", ctypes.c_int32),
+                ("loss", ctypes.c_int32), ("cols", ctypes.c_int64), ("col_offset", ctypes.c_int64),
+                ("global_cols", ctypes.c_int64), ("opt", Opt), ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double),
+                ("beta2_d", ctypes.c_double), ("step", ctypes.c_int64), ("n_partials", ctypes.c_int64),
+                ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class MFStepIn(ctypes.Structure):
+    _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
+                ("global_pos", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
+                ("plan_item_slot_off", ctypes.c_void_p)]
+
+
+# (name, restype, argtypes) for every symbol declared in include/rg_hip.h
+SIGNATURES = [
+    ("rg_mt_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.c_void_p]),
+    ("rg_mf_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_mf_plan_units_per_block", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_mf_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
+    ("rg_mf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
+                                   ctypes.POINTER(MFWork), ctypes.c_int32]),
+    ("rg_mf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                   ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
+    ("rg_mf_grads", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
+    ("rg_mf_apply_dense", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,
+                                         ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]),
+    ("rg_loss_finalize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_void_p]),
+    ("rg_mf_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int64, ctypes.c_void_p]),
+    ("rg_mf_stepper_create", ctypes.c_void_p, [ctypes.POINTER(MFStepperConfig)]),
+    ("rg_mf_stepper_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("rg_mf_stepper_train", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                           ctypes.POINTER(MFStepIn), ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    ("rg_mf_stepper_acquire", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                             ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
+    ("rg_mf_stepper_release", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_opt", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Opt)]),
+    ("rg_mf_stepper_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_advance", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]),
+    ("rg_mf_stepper_sync_mt", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
+    ("rg_event_elapsed_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_last_error", ctypes.c_char_p, []),
+    ("rg_version", ctypes.c_char_p, []),
+]
+
+_lib = None
+_load_error = None
+
+
+def load(path=None):
+    """Load librg_hip.so (once) and bind every exported entry point."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"librg_hip.so not found at {p}: build it with "
+                           "`python -m recommendation_gans_amd.build` (hipcc, gfx950). "
+                           "There is no CPU fallback for the hot path.")
+    try:
+        L = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover
+        _load_error = e
+        raise RuntimeError(f"cannot load {p}: {e}") from e
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != RG_OK:
+        msg = load().rg_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def elapsed_ms(ev_begin, ev_end):
+    """Elapsed time of a torch.cuda.Event pair recorded natively (rg_mf_stepper_train)."""
+    ms = ctypes.c_float()
+    check(load().rg_event_elapsed_ms(ctypes.c_void_p(ev_begin.cuda_event), ctypes.c_void_p(ev_end.cuda_event),
+                                     ctypes.byref(ms)), "rg_event_elapsed_ms")
+    return ms.value
+
+
+def require_gpu(tensor_or_device=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("the recommendation_gans_amd hot path runs on an MI355X (ROCm) GPU only; "
+                           "torch.cuda.is_available() is False")

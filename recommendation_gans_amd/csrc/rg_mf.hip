@@ -1,0 +1,904 @@
+// Matrix-factorisation training step for gfx950 (MI355X).
+//
+// Replaces, per step (implicit.py:347-364 run_train_iteration):
+//   BilinearNet.forward on B positives and n*B negatives
+//       (spotlight/factorization/representations.py:62-91),
+//   the loss (spotlight/losses.py: pointwise :20, bpr :59, hinge :99, adaptive :133),
+//   loss.backward() -> embedding_dense_backward into dense (U,d),(I,d),(U,1),(I,1) grads,
+//   optimizer.step() (spotlight/optimizers.py) over EVERY row (coupled L2).
+//
+// Two kernels per step, both HBM-bound:
+//   mf_pairs  one "unit" = one batch column b: its positive and its n negatives
+//             (flat draws k*B + b).  LPU lanes per unit, one float4 of every
+//             gathered row per lane, dot products by DPP row reductions, loss
+//             terms, dL/dz.  Instead of scatter-adding row gradients with float
+//             atomics (memory-side, ~1.3 TB/s chip-wide) each pair appends a
+//             4+4-byte {other row, dz} entry to the list of each of its two rows
+//             (one returning int atomic per row); rows touched more than
+//             RG_MF_LIST_CAP times spill the excess into dense overflow
+//             accumulators with float atomics (Zipf-hot items only).
+//   mf_apply  streams every row of both tables once: p, m, v in; the row's
+//             gradient is PULLED from its list (gathering the other table's
+//             pre-step row, which is why the parameter tables ping-pong) plus
+//             weight_decay * p; Adam / SGD / RMSprop; p', m, v out; the list
+//             counter and overflow accumulators are reset in the same pass.
+#include "rg_common.h"
+
+namespace rg {
+
+constexpr int kCap = RG_MF_LIST_CAP;
+constexpr int kNMax = RG_MF_MAX_NEG;
+constexpr int kBlock = 256;
+
+// kFused: forward + loss + lists.  kLossOnly: forward + loss (validation).
+// Adaptive hinge needs the global max first: kAdaptFwd (scores + max),
+// then kAdaptBwd (positives vs max + lists) or kAdaptLoss (loss only).
+enum Phase : int { kFused = 0, kLossOnly = 1, kAdaptFwd = 2, kAdaptBwd = 3, kAdaptLoss = 4 };
+
+struct PairsArgs {
+    const float *user_w, *item_w, *user_b, *item_b;
+    int64_t num_users;
+    int32_t dim;
+    const int64_t *pos_user, *pos_item;
+    int64_t n_pos, cols, col_offset, global_cols;
+    const uint2 *words;
+    const int2 *pool;
+    int64_t pool_len;
+    int32_t n_neg, loss;
+    float n_a, n_b;            // mean denominators (as ATen divides: grad / numel)
+    int32_t *row_count;
+    int2 *row_list;
+    float *hot_grad, *hot_bias_grad;
+    float *partials;
+    float *scores;             // adaptive: [cols] positive scores
+    unsigned long long *max_key;
+    int32_t *active_count;
+    const int32_t *perm;       // plan: processing position -> column (null: identity)
+    const int32_t *pos_slot;   // plan: position -> partial slot of its positive's item side
+    float *part_row, *part_bias;
+    const int2 *pairs;         // prepared (user, item) per pair: [(1 + n) * cols], processing order
+};
+
+// rg_mf_prepare: pairs[q * cols + s] for q = 0 (positive) and q = 1 + k (negative k)
+__global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out) {
+    __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t total = (int64_t)(1 + a.n_neg) * a.cols;
+    if (idx >= total) return;
+    const int64_t q = idx / a.cols, s = idx - q * a.cols;
+    const int64_t col = a.perm ? (int64_t)a.perm[s] : s;
+    int2 r;
+    if (q == 0) {
+        r = (s < a.n_pos) ? make_int2((int)a.pos_user[col], (int)a.pos_item[col]) : make_int2(0, 0);
+    } else {
+        const int64_t j = (q - 1) * a.global_cols + a.col_offset + col;
+        const uint2 w = a.words[j];
+        r = a.pool[choice_index(w.x, w.y, a.pool_len)];
+    }
+    out[idx] = r;
+}
+
+// atomically add a row-vector contribution (overflow path, rare)
+template <class L>
+__device__ __forceinline__ void overflow_add(float *__restrict__ hot, int64_t row, int D, int sub, float dz,
+                                             const float (&o)[L::EPL]) {
+#pragma unroll
+    for (int e = 0; e < L::EPL; ++e) {
+        const int c = L::elem(sub, e);
+        if (L::VEC || c < D) atomicAdd(hot + row * (int64_t)D + c, dz * o[e]);
+    }
+}
+
+// select x[q] for a runtime q without dynamic register indexing (no scratch)
+template <int N, class T>
+__device__ __forceinline__ T pick(const T (&x)[N], int q) {
+    T r = x[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) r = (q == k) ? x[k] : r;
+    return r;
+}
+
+constexpr int kLdsFloats = 1280;   // >= units per block * (dim + 1) for every layout
+
+// One unit = one batch column: pair q = 0 is the positive, q = 1..n the
+// negatives k*global_cols + col.  Every gather uses an always-valid index and is
+// issued unconditionally (results of invalid pairs are masked afterwards), so a
+// wave has all of its rows in flight at once.  The gathered rows die after their
+// dot product except the positive's user row, which feeds the planned item-side
+// partial sums; the rare list-overflow path re-gathers.
+//
+// List tasks: t = 2q + side (side 0: user row of pair q, 1: its item row), spread
+// over the unit's lanes as t = sub + j*LPU.  With a plan, the positives are
+// processed in item-sorted order and the positive's item side (t = 1, the Zipf-hot
+// rows) is instead reduced per block in LDS into one partial row per
+// (item, block): plain stores, no atomics, fixed order.
+template <class L, int PHASE, int NMAX>
+__global__ __launch_bounds__(kBlock) void mf_pairs_kernel(PairsArgs a) {
+    constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW, NP = NMAX + 1;
+    constexpr int UPB = kBlock / LPU;                  // units per block
+    constexpr int TPL = (2 * NP + LPU - 1) / LPU;      // list tasks per lane
+    constexpr bool kBackward = (PHASE == kFused) || (PHASE == kAdaptBwd);
+    constexpr bool kScoresFromBuf = (PHASE == kAdaptBwd) || (PHASE == kAdaptLoss);
+    __shared__ float red[2][kBlock / kWave];
+    __shared__ float lrow[kLdsFloats];
+    __shared__ int lslot[UPB];
+    __shared__ float ldz[kBackward ? UPB * NP : 1];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int ubase = lane & ~(LPU - 1);
+    const int ublk = threadIdx.x / LPU;               // unit within the block
+    const int64_t s = (int64_t)blockIdx.x * UPB + ublk; // processing position
+    const bool active = s < a.cols;
+    const bool plan = a.pos_slot != nullptr;
+    const bool has_pos = active && s < a.n_pos;        // a plan puts the positives first
+    const int D = a.dim;
+    const int n = a.n_neg;
+    const bool pairwise = (a.loss == RG_LOSS_BPR) || (a.loss == RG_LOSS_HINGE);
+
+    // ---- ids of every pair, prepared in processing order (one coalesced round trip) ----
+    int uid[NP], iid[NP];
+    bool valid[NP];
+    valid[0] = has_pos;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k)   // flat negatives that pair with no positive only matter to pointwise / adaptive
+        valid[k + 1] = !kScoresFromBuf && active && k < n && (has_pos || !pairwise);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const int2 pr = a.pairs[valid[q] || q == 0 ? (int64_t)q * a.cols + (active ? s : 0) : 0];
+        uid[q] = pr.x;
+        iid[q] = pr.y;
+    }
+
+    // ---- claim list slots early (their latency hides under the gathers) -------
+    int slot[TPL];
+#pragma unroll
+    for (int j = 0; j < TPL; ++j) {
+        slot[j] = 0;
+        const int t = sub + j * LPU;
+        if (kBackward && t < 2 * NP && !(plan && t == 1)) {
+            const int q = t >> 1;
+            if (pick(valid, q)) {
+                const int64_t row = (t & 1) ? a.num_users + pick(iid, q) : (int64_t)pick(uid, q);
+                slot[j] = atomicAdd(a.row_count + row, 1);
+            }
+        }
+    }
+
+    // ---- gather rows, scores ---------------------------------------------------
+    float p[NP];
+    float upos[EPL];      // the positive's user row (planned item-side partial sums)
+    L::zero(upos);
+    if (kScoresFromBuf) {
+        p[0] = has_pos ? a.scores[s] : 0.5f;
+#pragma unroll
+        for (int q = 1; q < NP; ++q) p[q] = 0.5f;
+        if (plan && kBackward) L::load(upos, a.user_w, uid[0], D, sub);
+    } else {
+        float ur[NP][EPL], ir[NP][EPL], ub[NP], ib[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            L::load(ur[q], a.user_w, uid[q], D, sub);
+            L::load(ir[q], a.item_w, iid[q], D, sub);
+            ub[q] = a.user_b[uid[q]];
+            ib[q] = a.item_b[iid[q]];
+        }
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) upos[e] = ur[0][e];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            float d = 0.0f;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) d = fmaf(ur[q][e], ir[q][e], d);
+            d = group_sum<LPU>(d);
+            p[q] = sigmoidf_ref((d + ub[q]) + ib[q]);
+        }
+    }
+
+    // ---- loss terms and dL/dp ---------------------------------------------------
+    float la = 0.0f, lb = 0.0f;
+    float dp[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) dp[q] = 0.0f;
+    if (PHASE == kAdaptFwd) {
+        if (sub == 0 && has_pos) a.scores[s] = p[0];
+        const int64_t col = a.perm ? (int64_t)a.perm[active ? s : 0] : s;
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) {
+            if (valid[k + 1] && sub == 0) {
+                const int64_t j = (int64_t)k * a.global_cols + a.col_offset + col;
+                const unsigned long long key = ((unsigned long long)__float_as_uint(p[k + 1]) << 32) |
+                                               (unsigned long long)(0xFFFFFFFFu - (uint32_t)j);
+                atomicMax(a.max_key, key);
+            }
+        }
+    } else if (kScoresFromBuf) {  // adaptive hinge, positives only (max negative: mf_adapt_max_kernel)
+        if (has_pos) {
+            const unsigned long long key = *a.max_key;
+            const float m = __uint_as_float((uint32_t)(key >> 32));
+            const float x = (m - p[0]) + 1.0f;
+            la = fmaxf(x, 0.0f);
+            if (x >= 0.0f) {
+                dp[0] = -(1.0f / a.n_a);
+                if (PHASE == kAdaptBwd && sub == 0) atomicAdd(a.active_count, 1);
+            }
+        }
+    } else if (a.loss == RG_LOSS_POINTWISE) {
+        if (has_pos) {
+            la = -fmaxf(logf(p[0]), -100.0f);
+            dp[0] = ((p[0] - 1.0f) / fmaxf((1.0f - p[0]) * p[0], 1e-12f)) / a.n_a;
+        }
+#pragma unroll
+        for (int k = 1; k < NP; ++k) {
+            if (valid[k]) {
+                lb += -fmaxf(logf(1.0f - p[k]), -100.0f);
+                dp[k] = (p[k] / fmaxf((1.0f - p[k]) * p[k], 1e-12f)) / a.n_b;
+            }
+        }
+    } else {  // bpr / hinge on the neg.view(n, B) pairing
+        const float g = 1.0f / a.n_a;
+        if (has_pos) {
+#pragma unroll
+            for (int k = 1; k < NP; ++k) {
+                if (valid[k]) {
+                    if (a.loss == RG_LOSS_BPR) {
+                        const float sg = sigmoidf_ref(p[0] - p[k]);
+                        la += 1.0f - sg;
+                        const float dx = (-g) * (1.0f - sg) * sg;
+                        dp[0] += dx;
+                        dp[k] = -dx;
+                    } else {
+                        const float x = (p[k] - p[0]) + 1.0f;
+                        la += fmaxf(x, 0.0f);
+                        const float dx = x >= 0.0f ? g : 0.0f;
+                        dp[0] -= dx;
+                        dp[k] = dx;
+                    }
+                }
+            }
+        }
+    }
+
+    // ---- dz, list entries, planned partials ----------------------------------------
+    if (kBackward) {
+        float dz[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) dz[q] = (dp[q] * (1.0f - p[q])) * p[q];
+        // the list tasks index dz by a lane-dependent pair: stage it through LDS
+        // (a register select chain is turned back into scratch by the compiler)
+        if (sub == 0) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) ldz[ublk * NP + q] = dz[q];
+        }
+        lds_barrier();
+        bool ovf = false;
+#pragma unroll
+        for (int j = 0; j < TPL; ++j) {
+            const int t = sub + j * LPU;
+            if (t < 2 * NP && !(plan && t == 1)) {
+                const int q = t >> 1;
+                if (pick(valid, q)) {
+                    const int u = pick(uid, q), i = pick(iid, q);
+                    const int64_t row = (t & 1) ? a.num_users + i : (int64_t)u;
+                    if (slot[j] < kCap)
+                        a.row_list[row * kCap + slot[j]] = make_int2((t & 1) ? u : i, __float_as_int(ldz[ublk * NP + q]));
+                    else
+                        ovf = true;
+                }
+            }
+        }
+        if (__any(ovf)) {   // wave-uniform: rows touched more than kCap times this step (re-gather)
+#pragma unroll
+            for (int t = 0; t < 2 * NP; ++t) {
+                const int sl = __shfl(slot[t / LPU], ubase + (t % LPU));
+                const int q = t >> 1;
+                if (valid[q] && sl >= kCap && !(plan && t == 1)) {
+                    float o[EPL];
+                    if (t & 1) {
+                        const int64_t row = a.num_users + iid[q];
+                        L::load(o, a.user_w, uid[q], D, sub);
+                        overflow_add<L>(a.hot_grad, row, D, sub, dz[q], o);
+                        if (sub == 0) atomicAdd(a.hot_bias_grad + row, dz[q]);
+                    } else {
+                        L::load(o, a.item_w, iid[q], D, sub);
+                        overflow_add<L>(a.hot_grad, uid[q], D, sub, dz[q], o);
+                        if (sub == 0) atomicAdd(a.hot_bias_grad + uid[q], dz[q]);
+                    }
+                }
+            }
+        }
+        if (plan) {
+            // block-level segmented sum of the positives' item-side rows, sorted by item
+            const int stride = D + 1;
+            const int myslot = has_pos ? a.pos_slot[s] : -1;
+            if (has_pos) {
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int c = L::elem(sub, e);
+                    if (L::VEC || c < D) lrow[ublk * stride + c] = dz[0] * upos[e];
+                }
+                if (sub == 0) lrow[ublk * stride + D] = dz[0];
+            }
+            if (sub == 0) lslot[ublk] = myslot;
+            lds_barrier();
+            if (has_pos && (ublk == 0 || lslot[ublk - 1] != myslot)) {   // segment head
+                float acc[EPL];
+                float accb = 0.0f;
+                L::zero(acc);
+                for (int v = ublk; v < UPB && lslot[v] == myslot; ++v) {
+#pragma unroll
+                    for (int e = 0; e < EPL; ++e) {
+                        const int c = L::elem(sub, e);
+                        if (L::VEC || c < D) acc[e] += lrow[v * stride + c];
+                    }
+                    accb += lrow[v * stride + D];
+                }
+                L::store(a.part_row, myslot, D, sub, acc);
+                if (sub == 0) a.part_bias[myslot] = accb;
+            }
+        }
+    }
+
+    // ---- deterministic loss partials: wave DPP sum -> block -> partials[block] ----
+    if (PHASE != kAdaptFwd) {
+        float va = (sub == 0) ? la : 0.0f;
+        float vb = (sub == 0) ? lb : 0.0f;
+        va = group_sum<kWave>(va);
+        vb = group_sum<kWave>(vb);
+        const int w = threadIdx.x >> 6;
+        if (lane == 0) { red[0][w] = va; red[1][w] = vb; }
+        lds_barrier();
+        if (threadIdx.x == 0) {
+            float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+            for (int i = 0; i < kBlock / kWave; ++i) { sa += red[0][i]; sb += red[1][i]; }
+            a.partials[2 * blockIdx.x] = sa;
+            a.partials[2 * blockIdx.x + 1] = sb;
+        }
+    }
+}
+
+// adaptive hinge: the global-max negative receives sum_b 1/Bp over active b
+// (spotlight/losses.py:170 torch.max(dim 0) backward -> argmax, first index on ties)
+template <class L>
+__global__ __launch_bounds__(kWave) void mf_adapt_max_kernel(PairsArgs a) {
+    constexpr int LPU = L::LPU, EPL = L::EPL;
+    const int lane = threadIdx.x;
+    const int sub = lane & (LPU - 1);
+    const unsigned long long key = *a.max_key;
+    const int64_t j = (int64_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+    const int64_t colg = j % a.global_cols;
+    const int64_t col = colg - a.col_offset;
+    if (col < 0 || col >= a.cols) return;            // another rank owns the max
+    if (lane >= LPU) return;
+    const float pm = __uint_as_float((uint32_t)(key >> 32));
+    const float dpv = (float)(*a.active_count) * (1.0f / a.n_a);
+    const float dz = (dpv * (1.0f - pm)) * pm;
+    const uint2 w = a.words[j];
+    const int2 pr = a.pool[choice_index(w.x, w.y, a.pool_len)];
+    float ur[EPL], ir[EPL];
+    L::load(ur, a.user_w, pr.x, a.dim, sub);
+    L::load(ir, a.item_w, pr.y, a.dim, sub);
+    for (int side = 0; side < 2; ++side) {
+        const int64_t row = side ? a.num_users + pr.y : (int64_t)pr.x;
+        int sl = 0;
+        if (sub == 0) sl = atomicAdd(a.row_count + row, 1);
+        sl = __shfl(sl, 0);
+        if (sl < kCap) {
+            if (sub == 0) a.row_list[row * kCap + sl] = make_int2(side ? pr.x : pr.y, __float_as_int(dz));
+        } else {
+            overflow_add<L>(a.hot_grad, row, a.dim, sub, dz, side ? ur : ir);
+            if (sub == 0) atomicAdd(a.hot_bias_grad + row, dz);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------- apply
+struct ApplyArgs {
+    const float *w_in[2], *b_in[2];
+    float *w_out[2], *b_out[2];
+    float *w_m[2], *w_v[2], *b_m[2], *b_v[2];
+    int64_t num_users, num_items;
+    int32_t dim;
+    int64_t row_begin, row_end;   // unified rows: users [0, U), items [U, U + I)
+    int32_t *row_count;
+    const int2 *row_list;
+    float *hot_grad, *hot_bias_grad;
+    const int32_t *item_slot_off; // plan: item i's partial slots [off[i], off[i+1])
+    const float *part_row, *part_bias;
+    rg_opt_t opt;
+    const float *partials;
+    int64_t n_partials;
+    double inv_a, inv_b;
+    float *loss_out;
+    float *grad;                  // flat [(re-rb)*D | (re-rb) | loss] (kGradOnly / kApplyDense)
+};
+
+// mf_apply modes: pull the gradient from the lists and update (single GPU);
+// pull into the flat dense gradient (before an all-reduce);
+// update from the (all-reduced) flat gradient.
+enum ApplyMode : int { kApplyPull = 0, kGradOnly = 1, kApplyDense = 2 };
+
+// torch.optim single-tensor update of one element, in the rounding torch's CPU
+// kernels use (checked on the reference's AVX-512 build): add(alpha) and addcmul
+// fuse their final multiply-add (FMA), addcdiv rounds (value * t1) / t2 then adds,
+// lerp(w = 1 - beta1) takes ATen's two-branch form.  g is the data gradient.
+__device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gdata, float &m, float &v) {
+    const float g = fmaf(o.weight_decay, p, gdata);         // grad.add(param, alpha=wd)
+    if (o.kind == RG_OPT_ADAM) {
+        const float w = o.one_minus_beta1;                  // exp_avg.lerp_(grad, 1 - beta1)
+        m = (fabsf(w) < 0.5f) ? fmaf(w, g - m, m) : fmaf(w - 1.0f, g - m, g);
+        v = fmaf(o.one_minus_beta2 * g, g, v * o.beta2);   // mul_(beta2).addcmul_(g, g, 1 - beta2)
+        const float denom = sqrtf(v) / o.bias_correction2_sqrt + o.eps;
+        return p + ((-o.step_size) * m) / denom;           // addcdiv_(m, denom, -step_size)
+    }
+    if (o.kind == RG_OPT_SGD) return fmaf(-o.lr, g, p);     // add_(g, alpha=-lr)
+    v = fmaf(o.one_minus_alpha * g, g, v * o.alpha);        // RMSprop (centered = False)
+    return p + ((-o.lr) * g) / (sqrtf(v) + o.eps);
+}
+
+// Streams every row of [row_begin, row_end) once (item rows first, so the few
+// long Zipf-hot item rows start early instead of trailing the grid).
+template <class L, int MODE>
+__global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
+    constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t k = wave * UPW + (lane / LPU);
+    const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
+    const int D = a.dim;
+
+    if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
+        double sa = 0.0, sb = 0.0;
+        for (int64_t i = lane; i < a.n_partials; i += kWave) {
+            sa += (double)a.partials[2 * i];
+            sb += (double)a.partials[2 * i + 1];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            sa += __shfl_xor(sa, off);
+            sb += __shfl_xor(sb, off);
+        }
+        if (lane == 0) {
+            const float lv = (float)(sa * a.inv_a + sb * a.inv_b);
+            *a.loss_out = lv;
+            if (MODE == kGradOnly) a.grad[nr * (int64_t)(D + 1)] = lv;
+        }
+    }
+    if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+        *a.loss_out = a.grad[nr * (int64_t)(D + 1)];
+
+    if (k >= nr) return;
+    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item part [ia0, re)
+    const int64_t ni = re > ia0 ? re - ia0 : 0;
+    const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
+    const int t = r < a.num_users ? 0 : 1;          // 0: user table, 1: item table
+    const int64_t lr_ = t ? r - a.num_users : r;
+    const int64_t gk = r - rb;                      // index in the flat gradient
+    const bool adam = a.opt.kind == RG_OPT_ADAM;
+    const bool has_v = a.opt.kind != RG_OPT_SGD;
+
+    float p[EPL], m[EPL], v[EPL], g[EPL];
+    float pb = 0.0f, mb = 0.0f, vb = 0.0f;
+    if (MODE != kGradOnly) {
+        L::load(p, a.w_in[t], lr_, D, sub);
+        if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
+        if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+        if (sub == 0) {
+            pb = a.b_in[t][lr_];
+            if (adam) mb = a.b_m[t][lr_];
+            if (has_v) vb = a.b_v[t][lr_];
+        }
+    }
+    L::zero(g);
+    float gb = 0.0f;
+
+    if (MODE == kApplyDense) {
+        L::load(g, a.grad, gk, D, sub);
+        if (sub == 0) gb = a.grad[nr * (int64_t)D + gk];
+    } else {
+        const int c = a.row_count[r];
+        if (c > 0) {
+            const int ne = c < kCap ? c : kCap;
+            int2 ent[kCap];
+#pragma unroll
+            for (int e = 0; e < kCap; ++e) ent[e] = e < ne ? a.row_list[r * kCap + e] : make_int2(0, 0);
+            const float *other = a.w_in[t ^ 1];
+            float o[kCap][EPL];
+#pragma unroll
+            for (int e = 0; e < kCap; ++e) {
+                if (e < ne) L::load(o[e], other, ent[e].x, D, sub); else L::zero(o[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < kCap; ++e) {
+                if (e < ne) {
+                    const float dz = __int_as_float(ent[e].y);
+#pragma unroll
+                    for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
+                    gb += dz;
+                }
+            }
+            if (c > kCap) {
+                float h[EPL];
+                L::load(h, a.hot_grad, r, D, sub);
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) g[q] += h[q];
+                L::zero(h);
+                L::store(a.hot_grad, r, D, sub, h);
+                if (sub == 0) {
+                    gb += a.hot_bias_grad[r];
+                    a.hot_bias_grad[r] = 0.0f;
+                }
+            }
+            if (sub == 0) a.row_count[r] = 0;
+        }
+        if (t == 1 && a.item_slot_off != nullptr) {   // planned positive partials of this item
+            const int s0 = a.item_slot_off[lr_], s1 = a.item_slot_off[lr_ + 1];
+            for (int sl = s0; sl < s1; sl += 4) {
+                float h[4][EPL];
+                float hb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int ss = sl + u < s1 ? sl + u : s0;
+                    L::load(h[u], a.part_row, ss, D, sub);
+                    hb[u] = a.part_bias[ss];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (sl + u < s1) {
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q) g[q] += h[u][q];
+                        gb += hb[u];
+                    }
+                }
+            }
+        }
+        if (MODE == kGradOnly) {
+            L::store(a.grad, gk, D, sub, g);
+            if (sub == 0) a.grad[nr * (int64_t)D + gk] = gb;
+            return;
+        }
+    }
+
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
+    L::store(a.w_out[t], lr_, D, sub, p);
+    if (adam) L::store(a.w_m[t], lr_, D, sub, m);
+    if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
+    if (sub == 0) {
+        pb = opt_update(a.opt, pb, gb, mb, vb);
+        a.b_out[t][lr_] = pb;
+        if (adam) a.b_m[t][lr_] = mb;
+        if (has_v) a.b_v[t][lr_] = vb;
+    }
+}
+
+// ---------------------------------------------------------------------------- scores / loss
+template <class L>
+__global__ __launch_bounds__(kBlock) void mf_scores_kernel(const float *__restrict__ uw, const float *__restrict__ iw,
+                                                           const float *__restrict__ ub, const float *__restrict__ ib,
+                                                           int D, const int64_t *__restrict__ users,
+                                                           const int64_t *__restrict__ items, int64_t n,
+                                                           float *__restrict__ out) {
+    constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t k = wave * UPW + (lane / LPU);
+    float ur[EPL], ir[EPL];
+    L::zero(ur);
+    L::zero(ir);
+    int64_t u = 0, i = 0;
+    if (k < n) {
+        u = users[k];
+        i = items[k];
+        L::load(ur, uw, u, D, sub);
+        L::load(ir, iw, i, D, sub);
+    }
+    float d = 0.0f;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) d = fmaf(ur[e], ir[e], d);
+    d = group_sum<LPU>(d);      // all lanes converged here (DPP)
+    if (k < n && sub == 0) out[k] = sigmoidf_ref((d + ub[u]) + ib[i]);
+}
+
+__global__ __launch_bounds__(kWave) void loss_finalize_kernel(const float *__restrict__ partials, int64_t np_,
+                                                              double inv_a, double inv_b, float *out) {
+    double sa = 0.0, sb = 0.0;
+    for (int64_t i = threadIdx.x; i < np_; i += kWave) {
+        sa += (double)partials[2 * i];
+        sb += (double)partials[2 * i + 1];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sa += __shfl_xor(sa, off);
+        sb += __shfl_xor(sb, off);
+    }
+    if (threadIdx.x == 0) *out = (float)(sa * inv_a + sb * inv_b);
+}
+
+template <class L>
+int64_t pairs_blocks(int64_t cols) {
+    constexpr int64_t UPB = kBlock / L::LPU;
+    return (cols + UPB - 1) / UPB;
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+namespace {
+struct PartialsLenF {
+    int64_t cols;
+    int64_t *nb;
+    template <class L>
+    int operator()() { *nb = pairs_blocks<L>(cols); return 0; }
+};
+
+struct UnitsPerBlockF {
+    int64_t *upb;
+    template <class L>
+    int operator()() { *upb = kBlock / L::LPU; return 0; }
+};
+
+struct PairsLaunchF {
+    PairsArgs *a;
+    hipStream_t s;
+    bool adaptive, backward;
+    template <class L>
+    int operator()() {
+        if (a->n_neg <= 5) return run<L, 5>();
+        return run<L, kNMax>();
+    }
+    template <class L, int NMAX>
+    int run() {
+        const int64_t nb = pairs_blocks<L>(a->cols);
+        if (!adaptive) {
+            if (backward)
+                hipLaunchKernelGGL((mf_pairs_kernel<L, kFused, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+            else
+                hipLaunchKernelGGL((mf_pairs_kernel<L, kLossOnly, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+            return check_launch("rg_mf_pairs");
+        }
+        if (hipMemsetAsync(a->max_key, 0, sizeof(unsigned long long), s) != hipSuccess ||
+            hipMemsetAsync(a->active_count, 0, sizeof(int32_t), s) != hipSuccess)
+            return check_launch("rg_mf_pairs(adaptive memset)");
+        hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptFwd, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+        if (backward) {
+            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptBwd, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+            hipLaunchKernelGGL((mf_adapt_max_kernel<L>), dim3(1), dim3(kWave), 0, s, *a);
+        } else {
+            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptLoss, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+        }
+        return check_launch("rg_mf_pairs(adaptive)");
+    }
+};
+
+struct ApplyLaunchF {
+    ApplyArgs *a;
+    hipStream_t s;
+    int mode;
+    template <class L>
+    int operator()() {
+        const int64_t rows = a->row_end - a->row_begin;
+        if (rows <= 0 && a->loss_out == nullptr) return RG_OK;
+        const int64_t waves = (rows + L::UPW - 1) / L::UPW;
+        int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+        if (nb < 1) nb = 1;
+        if (mode == kApplyPull)
+            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull>), dim3(nb), dim3(kBlock), 0, s, *a);
+        else if (mode == kGradOnly)
+            hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly>), dim3(nb), dim3(kBlock), 0, s, *a);
+        else
+            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyDense>), dim3(nb), dim3(kBlock), 0, s, *a);
+        return check_launch("rg_mf_apply");
+    }
+};
+
+struct ScoresLaunchF {
+    const float *uw, *iw, *ub, *ib;
+    int dim;
+    const int64_t *users, *items;
+    int64_t n;
+    float *out;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        const int64_t waves = (n + L::UPW - 1) / L::UPW;
+        const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+        hipLaunchKernelGGL((mf_scores_kernel<L>), dim3(nb), dim3(kBlock), 0, s, uw, iw, ub, ib, dim, users, items,
+                           n, out);
+        return check_launch("rg_mf_scores");
+    }
+};
+}  // namespace
+
+extern "C" int64_t rg_mf_partials_len(int64_t cols, int32_t dim) {
+    int64_t nb = -1;
+    PartialsLenF f{cols, &nb};
+    if (dispatch_dim(dim, f) != 0) return -1;
+    return 2 * nb;
+}
+
+extern "C" int64_t rg_mf_plan_units_per_block(int32_t dim) {
+    int64_t upb = -1;
+    UnitsPerBlockF f{&upb};
+    if (dispatch_dim(dim, f) != 0) return -1;
+    return upb;
+}
+
+static int check_tables(const rg_mf_tables_t *t) {
+    if (t == nullptr) return fail_arg("null tables");
+    if (!t->user_w || !t->item_w || !t->user_b || !t->item_b) return fail_arg("null parameter table");
+    if (t->num_users <= 0 || t->num_items <= 0) return fail_arg("empty table");
+    if (t->num_users + t->num_items >= (int64_t)1 << 31) return fail_arg("num_users + num_items must be < 2^31");
+    if (t->dim < 1 || t->dim > 256) return fail_arg("dim must be in [1, 256]");
+    return RG_OK;
+}
+
+extern "C" int rg_mf_pairs(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *b, rg_mf_work_t *w,
+                           int32_t backward) {
+    int rc = check_tables(t);
+    if (rc) return rc;
+    if (b == nullptr || w == nullptr) return fail_arg("rg_mf_pairs: null batch/work");
+    if (b->n_neg < 1 || b->n_neg > kNMax) return fail_arg("rg_mf_pairs: n_neg must be in [1, 8]");
+    if (b->cols <= 0 || b->n_pos < 0 || b->n_pos > b->cols) return fail_arg("rg_mf_pairs: bad n_pos/cols");
+    if (b->col_offset < 0 || b->col_offset + b->cols > b->global_cols) return fail_arg("rg_mf_pairs: bad column slice");
+    if (b->global_pos <= 0 && b->loss != RG_LOSS_POINTWISE) return fail_arg("rg_mf_pairs: empty global batch");
+    if (b->pool_len <= 0 || !b->pool || !b->words) return fail_arg("rg_mf_pairs: empty pool / no words");
+    if (b->n_pos > 0 && (!b->pos_user || !b->pos_item)) return fail_arg("rg_mf_pairs: null positives");
+    if (b->loss < 0 || b->loss > RG_LOSS_ADAPTIVE_HINGE) return fail_arg("rg_mf_pairs: bad loss kind");
+    if (!w->loss_partials) return fail_arg("rg_mf_pairs: null loss_partials");
+    if (backward && (!w->row_count || !w->row_list || !w->hot_grad || !w->hot_bias_grad))
+        return fail_arg("rg_mf_pairs: null backward scratch");
+    const bool adaptive = b->loss == RG_LOSS_ADAPTIVE_HINGE;
+    if (adaptive && (!w->scores || !w->max_key || !w->active_count))
+        return fail_arg("rg_mf_pairs: adaptive hinge needs scores/max_key/active_count");
+    if (w->plan_perm && (!w->plan_pos_slot || !w->part_row || !w->part_bias || !w->plan_item_slot_off))
+        return fail_arg("rg_mf_pairs: incomplete plan");
+
+    PairsArgs a{};
+    a.user_w = t->user_w; a.item_w = t->item_w; a.user_b = t->user_b; a.item_b = t->item_b;
+    a.num_users = t->num_users; a.dim = t->dim;
+    a.pos_user = b->pos_user; a.pos_item = b->pos_item;
+    a.n_pos = b->n_pos; a.cols = b->cols; a.col_offset = b->col_offset; a.global_cols = b->global_cols;
+    a.words = reinterpret_cast<const uint2 *>(b->words);
+    a.pool = reinterpret_cast<const int2 *>(b->pool);
+    a.pool_len = b->pool_len; a.n_neg = b->n_neg; a.loss = b->loss;
+    switch (b->loss) {
+        case RG_LOSS_POINTWISE:
+            a.n_a = (float)b->global_pos;
+            a.n_b = (float)((int64_t)b->n_neg * b->global_cols);
+            break;
+        case RG_LOSS_BPR:
+        case RG_LOSS_HINGE:
+            a.n_a = (float)((int64_t)b->n_neg * b->global_pos);
+            a.n_b = 1.0f;
+            break;
+        default:
+            a.n_a = (float)b->global_pos;
+            a.n_b = 1.0f;
+    }
+    a.row_count = w->row_count;
+    a.row_list = reinterpret_cast<int2 *>(w->row_list);
+    a.hot_grad = w->hot_grad; a.hot_bias_grad = w->hot_bias_grad;
+    a.partials = w->loss_partials; a.scores = w->scores;
+    a.max_key = reinterpret_cast<unsigned long long *>(w->max_key);
+    a.active_count = w->active_count;
+    if (!b->pairs) return fail_arg("rg_mf_pairs: batch->pairs not prepared (rg_mf_prepare)");
+    a.pairs = reinterpret_cast<const int2 *>(b->pairs);
+    a.perm = w->plan_perm;
+    a.pos_slot = backward ? w->plan_pos_slot : nullptr;   // partials only in the backward pass
+    a.part_row = w->part_row; a.part_bias = w->part_bias;
+    PairsLaunchF f{&a, (hipStream_t)stream, adaptive, backward != 0};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_prepare(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w) {
+    if (!b || !b->pairs) return fail_arg("rg_mf_prepare: null batch/pairs");
+    if (b->n_neg < 1 || b->n_neg > kNMax) return fail_arg("rg_mf_prepare: n_neg must be in [1, 8]");
+    if (b->cols <= 0 || b->n_pos < 0 || b->n_pos > b->cols) return fail_arg("rg_mf_prepare: bad n_pos/cols");
+    if (b->col_offset < 0 || b->col_offset + b->cols > b->global_cols) return fail_arg("rg_mf_prepare: bad slice");
+    if (b->pool_len <= 0 || !b->pool || !b->words) return fail_arg("rg_mf_prepare: empty pool / no words");
+    if (b->n_pos > 0 && (!b->pos_user || !b->pos_item)) return fail_arg("rg_mf_prepare: null positives");
+    PairsArgs a{};
+    a.pos_user = b->pos_user; a.pos_item = b->pos_item;
+    a.n_pos = b->n_pos; a.cols = b->cols; a.col_offset = b->col_offset; a.global_cols = b->global_cols;
+    a.words = reinterpret_cast<const uint2 *>(b->words);
+    a.pool = reinterpret_cast<const int2 *>(b->pool);
+    a.pool_len = b->pool_len; a.n_neg = b->n_neg;
+    a.perm = w ? w->plan_perm : nullptr;
+    const int64_t total = (int64_t)(1 + b->n_neg) * b->cols;
+    hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, reinterpret_cast<int2 *>(b->pairs));
+    return check_launch("rg_mf_prepare");
+}
+
+static int apply_common(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const float *grad_in,
+                        float *grad_out, const rg_opt_t *opt, int64_t row_begin, int64_t row_end,
+                        const rg_mf_loss_t *loss, float *dense_loss_out, int mode) {
+    int rc = check_tables(t);
+    if (rc) return rc;
+    const int64_t nrows = t->num_users + t->num_items;
+    if (row_begin < 0) row_begin = 0;
+    if (row_end < 0 || row_end > nrows) row_end = nrows;
+    if (row_begin > row_end) return fail_arg("rg_mf_apply: row_begin > row_end");
+    if (mode != kGradOnly) {
+        if (!opt) return fail_arg("rg_mf_apply: null opt");
+        if (!t->user_w_out || !t->item_w_out || !t->user_b_out || !t->item_b_out)
+            return fail_arg("rg_mf_apply: null output tables");
+        if (mode == kApplyPull && (t->user_w_out == t->user_w || t->item_w_out == t->item_w ||
+                                   t->user_b_out == t->user_b || t->item_b_out == t->item_b))
+            return fail_arg("rg_mf_apply: output tables must not alias the inputs (ping-pong)");
+        if (opt->kind < RG_OPT_ADAM || opt->kind > RG_OPT_RMSPROP) return fail_arg("rg_mf_apply: bad optimizer");
+        if (opt->kind == RG_OPT_ADAM && (!t->user_w_m || !t->item_w_m || !t->user_b_m || !t->item_b_m))
+            return fail_arg("rg_mf_apply: Adam needs m state");
+        if (opt->kind != RG_OPT_SGD && (!t->user_w_v || !t->item_w_v || !t->user_b_v || !t->item_b_v))
+            return fail_arg("rg_mf_apply: optimizer needs v state");
+    }
+    if (mode != kApplyDense) {
+        if (!w || !w->row_count || !w->row_list || !w->hot_grad || !w->hot_bias_grad)
+            return fail_arg("rg_mf_apply: null scratch");
+        if (loss && loss->out && !w->loss_partials) return fail_arg("rg_mf_apply: loss needs partials");
+    }
+    if (mode != kApplyPull && !(grad_in || grad_out)) return fail_arg("rg_mf_apply: null gradient buffer");
+    ApplyArgs a{};
+    a.w_in[0] = t->user_w; a.w_in[1] = t->item_w; a.b_in[0] = t->user_b; a.b_in[1] = t->item_b;
+    a.w_out[0] = t->user_w_out; a.w_out[1] = t->item_w_out; a.b_out[0] = t->user_b_out; a.b_out[1] = t->item_b_out;
+    a.w_m[0] = t->user_w_m; a.w_m[1] = t->item_w_m; a.w_v[0] = t->user_w_v; a.w_v[1] = t->item_w_v;
+    a.b_m[0] = t->user_b_m; a.b_m[1] = t->item_b_m; a.b_v[0] = t->user_b_v; a.b_v[1] = t->item_b_v;
+    a.num_users = t->num_users; a.num_items = t->num_items; a.dim = t->dim;
+    a.row_begin = row_begin; a.row_end = row_end;
+    if (w) {
+        a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
+        a.hot_grad = w->hot_grad; a.hot_bias_grad = w->hot_bias_grad;
+        a.partials = w->loss_partials;
+        if (w->plan_perm) {
+            a.item_slot_off = w->plan_item_slot_off;
+            a.part_row = w->part_row; a.part_bias = w->part_bias;
+        }
+    }
+    if (opt) a.opt = *opt;
+    if (mode == kApplyDense) {
+        a.loss_out = dense_loss_out;
+    } else if (loss) {
+        a.n_partials = loss->n_partials; a.inv_a = loss->inv_a; a.inv_b = loss->inv_b;
+        a.loss_out = loss->out;
+    }
+    a.grad = grad_out ? grad_out : const_cast<float *>(grad_in);
+    ApplyLaunchF f{&a, (hipStream_t)stream, mode};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_apply(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                           int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss) {
+    return apply_common(stream, t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull);
+}
+
+extern "C" int rg_mf_grads(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, float *grad_dev,
+                           int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss) {
+    if (!grad_dev) return fail_arg("rg_mf_grads: null grad");
+    return apply_common(stream, t, w, nullptr, grad_dev, nullptr, row_begin, row_end, loss, nullptr, kGradOnly);
+}
+
+extern "C" int rg_mf_apply_dense(void *stream, const rg_mf_tables_t *t, const float *grad_dev, const rg_opt_t *opt,
+                                 int64_t row_begin, int64_t row_end, float *loss_out_dev) {
+    if (!grad_dev) return fail_arg("rg_mf_apply_dense: null grad");
+    return apply_common(stream, t, nullptr, grad_dev, nullptr, opt, row_begin, row_end, nullptr, loss_out_dev,
+                        kApplyDense);
+}
+
+extern "C" int rg_loss_finalize(void *stream, const float *partials, int64_t n_partials, double inv_a,
+                                double inv_b, float *out) {
+    if (!partials || !out || n_partials < 0) return fail_arg("rg_loss_finalize: bad args");
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(kWave), 0, (hipStream_t)stream, partials, n_partials,
+                       inv_a, inv_b, out);
+    return check_launch("rg_loss_finalize");
+}
+
+extern "C" int rg_mf_scores(void *stream, const float *uw, const float *iw, const float *ub, const float *ib,
+                            int32_t dim, const int64_t *users, const int64_t *items, int64_t n, float *out) {
+    if (!uw || !iw || !ub || !ib || !users || !items || !out) return fail_arg("rg_mf_scores: null pointer");
+    if (n < 0) return fail_arg("rg_mf_scores: n < 0");
+    if (n == 0) return RG_OK;
+    ScoresLaunchF f{uw, iw, ub, ib, dim, users, items, n, out, (hipStream_t)stream};
+    return dispatch_dim(dim, f);
+}
