@@ -11,6 +11,12 @@ coupled-L2 Adam update of every row of the four BilinearNet tables (the
 reference's semantics: implicit.py:347-364, spotlight/optimizers.py:10-16).
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
+With N > 1 ranks (one process per GPU) the step is user-sharded
+(recommendation_gans_amd/sharding.py): rank r owns users u % N == r (rows,
+optimizer state, positives, pool entries, its own MT stream), items are
+replicated and their gradient is all-reduced with RCCL inside the native step,
+overlapped with the user-shard update.
+
 Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
 max over ranks of the timed wall time.  `roofline` is for the dominant kernel
 (rg_mf_apply, the dense optimizer pass), timed with HIP events on the stream it
@@ -106,9 +112,9 @@ def main():
     torch.cuda.set_device(dev)
 
     from recommendation_gans_amd import build as rg_build
+    from recommendation_gans_amd import sharding
     from recommendation_gans_amd.mf_engine import MFEngine
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
-    from oracle import rng as orng  # noqa: F401  (state glue only; not on the timed path)
 
     if not os.path.exists(rg_build.LIB):
         rg_build.build()
@@ -120,43 +126,42 @@ def main():
     Iw = torch.empty(I, d).normal_(0, 1.0 / d)
     random.seed(0)
     mt = np.asarray(random.getstate()[1], dtype=np.uint32)
-    eng = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), data.pool_u, data.pool_i, mt, loss=args.loss,
-                   optimizer=args.optim, lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev,
-                   rank=rank, world_size=world, prefetch=not args.no_prefetch)
-    tu = torch.from_numpy(data.train_u).to(dev)
-    ti = torch.from_numpy(data.train_i).to(dev)
+    comm = None
+    if world > 1:
+        from recommendation_gans_amd.comm import RcclComm
+        comm = RcclComm(dev)
+    pool_u, pool_i = sharding.shard_pool(data.pool_u, data.pool_i, rank, world)
+    train_u, train_i = sharding.shard_interactions(data.train_u, data.train_i, rank, world)
+    U_local = sharding.num_local_users(U, rank, world)
+    eng = MFEngine(sharding.shard_rows(Uw, rank, world), Iw, torch.zeros(U_local), torch.zeros(I), pool_u, pool_i,
+                   sharding.rank_mt_state(mt, rank), loss=args.loss, optimizer=args.optim, lr=1e-3,
+                   weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, rank=rank, world_size=world,
+                   prefetch=not args.no_prefetch, comm=comm)
+    tu = torch.from_numpy(train_u).to(dev)
+    ti = torch.from_numpy(train_i).to(dev)
     gb = B * world
-    nbatches = len(data.train_u) // gb
+    nbatches = len(train_u) // B
     # per-batch plans: the epoch order is fixed for the whole fit (implicit.py:262), so
     # they are built once, before timing (like the reference's own data preparation)
     nplan = min(nbatches, args.warmup + args.steps)
-    plans = [eng.make_plan(ti[g * gb + rank * B:g * gb + rank * B + B]) for g in range(nplan)]
+    plans = [eng.make_plan(ti[g * B:g * B + B]) for g in range(nplan)]
 
     def batch(s):
         g = s % nbatches
-        lo = g * gb + rank * B
-        return tu[lo:lo + B], ti[lo:lo + B], plans[g % nplan]
+        return tu[g * B:g * B + B], ti[g * B:g * B + B], plans[g % nplan]
 
-    if world > 1:
-        def allreduce(t):
-            dist.all_reduce(t)
+    # step inputs (ids + plan pointers) built before timing; each call also hands the
+    # NEXT step's input to the native stepper, which generates its words ahead
+    inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + 1)]
 
-        def step(s, ev=None):
-            u, i, p = batch(s)
-            return eng.train_step_dp(u, i, gb, allreduce, plan=p)
-    else:
-        # step inputs (ids + plan pointers) built before timing; each call also hands the
-        # NEXT step's input to the native stepper, which generates its words ahead
-        inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + 1)]
-
-        def step(s, ev=None):
-            return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev)
+    def step(s, ev=None):
+        return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev)
 
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)] if world == 1 else None
+           for _ in range(args.steps)]
     if evs:   # torch creates the HIP event lazily on its first record
         for a, b_ in evs:
             a.record()
@@ -179,7 +184,9 @@ def main():
 
     if rank == 0:
         value = args.steps * B * world / el
-        gather, ids, adam = algorithmic_bytes(U, I, d, B, n)
+        # per rank: its user shard + every item go through the dense optimizer pass
+        gather, ids, adam = algorithmic_bytes(U_local, I, d, B, n)
+        user_adam = 6 * U_local * (4 * d + 4) if world > 1 else adam
         out = {"metric": METRIC, "value": value, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -197,13 +204,13 @@ def main():
             from recommendation_gans_amd import _lib
             ms = [_lib.elapsed_ms(a, b) for a, b in evs]
             avg = float(np.mean(ms)) * 1e-3
-            ach = adam / avg / 1e9
+            ach = user_adam / avg / 1e9
             out["roofline"] = {"bound": "hbm", "kernel": "rg_mf_apply (mf_apply_kernel)", "achieved": ach,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                               "traffic": None, "algorithmic_bytes_per_launch": adam,
+                               "traffic": None, "algorithmic_bytes_per_launch": user_adam,
                                "avg_launch_us": avg * 1e6}
             pmc = os.path.join(ROOT, "profiles", "pmc_apply.json")
-            if os.path.exists(pmc):
+            if world == 1 and os.path.exists(pmc):
                 p = json.load(open(pmc))
                 if p.get("dim") == d and p.get("batch") == B:
                     out["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
@@ -212,6 +219,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
+        del eng
+        comm.close()
         dist.destroy_process_group()
 
 

@@ -25,6 +25,10 @@
  *   rg_mf_scores        BilinearNet.forward (eval / predict)
  *                                                          implicit.py:368, :412
  *   rg_loss_finalize    loss.item() of run_val_iteration    implicit.py:366-379
+ *   rg_mf_stepper_*     the loop body of fit: one call per run_train_iteration
+ *                                                          implicit.py:290-298, :347-364
+ *   rg_comm_*           RCCL communicator of the user-sharded data-parallel step
+ *                       (the reference is single-device)
  */
 #ifndef RG_HIP_H
 #define RG_HIP_H
@@ -86,8 +90,9 @@ typedef struct rg_mf_batch {
     int64_t n_pos;          /* <= cols; < cols only on the last partial batch */
     int64_t cols;           /* this rank's columns (batch_size) */
     int64_t col_offset;     /* first global column owned by this rank */
-    int64_t global_cols;    /* batch_size * world_size */
+    int64_t global_cols;    /* columns of the draw this slice is cut from (batch_size [* world_size]) */
     int64_t global_pos;     /* positives in the whole (global) batch */
+    int64_t neg_cols;       /* negatives per draw row over every rank (mean denominator); 0: global_cols */
     const uint32_t *words;  /* raw MT19937 words of this step (rg_mt_generate): draw j uses [2j], [2j+1] */
     const int32_t *pool;    /* negative pool as int32 (user, item) pairs [pool_len] */
     int64_t pool_len;
@@ -202,10 +207,29 @@ int rg_mf_scores(void *stream, const float *user_w, const float *item_w,
                  const int64_t *users, const int64_t *items, int64_t n, float *out);
 
 /* ------------------------------------------------------------------------------
+ * RCCL communicator (rg_comm.cpp) for the user-sharded data-parallel step: one
+ * process per GPU; rank 0 makes the id, the caller broadcasts it (torch.distributed),
+ * every rank creates its communicator on `device`.
+ * ---------------------------------------------------------------------------- */
+#define RG_COMM_ID_BYTES 128
+int rg_comm_unique_id(uint8_t *out, int64_t len);
+void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, int32_t device);
+int rg_comm_destroy(void *comm);
+/* In-place sum over ranks, stream-ordered with respect to `stream` (runs on the
+ * communicator's own stream between two events). */
+int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf_dev, int64_t n);
+
+/* ------------------------------------------------------------------------------
  * Native step runtime (rg_stepper.cpp): one call per training step enqueues
  *   side stream:  rg_mt_generate + rg_mf_prepare of the NEXT step (generated ahead)
  *   main stream:  rg_mf_pairs -> rg_mf_apply of the current step
  * Replaces the loop body implicit.py:290-298 / run_train_iteration :347-364.
+ *
+ * User-sharded data parallelism (item_grad != NULL): this rank's tables hold its
+ * own users (rows [0, num_users)) and every item (replicated).  The step becomes
+ *   rg_mf_pairs -> rg_mf_grads(item rows -> item_grad) -> [comm: all-reduce on the
+ *   communicator stream] || rg_mf_apply(user rows) -> rg_mf_apply_dense(item rows)
+ * so the only exchange is the item gradient, overlapped with the user update.
  * ---------------------------------------------------------------------------- */
 typedef struct rg_mf_stepper_config {
     rg_mf_tables_t tables[2];       /* tables[k]: reads set k, writes set 1 - k */
@@ -216,7 +240,10 @@ typedef struct rg_mf_stepper_config {
     const int32_t *pool;
     int64_t pool_len;
     int32_t n_neg, loss;
-    int64_t cols, col_offset, global_cols;
+    int64_t cols, col_offset, global_cols;   /* draw layout: j = (q-1)*global_cols + col_offset + col */
+    int64_t neg_cols;               /* negatives per draw row over every rank (loss denominator) */
+    float *item_grad;               /* [num_items*(dim+1) + 1]: user-sharded DP step when non-null */
+    void *comm;                     /* rg_comm_create handle (NULL: single rank, no exchange) */
     rg_opt_t opt;                   /* kind + fp32 hyper-parameters */
     double lr_d, beta1_d, beta2_d;  /* the same as Python floats (Adam bias corrections) */
     int64_t step;                   /* optimizer steps already taken */

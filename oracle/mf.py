@@ -53,33 +53,41 @@ def scores(U, I, ub, ib, u, i):
 
 
 # ------------------------------------------------------------------ losses
-def loss_and_dp(kind, p_pos, p_neg, n, batch_size):
+def loss_and_dp(kind, p_pos, p_neg, n, batch_size, den=None):
     """Return (loss, dL/dp_pos, dL/dp_neg) for the loss selected by ``kind``.
 
     p_pos: (Bp,) positive scores (Bp <= batch_size on the last partial batch).
     p_neg: (n*batch_size,) negative scores, flat as drawn (implicit.py:352).
+    den:   None -> the reference's means over this batch.  (pos_den, neg_den) ->
+           sums divided by those counts instead: one rank's share of a loss whose
+           means run over the positives / negatives of every data-parallel rank.
     """
     Bp = p_pos.shape[0]
+    pos_den, neg_den = (Bp, p_neg.shape[0]) if den is None else den
     if kind == "pointwise":
-        lp = -torch.clamp(torch.log(p_pos), min=-100.0).mean()
-        ln = -torch.clamp(torch.log(1.0 - p_neg), min=-100.0).mean()
+        if den is None:
+            lp = -torch.clamp(torch.log(p_pos), min=-100.0).mean()
+            ln = -torch.clamp(torch.log(1.0 - p_neg), min=-100.0).mean()
+        else:
+            lp = -torch.clamp(torch.log(p_pos), min=-100.0).sum() / pos_den
+            ln = -torch.clamp(torch.log(1.0 - p_neg), min=-100.0).sum() / neg_den
         eps = 1e-12
-        dpp = (1.0 / Bp) * (p_pos - 1.0) / torch.clamp((1.0 - p_pos) * p_pos, min=eps)
-        dpn = (1.0 / p_neg.shape[0]) * (p_neg - 0.0) / torch.clamp((1.0 - p_neg) * p_neg, min=eps)
+        dpp = (1.0 / pos_den) * (p_pos - 1.0) / torch.clamp((1.0 - p_pos) * p_pos, min=eps)
+        dpn = (1.0 / neg_den) * (p_neg - 0.0) / torch.clamp((1.0 - p_neg) * p_neg, min=eps)
         return lp + ln, dpp, dpn
     if kind in ("bpr", "hinge"):
         negm = p_neg.view(n, batch_size)[:, :Bp]
-        g = 1.0 / (n * Bp)
+        g = 1.0 / (n * pos_den)
         dpn = torch.zeros(n, batch_size, dtype=p_pos.dtype)
         if kind == "bpr":
             s = torch.sigmoid(p_pos[None, :] - negm)
-            loss = (1.0 - s).mean()
+            loss = (1.0 - s).mean() if den is None else (1.0 - s).sum() * g
             dx = (-g) * (1.0 - s) * s          # d/dx of (1 - sigmoid(x)), x = pos - neg
             dpp = dx.sum(0)
             dpn[:, :Bp] = -dx
         else:
             x = negm - p_pos[None, :] + 1.0
-            loss = torch.clamp(x, min=0.0).mean()
+            loss = torch.clamp(x, min=0.0).mean() if den is None else torch.clamp(x, min=0.0).sum() * g
             dx = g * (x >= 0).to(p_pos.dtype)
             dpp = -dx.sum(0)
             dpn[:, :Bp] = dx
@@ -87,8 +95,8 @@ def loss_and_dp(kind, p_pos, p_neg, n, batch_size):
     if kind == "adaptive_hinge":
         m, idx = torch.max(p_neg, 0)
         x = m - p_pos + 1.0
-        loss = torch.clamp(x, min=0.0).mean()
-        dx = (1.0 / Bp) * (x >= 0).to(p_pos.dtype)
+        loss = torch.clamp(x, min=0.0).mean() if den is None else torch.clamp(x, min=0.0).sum() / pos_den
+        dx = (1.0 / pos_den) * (x >= 0).to(p_pos.dtype)
         dpn = torch.zeros_like(p_neg)
         dpn[int(idx)] = dx.sum()
         return loss, -dx, dpn
@@ -178,19 +186,25 @@ class MFOracle:
         t = torch.from_numpy(idx)
         return idx, self.pool_u[t], self.pool_i[t]
 
-    def step(self, pos_u, pos_i, return_all=False):
+    def step(self, pos_u, pos_i, return_all=False, den=None, exchange=None):
+        """``den``/``exchange``: the user-sharded data-parallel step (one rank's shard,
+        recommendation_gans_amd/sharding.py): loss means over every rank's positives
+        and negatives, and ``exchange(grads) -> grads`` (the item-gradient all-reduce)
+        between backward and the optimizer update."""
         U, I, ub, ib = self.params
         pos_u = torch.as_tensor(pos_u).long()
         pos_i = torch.as_tensor(pos_i).long()
         p_pos = scores(U, I, ub, ib, pos_u, pos_i)
         idx, nu, ni = self.draw(self.n * self.batch_size)
         p_neg = scores(U, I, ub, ib, nu, ni)
-        loss, dpp, dpn = loss_and_dp(self.loss_kind, p_pos, p_neg, self.n, self.batch_size)
+        loss, dpp, dpn = loss_and_dp(self.loss_kind, p_pos, p_neg, self.n, self.batch_size, den=den)
         dzp = dpp * (1.0 - p_pos) * p_pos
         dzn = dpn * (1.0 - p_neg) * p_neg
         u = torch.cat([pos_u, nu])
         i = torch.cat([pos_i, ni])
         grads = dense_grads(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
+        if exchange is not None:
+            grads = exchange(grads)
         self.opt.step(self.params, grads)
         if return_all:
             return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx,

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_PKG, "librg_hip.so")
 RG_OK = 0
 RG_MF_LIST_CAP = 8
 RG_MF_MAX_NEG = 8
+RG_COMM_ID_BYTES = 128
 RG_MT_PAD = 1280
 
 LOSS_KINDS = {"pointwise": 0, "bpr": 1, "hinge": 2, "adaptive_hinge": 3}
@@ -41,7 +42,7 @@ class MFTables(ctypes.Structure):
 class MFBatch(ctypes.Structure):
     _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p),
                 ("n_pos", ctypes.c_int64), ("cols", ctypes.c_int64), ("col_offset", ctypes.c_int64),
-                ("global_cols", ctypes.c_int64), ("global_pos", ctypes.c_int64),
+                ("global_cols", ctypes.c_int64), ("global_pos", ctypes.c_int64), ("neg_cols", ctypes.c_int64),
                 ("words", ctypes.c_void_p), ("pool", ctypes.c_void_p), ("pool_len", ctypes.c_int64),
                 ("n_neg", ctypes.c_int32), ("loss", ctypes.c_int32), ("pairs", ctypes.c_void_p)]
 
@@ -72,7 +73,8 @@ class MFStepperConfig(ctypes.Structure):
                 ("mt_state_before", ctypes.c_void_p), ("words", ctypes.c_void_p * 2), ("pairs", ctypes.c_void_p * 2),
                 ("pool", ctypes.c_void_p), ("pool_len", ctypes.c_int64), ("n_neg", ctypes.c_int32),
                 ("loss", ctypes.c_int32), ("cols", ctypes.c_int64), ("col_offset", ctypes.c_int64),
-                ("global_cols", ctypes.c_int64), ("opt", Opt), ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double),
+                ("global_cols", ctypes.c_int64), ("neg_cols", ctypes.c_int64), ("item_grad", ctypes.c_void_p),
+                ("comm", ctypes.c_void_p), ("opt", Opt), ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double),
                 ("beta2_d", ctypes.c_double), ("step", ctypes.c_int64), ("n_partials", ctypes.c_int64),
                 ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
@@ -85,6 +87,10 @@ class MFStepIn(ctypes.Structure):
 
 # (name, restype, argtypes) for every symbol declared in include/rg_hip.h
 SIGNATURES = [
+    ("rg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("rg_comm_create", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("rg_comm_allreduce_sum_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     ("rg_mt_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_void_p]),
     ("rg_mf_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),

@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librg_hip.so")
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp"]
+SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp"]
 HEADERS = ["rg_common.h"]
 
 
@@ -71,7 +71,10 @@ def build(force=False, verbose=False, jobs=8):
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(f"--- {s}\n{o}" for s, o in failed))
     tmp = LIB + ".tmp"
-    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
+    # librccl.so.1 by SONAME: inside a process that imported torch it binds to the
+    # RCCL torch already loaded (same library torch.distributed's "nccl" backend uses)
+    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + \
+        ["-L/opt/rocm/lib", "-lrccl"]
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
     return LIB

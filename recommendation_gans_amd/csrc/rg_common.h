@@ -14,6 +14,9 @@ constexpr int kWave = 64;
 void set_error(const std::string &msg);
 int fail_arg(const std::string &msg);
 int check_launch(const char *what);
+// rg_comm.cpp: all-reduce of buf on the communicator stream, fenced against `stream`
+int comm_begin(void *comm, hipStream_t stream, float *buf, int64_t n);
+int comm_end(void *comm, hipStream_t stream);
 
 // ---------------------------------------------------------------- DPP
 // Cross-lane moves inside a 16-lane DPP row (no LDS traffic, all lanes valid).

@@ -766,7 +766,7 @@ extern "C" int rg_mf_pairs(void *stream, const rg_mf_tables_t *t, const rg_mf_ba
     switch (b->loss) {
         case RG_LOSS_POINTWISE:
             a.n_a = (float)b->global_pos;
-            a.n_b = (float)((int64_t)b->n_neg * b->global_cols);
+            a.n_b = (float)((int64_t)b->n_neg * (b->neg_cols > 0 ? b->neg_cols : b->global_cols));
             break;
         case RG_LOSS_BPR:
         case RG_LOSS_HINGE:

@@ -48,6 +48,7 @@ rg_mf_batch_t make_batch(const Stepper &st, const rg_mf_step_in_t &in, int b) {
     x.col_offset = st.cfg.col_offset;
     x.global_cols = st.cfg.global_cols;
     x.global_pos = in.global_pos;
+    x.neg_cols = st.cfg.neg_cols;
     x.words = st.cfg.words[b];
     x.pool = st.cfg.pool;
     x.pool_len = st.cfg.pool_len;
@@ -125,7 +126,7 @@ rg_mf_loss_t loss_of(const Stepper &st, int64_t global_pos, float *out) {
     l.n_partials = st.cfg.n_partials;
     l.out = out;
     const double n = (double)st.cfg.n_neg;
-    const double gp = (double)global_pos, gc = (double)st.cfg.global_cols;
+    const double gp = (double)global_pos, gc = (double)st.cfg.neg_cols;
     switch (st.cfg.loss) {
         case RG_LOSS_POINTWISE: l.inv_a = 1.0 / gp; l.inv_b = 1.0 / (n * gc); break;
         case RG_LOSS_BPR:
@@ -163,6 +164,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->cfg = *cfg;
     st->set = cfg->current_set;
     st->words_per_step = 2 * (int64_t)cfg->n_neg * cfg->global_cols;
+    if (st->cfg.neg_cols <= 0) st->cfg.neg_cols = cfg->global_cols;
     hipError_t e = hipStreamCreateWithFlags(&st->side, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 2; ++i) {
         e = hipEventCreateWithFlags(&st->ready[i], hipEventDisableTiming);
@@ -213,12 +215,27 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
     const rg_opt_t o = opt_at(*st, st->cfg.step);
     const rg_mf_loss_t l = loss_of(*st, cur->global_pos, loss_out);
     hipError_t e;
+    const rg_mf_tables_t *tb = &st->cfg.tables[st->set];
+    const int64_t U = tb->num_users, R = tb->num_users + tb->num_items;
+    if (st->cfg.item_grad) {                     // user-sharded data parallel
+        if ((rc = rg_mf_grads(s, tb, &w, st->cfg.item_grad, U, R, &l))) return rc;
+        if (st->cfg.comm && (rc = rg::comm_begin(st->cfg.comm, s, st->cfg.item_grad,
+                                                 tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+            return rc;
+    }
     if (ev_apply_begin && (e = hipEventRecord((hipEvent_t)ev_apply_begin, s)) != hipSuccess)
         return hip_fail("stepper: record event", e);
-    rc = rg_mf_apply(s, &st->cfg.tables[st->set], &w, &o, 0, -1, &l);
-    if (rc) return rc;
+    if (st->cfg.item_grad) {
+        if ((rc = rg_mf_apply(s, tb, &w, &o, 0, U, nullptr))) return rc;
+    } else {
+        if ((rc = rg_mf_apply(s, tb, &w, &o, 0, -1, &l))) return rc;
+    }
     if (ev_apply_end && (e = hipEventRecord((hipEvent_t)ev_apply_end, s)) != hipSuccess)
         return hip_fail("stepper: record event", e);
+    if (st->cfg.item_grad) {
+        if (st->cfg.comm && (rc = rg::comm_end(st->cfg.comm, s))) return rc;
+        if ((rc = rg_mf_apply_dense(s, tb, st->cfg.item_grad, &o, U, R, loss_out))) return rc;
+    }
     st->set = 1 - st->set;
     return RG_OK;
 }

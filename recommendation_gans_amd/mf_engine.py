@@ -151,7 +151,15 @@ class MFEngine:
 
     def __init__(self, user_w, item_w, user_b, item_b, pool_u, pool_i, mt_state, *, loss="pointwise",
                  optimizer="adam", lr=1e-3, weight_decay=0.0, betas=(0.5, 0.999), eps=1e-8, alpha=0.99,
-                 n_neg=5, batch_size=256, device="cuda", rank=0, world_size=1, prefetch=True):
+                 n_neg=5, batch_size=256, device="cuda", rank=0, world_size=1, prefetch=True,
+                 dp=None, comm=None):
+        """``dp``: data-parallel layout when world_size > 1 --
+        "user_shard" (default): the tables passed are this rank's user shard plus every
+            item (sharding.py); own MT stream, local draw layout, the item gradient is
+            the only exchange (``comm``: an RcclComm, else ``train_step_sharded``);
+        "global_stream": replicated tables, every rank draws its slice of one global
+            stream (rank r takes columns [r*B, (r+1)*B) of the global batch's draw),
+            the full flat gradient is exchanged (``train_step_dp``)."""
         _lib.require_gpu()
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
@@ -159,6 +167,9 @@ class MFEngine:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         if not 1 <= n_neg <= RG_MF_MAX_NEG:
             raise ValueError(f"num_negative_samples must be in [1, {RG_MF_MAX_NEG}] for the fused kernel")
+        dp = dp or ("user_shard" if world_size > 1 or comm is not None else None)
+        if dp not in (None, "user_shard", "global_stream"):
+            raise ValueError(f"unknown data-parallel layout {dp!r}")
         if loss == "adaptive_hinge" and world_size != 1:
             raise NotImplementedError("adaptive_hinge is implemented for world_size 1")
         self.lib = _lib.load()
@@ -194,7 +205,13 @@ class MFEngine:
         self.n_neg = int(n_neg)
         self.batch_size = int(batch_size)
         self.rank, self.world = int(rank), int(world_size)
-        self.global_cols = self.batch_size * self.world
+        self.dp = dp
+        self.comm = comm
+        if dp == "global_stream":
+            self.col_offset, self.global_cols = self.rank * self.batch_size, self.batch_size * self.world
+        else:
+            self.col_offset, self.global_cols = 0, self.batch_size
+        self.neg_cols = self.batch_size * self.world
         self.words_per_step = 2 * self.n_neg * self.global_cols
         self.prefetch = prefetch
         rows = self.U + self.I
@@ -212,6 +229,7 @@ class MFEngine:
         self.part_bias = torch.zeros(self.batch_size, **f32)
         self.units_per_block = int(self.lib.rg_mf_plan_units_per_block(self.dim))
         self.grad_buf = None
+        self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
         self.mt_buf = _as_u32_tensor(mt_state, dev)
         self.mt_before = torch.zeros(625, dtype=torch.int32, device=dev)
         self.words = [torch.zeros(self.words_per_step + RG_MT_PAD, dtype=torch.int32, device=dev)
@@ -231,7 +249,10 @@ class MFEngine:
         cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
         cfg.pool, cfg.pool_len = ptr(self.pool), self.pool_len
         cfg.n_neg, cfg.loss = self.n_neg, LOSS_KINDS[loss]
-        cfg.cols, cfg.col_offset, cfg.global_cols = self.batch_size, self.rank * self.batch_size, self.global_cols
+        cfg.cols, cfg.col_offset, cfg.global_cols = self.batch_size, self.col_offset, self.global_cols
+        cfg.neg_cols = self.neg_cols
+        cfg.item_grad = ptr(self.item_grad)
+        cfg.comm = comm.handle if comm is not None else None
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
         cfg.step, cfg.n_partials, cfg.current_set = 0, self.n_partials, 0
@@ -288,7 +309,7 @@ class MFEngine:
         return self.tabs[self.cur]
 
     def loss_scales(self, global_pos):
-        n, gc = self.n_neg, self.global_cols
+        n, gc = self.n_neg, self.neg_cols
         if self.loss == "pointwise":
             return 1.0 / global_pos, 1.0 / (n * gc)
         if self.loss in ("bpr", "hinge"):
@@ -332,6 +353,10 @@ class MFEngine:
         return self.train_step_in(cur, next_input if self.prefetch else None, apply_events)
 
     def train_step_in(self, cur, next_input=None, apply_events=None):
+        if self.dp == "user_shard" and self.world > 1 and self.comm is None:
+            raise RuntimeError("user-sharded step over several ranks needs an RcclComm (or train_step_sharded)")
+        if self.dp == "global_stream" and self.world > 1:
+            raise RuntimeError("dp='global_stream' steps go through train_step_dp")
         ev0 = ev1 = None
         if apply_events is not None:
             ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
@@ -416,6 +441,20 @@ class MFEngine:
         g = self.grads(pos_u, pos_i, global_pos, plan=plan)
         allreduce(g)
         return self.apply_dense(g)
+
+    def train_step_sharded(self, pos_u, pos_i, global_pos, allreduce, plan=None):
+        """The user-sharded step with the item-gradient exchange done by ``allreduce``
+        (in-place sum, e.g. torch.distributed over gloo in tests): what
+        rg_mf_stepper_train does natively with an RCCL communicator."""
+        if self.dp != "user_shard":
+            raise RuntimeError("train_step_sharded needs dp='user_shard'")
+        self.pairs_and_lists(pos_u, pos_i, global_pos, plan)
+        g = self.pull_grads(self.U, self.U + self.I)
+        allreduce(g)
+        self.apply_rows(0, self.U, loss=False)
+        self.apply_dense_rows(g, self.U, self.U + self.I)
+        self.finish_step()
+        return self.loss_out
 
     def val_loss(self, pos_u, pos_i, global_pos=None):
         """run_val_iteration (implicit.py:366): forward + loss on the same draw stream, no update."""

@@ -306,12 +306,38 @@ def test_mf_dense_update_path(dev, loss):
             close_norm(e.v[k], o.opt.state[k][1].reshape(e.v[k].shape), what=f"dense step {s} v{k}")
 
 
-@pytest.mark.parametrize("opt", ["adam", "sgd", "rms"])
+def _torch_formula_step(opt, p, gr, m, v, t, lr, wd, cr_sqrt, betas=(0.5, 0.999), alpha=0.99, eps=1e-8):
+    """torch.optim's single-tensor update written out op by op (torch/optim/adam.py,
+    rmsprop.py, sgd.py), CPU tensor ops so each op keeps torch's own rounding; with
+    cr_sqrt the sqrt is correctly rounded instead (ATen's CPU fp32 sqrt goes through
+    MKL VML, which is 1 ulp off for small inputs such as v ~ 1e-21)."""
+    sqrt = (lambda x: x.double().sqrt().float()) if cr_sqrt else torch.sqrt
+    g = gr.add(p, alpha=wd)
+    if opt == "sgd":
+        return p.add(g, alpha=-lr), m, v
+    if opt == "adam":
+        b1, b2 = betas
+        m = m.lerp(g, 1 - b1)
+        v = v.mul(b2).addcmul(g, g, value=1 - b2)
+        denom = (sqrt(v) / ((1 - b2 ** t) ** 0.5)).add(eps)
+        return p.addcdiv(m, denom, value=-(lr / (1 - b1 ** t))), m, v
+    v = v.mul(alpha).addcmul(g, g, value=1 - alpha)
+    return p.addcdiv(g, sqrt(v).add(eps), value=-lr), m, v
+
+
+def _ulps(a, b):
+    return np.abs(a.numpy().view(np.int32).astype(np.int64) - b.numpy().view(np.int32).astype(np.int64))
+
+
 @pytest.mark.parametrize("d", [64, 50])
+@pytest.mark.parametrize("opt", ["adam", "sgd", "rms"])
 def test_optimizer_update_matches_torch(dev, opt, d):
-    """Given the same gradient, rg_mf_apply_dense's update equals torch.optim's
-    single-tensor CPU update (the reference's optimizer) to ~1 ulp, over 3 steps with
-    evolving m/v, including elements with |g| ~ eps."""
+    """Given the same gradient, rg_mf_apply_dense's update is torch.optim's
+    single-tensor CPU update, over 3 steps with evolving m/v and elements with
+    |g| ~ eps.  Teacher-forced from the GPU's previous p/m/v, every element is within
+    1 ulp of torch's op sequence (with torch's sqrt or a correctly rounded one), p, m
+    and v; the trajectory stays within 2^-18 of the largest |p| + |update| each
+    element has seen of torch.optim itself."""
     from recommendation_gans_amd.mf_engine import MFEngine
     U, I = 120, 70
     g = torch.Generator().manual_seed(1)
@@ -323,21 +349,43 @@ def test_optimizer_update_matches_torch(dev, opt, d):
     topt = {"adam": lambda ps: torch.optim.Adam(ps, lr=1e-2, betas=(0.5, 0.999), weight_decay=1e-5),
             "sgd": lambda ps: torch.optim.SGD(ps, lr=1e-2, weight_decay=1e-5),
             "rms": lambda ps: torch.optim.RMSprop(ps, lr=1e-2, weight_decay=1e-5)}[opt](tparams)
+    hist = [p.abs() for p in params]      # largest |p| + |update| each element has seen
     for step in range(3):
         grads = [torch.randn(p.shape, generator=g) * 10 ** float(torch.randint(-9, -2, (1,), generator=g))
                  for p in params]
         grads[0][0, :5] = torch.tensor([1e-8, -1e-8, 3e-9, 0.0, -2e-8])     # |g| ~ eps
+        torch.cuda.synchronize()
+        state = lambda x, k: torch.zeros_like(params[k]) if x is None else x.cpu().reshape(params[k].shape).clone()
+        before = [(e.params()[k].cpu().clone(), state(e.m[k], k), state(e.v[k], k)) for k in range(4)]
         flat = torch.cat([grads[0].reshape(-1), grads[1].reshape(-1), grads[2], grads[3], torch.zeros(1)])
         e.apply_dense(flat.to(dev))
+        prev = [p.detach().clone() for p in tparams]
         for p, gr in zip(tparams, grads):
             p.grad = gr.clone()
         topt.step()
         torch.cuda.synchronize()
         for k in range(4):
-            # same rounding as torch's CPU kernels (FMA where they fuse): at most 1 ulp
-            got, ref = e.params()[k].cpu().numpy(), tparams[k].detach().numpy()
-            ulps = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+            got = e.params()[k].cpu()
+            p0, m0, v0 = before[k]
+            refs = [_torch_formula_step(opt, p0, grads[k], m0, v0, step + 1, lr=1e-2, wd=1e-5, cr_sqrt=cr)
+                    for cr in (False, True)]
+            ulps = np.minimum(_ulps(got, refs[0][0]), _ulps(got, refs[1][0]))
             assert ulps.max() <= 1, f"{opt} step {step} tensor {k}: {int((ulps > 0).sum())} differ, max {ulps.max()} ulp"
+            for name, dev_state, ref_state in (("m", e.m[k], refs[0][1]), ("v", e.v[k], refs[0][2])):
+                if dev_state is not None:
+                    su = _ulps(dev_state.cpu().reshape(ref_state.shape), ref_state)
+                    assert su.max() <= 1, f"{opt} step {step} tensor {k} {name}: max {su.max()} ulp"
+            tref = tparams[k].detach()
+            # an update that cancels p leaves the few-ulp error of the larger magnitudes
+            hist[k] = torch.maximum(hist[k], prev[k].abs() + (tref - prev[k]).abs())
+            scale = hist[k]
+            err = (got - tref).abs()
+            worst = int((err / scale).reshape(-1).argmax())
+            assert bool((err <= 2.0 ** -18 * scale).all()), \
+                (f"{opt} step {step} tensor {k}: vs torch.optim max err/scale {float((err / scale).max()):.3g} "
+                 f"at {worst}: got {float(got.reshape(-1)[worst])!r} torch {float(tref.reshape(-1)[worst])!r} "
+                 f"prev gpu {float(p0.reshape(-1)[worst])!r} prev torch {float(prev[k].reshape(-1)[worst])!r} "
+                 f"g {float(grads[k].reshape(-1)[worst])!r}")
 
 
 def test_scores_and_val_loss(dev):
