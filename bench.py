@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true")
+    ap.add_argument("--events-every", type=int, default=8,
+                    help="record the rg_mf_apply timing events on every k-th timed step")
     return ap.parse_args()
 
 
@@ -160,18 +162,20 @@ def main():
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
+    every = max(1, args.events_every)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    if evs:   # torch creates the HIP event lazily on its first record
-        for a, b_ in evs:
-            a.record()
-            b_.record()
+           if s % every == 0 else None for s in range(args.steps)]
+    for ev in evs:   # torch creates the HIP event lazily on its first record
+        if ev is not None:
+            ev[0].record()
+            ev[1].record()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(args.warmup + s, evs[s] if evs else None)
+        step(args.warmup + s, evs[s])
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -200,9 +204,10 @@ def main():
         out["step_roofline"] = {"bytes_per_step": step_bytes,
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
                                 "frac": step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS}
-        if evs:
+        out["host_enqueue_us_per_step"] = t_enq / args.steps * 1e6
+        if any(ev is not None for ev in evs):
             from recommendation_gans_amd import _lib
-            ms = [_lib.elapsed_ms(a, b) for a, b in evs]
+            ms = [_lib.elapsed_ms(a, b) for a, b in (ev for ev in evs if ev is not None)]
             avg = float(np.mean(ms)) * 1e-3
             ach = user_adam / avg / 1e9
             out["roofline"] = {"bound": "hbm", "kernel": "rg_mf_apply (mf_apply_kernel)", "achieved": ach,

@@ -159,6 +159,15 @@ typedef struct rg_opt {
 int rg_mt_generate(void *stream, uint32_t *state_dev, uint32_t *out_words_dev,
                    int64_t nwords, uint32_t *state_before_dev);
 
+/* Host reference of the MT19937 jump-ahead (rg_mtjump.cpp): the window-form state
+ * (x[D .. D+624), position 624) of the word stream x[] that starts at state_host's
+ * next word, computed as an XOR of stream windows with the coefficients of
+ * t^(D-1) mod chi(t).  D >= 1.  Host memory only. */
+int rg_mt_window_host(const uint32_t *state_host, int64_t D, uint32_t *window_out_host);
+/* Window-form state x[P-624 .. P) -> CPython's getstate() layout for the same stream
+ * position with position `pos` (1..624) inside its block.  Host memory only. */
+int rg_mt_window_to_cpython(const uint32_t *window_host, int32_t pos, uint32_t *state_out_host);
+
 /* Number of float loss partials rg_mf_pairs writes for `cols` columns. */
 int64_t rg_mf_partials_len(int64_t cols, int32_t dim);
 

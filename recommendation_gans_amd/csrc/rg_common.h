@@ -18,6 +18,29 @@ int check_launch(const char *what);
 int comm_begin(void *comm, hipStream_t stream, float *buf, int64_t n);
 int comm_end(void *comm, hipStream_t stream);
 
+// ---------------------------------------------------------------- MT jump-ahead
+// One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,
+// rg_sampler.hip).  Device buffers are owned by the plan.
+constexpr int kMtMaxTail = 8;
+struct MtTailSegs {
+    int64_t start[kMtMaxTail], len[kMtMaxTail];
+    int n;
+};
+struct MtJumpPlan {
+    int64_t words = 0, head = 0;   // words per step, head length
+    MtTailSegs segs{};
+    int chunks = 0;                // blocks per jump in mt_jump_kernel
+    int32_t *terms = nullptr;      // concatenated set bits of t^(D-1) mod chi, per slot
+    int32_t *term_off = nullptr;   // [segs.n + 2]
+    uint32_t *raw = nullptr;       // [(segs.n + 1) * 624] XOR accumulators
+};
+// nullptr if `words` is too short for the jump path (then use rg_mt_generate)
+MtJumpPlan *mt_jump_plan_create(int64_t words);
+void mt_jump_plan_destroy(MtJumpPlan *plan);
+// head -> jump -> tail on `stream`: out[0 .. words) and the next window-form state
+int mt_produce_jump(hipStream_t stream, const MtJumpPlan &plan, uint32_t *state, uint32_t *out,
+                    uint32_t *state_before);
+
 // ---------------------------------------------------------------- DPP
 // Cross-lane moves inside a 16-lane DPP row (no LDS traffic, all lanes valid).
 template <int CTRL>

@@ -22,6 +22,8 @@
 //             pre-step row, which is why the parameter tables ping-pong) plus
 //             weight_decay * p; Adam / SGD / RMSprop; p', m, v out; the list
 //             counter and overflow accumulators are reset in the same pass.
+#include <cstdlib>
+
 #include "rg_common.h"
 
 namespace rg {
@@ -60,8 +62,8 @@ struct PairsArgs {
 };
 
 // rg_mf_prepare: pairs[q * cols + s] for q = 0 (positive) and q = 1 + k (negative k)
-__global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out) {
-    __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
+__global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out, int prio) {
+    if (prio) __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
     const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t total = (int64_t)(1 + a.n_neg) * a.cols;
     if (idx >= total) return;
@@ -807,8 +809,9 @@ extern "C" int rg_mf_prepare(void *stream, const rg_mf_batch_t *b, const rg_mf_w
     a.pool_len = b->pool_len; a.n_neg = b->n_neg;
     a.perm = w ? w->plan_perm : nullptr;
     const int64_t total = (int64_t)(1 + b->n_neg) * b->cols;
+    static const int prio = [] { const char *e = getenv("RG_PREP_PRIO"); return e ? atoi(e) : 1; }();
     hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, reinterpret_cast<int2 *>(b->pairs));
+                       (hipStream_t)stream, a, reinterpret_cast<int2 *>(b->pairs), prio);
     return check_launch("rg_mf_prepare");
 }
 

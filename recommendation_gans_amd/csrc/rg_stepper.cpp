@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -32,6 +33,11 @@ struct Stepper {
     bool pending = false;        // buffer 1-buf holds words (+ pairs) generated ahead
     rg_mf_step_in_t pending_in{};
     int64_t words_per_step = 0;
+    // MT jump-ahead (long steps): the device state is then in window form after the
+    // first step; cp_pos tracks CPython's position-in-block of the same stream point
+    rg::MtJumpPlan *jump = nullptr;
+    bool window_form = false, window_prev = false;
+    int32_t cp_pos = 624, cp_pos_prev = 624;
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -68,13 +74,25 @@ bool same_input(const rg_mf_step_in_t &a, const rg_mf_step_in_t &b) {
     return std::memcmp(&a, &b, sizeof(a)) == 0;
 }
 
-// words (+ prepared pairs) for `in` into buffer b on the side stream
-int produce(Stepper &st, const rg_mf_step_in_t &in, int b) {
+// words (+ prepared pairs) for `in` into buffer b on the side stream, after the
+// consumer of buffer `after` (b itself, or the buffer the current step's pairs
+// kernel reads: then the sampler runs beside the HBM-bound apply, never beside
+// the latency-bound pairs kernel whose slowest block sets its duration)
+int produce(Stepper &st, const rg_mf_step_in_t &in, int b, int after) {
     hipError_t e;
-    if (st.consumed_valid[b] && (e = hipStreamWaitEvent(st.side, st.consumed[b], 0)) != hipSuccess)
+    if (st.consumed_valid[after] && (e = hipStreamWaitEvent(st.side, st.consumed[after], 0)) != hipSuccess)
         return hip_fail("stepper: wait consumed", e);
-    int rc = rg_mt_generate(st.side, st.cfg.mt_state, st.cfg.words[b], st.words_per_step, st.cfg.mt_state_before);
+    st.cp_pos_prev = st.cp_pos;
+    st.window_prev = st.window_form;
+    int rc;
+    if (st.jump) {
+        rc = rg::mt_produce_jump(st.side, *st.jump, st.cfg.mt_state, st.cfg.words[b], st.cfg.mt_state_before);
+        st.window_form = true;
+    } else {
+        rc = rg_mt_generate(st.side, st.cfg.mt_state, st.cfg.words[b], st.words_per_step, st.cfg.mt_state_before);
+    }
     if (rc) return rc;
+    st.cp_pos = (int32_t)((st.cp_pos + st.words_per_step - 1) % 624 + 1);
     rg_mf_work_t w = st.cfg.work;
     set_plan(w, in);
     rg_mf_batch_t batch = make_batch(st, in, b);
@@ -90,6 +108,8 @@ int discard(Stepper &st) {
     hipError_t e = hipMemcpyAsync(st.cfg.mt_state, st.cfg.mt_state_before, 625 * sizeof(uint32_t),
                                   hipMemcpyDeviceToDevice, st.side);
     if (e != hipSuccess) return hip_fail("stepper: restore MT state", e);
+    st.cp_pos = st.cp_pos_prev;
+    st.window_form = st.window_prev;
     st.pending = false;
     return RG_OK;
 }
@@ -104,7 +124,7 @@ int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int *b_o
         int rc = discard(st);
         if (rc) return rc;
         b = 1 - st.buf;
-        rc = produce(st, in, b);
+        rc = produce(st, in, b, b);
         if (rc) return rc;
     }
     hipError_t e = hipStreamWaitEvent(stream, st.ready[b], 0);
@@ -170,11 +190,16 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         e = hipEventCreateWithFlags(&st->ready[i], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&st->consumed[i], hipEventDisableTiming);
     }
+    uint32_t pos = 624;
+    if (e == hipSuccess) e = hipMemcpy(&pos, cfg->mt_state + 624, sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
         hip_fail("rg_mf_stepper_create", e);
         delete st;
         return nullptr;
     }
+    st->cp_pos = st->cp_pos_prev = (int32_t)pos;
+    const char *env = getenv("RG_MT_JUMP");
+    if (!env || atoi(env)) st->jump = rg::mt_jump_plan_create(st->words_per_step);
     return st;
 }
 
@@ -187,6 +212,7 @@ extern "C" int rg_mf_stepper_destroy(void *h) {
         if (st->consumed[i]) hipEventDestroy(st->consumed[i]);
     }
     if (st->side) hipStreamDestroy(st->side);
+    rg::mt_jump_plan_destroy(st->jump);
     delete st;
     return RG_OK;
 }
@@ -204,10 +230,12 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
     rg_mf_batch_t batch = make_batch(*st, *cur, b);
     rc = rg_mf_pairs(s, &st->cfg.tables[st->set], &batch, &w, 1);
     if (rc) return rc;
-    if ((rc = release(*st, s))) return rc;
+    static const bool late = [] { const char *e = getenv("RG_RELEASE_LATE"); return e && atoi(e); }();
+    if (!late && (rc = release(*st, s))) return rc;
     if (next) {                                  // generate the next step's words ahead
         const int nb = 1 - b;
-        if ((rc = produce(*st, *next, nb))) return rc;
+        static const bool after_pairs = [] { const char *e = getenv("RG_SAMPLER_AFTER_PAIRS"); return !e || atoi(e); }();
+        if ((rc = produce(*st, *next, nb, (after_pairs && !late) ? b : nb))) return rc;
         st->pending = true;
         st->pending_in = *next;
     }
@@ -236,6 +264,9 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
         if (st->cfg.comm && (rc = rg::comm_end(st->cfg.comm, s))) return rc;
         if ((rc = rg_mf_apply_dense(s, tb, st->cfg.item_grad, &o, U, R, loss_out))) return rc;
     }
+    // buffer b is free again once this step ends: recorded here rather than between
+    // pairs and apply, so the step's event packets sit at one kernel boundary
+    if (late && (rc = release(*st, s))) return rc;
     st->set = 1 - st->set;
     return RG_OK;
 }
@@ -291,11 +322,22 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
     if (e != hipSuccess) return hip_fail("stepper: sync", e);
     if (direction == 0) {   // device -> host: the state after the last CONSUMED word
         const uint32_t *src = st->pending ? st->cfg.mt_state_before : st->cfg.mt_state;
-        e = hipMemcpy(host_state, src, 625 * sizeof(uint32_t), hipMemcpyDeviceToHost);
-    } else {                // host -> device: drops anything generated ahead
-        st->pending = false;
-        e = hipMemcpy(st->cfg.mt_state, host_state, 625 * sizeof(uint32_t), hipMemcpyHostToDevice);
+        const bool window = st->pending ? st->window_prev : st->window_form;
+        const int32_t pos = st->pending ? st->cp_pos_prev : st->cp_pos;
+        uint32_t dev[625];
+        e = hipMemcpy(dev, src, 625 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_fail("stepper: copy MT state", e);
+        if (!window) {
+            std::memcpy(host_state, dev, sizeof(dev));
+            return RG_OK;
+        }
+        return rg_mt_window_to_cpython(dev, pos, host_state);
     }
+    // host -> device: drops anything generated ahead
+    st->pending = false;
+    st->window_form = st->window_prev = false;
+    st->cp_pos = st->cp_pos_prev = (int32_t)host_state[624];
+    e = hipMemcpy(st->cfg.mt_state, host_state, 625 * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail("stepper: copy MT state", e);
     return RG_OK;
 }

@@ -423,3 +423,56 @@ def test_large_full_size_properties(dev):
     st = orng.py_seed_state(0)
     orng.py_choices_indices(st, P, 5 * n * B)
     assert (e.mt_state() == st).all()
+
+
+@pytest.mark.parametrize("n", [5, 8])
+def test_jump_sampler_full_size_steps(dev, n):
+    """Steps of >= 41,120 words take the jump-ahead sampler (head + XOR-of-windows jump +
+    parallel tail segments; rg_mtjump.cpp).  With prefetch, a validation draw in
+    between (rolls back a prefetched step), export and re-import of the state:
+    negative pairs bit-exact, MT state exact, losses/tables as the oracle."""
+    from recommendation_gans_amd.mf_engine import MFEngine
+    U, I, d, B = 300, 200, 16, 8192
+    g = torch.Generator().manual_seed(3)
+    tabs = [torch.randn(U, d, generator=g) / d, torch.randn(I, d, generator=g) / d,
+            torch.zeros(U, 1), torch.zeros(I, 1)]
+    rs = np.random.RandomState(3)
+    pool_u, pool_i = rs.randint(0, U, 20000), rs.randint(0, I, 20000)
+    st = orng.py_seed_state(9)
+    st[624] = 300                                   # start mid-block
+    o = omf.MFOracle(*[t.clone() for t in tabs], pool_u, pool_i, st.copy(), loss="bpr", optimizer="adam",
+                     lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B)
+    o64 = omf.MFOracle(*[t.clone().double() for t in tabs], pool_u, pool_i, st.copy(), loss="bpr", optimizer="adam",
+                       lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B)
+    e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), pool_u, pool_i, st.copy(), loss="bpr",
+                 optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev)
+    batches = [(rs.randint(0, U, B), rs.randint(0, I, B)) for _ in range(5)]
+    dbat = [(torch.from_numpy(u).to(dev), torch.from_numpy(i).to(dev)) for u, i in batches]
+    for s in range(4):
+        nxt = e.step_input(*dbat[s + 1]) if s < 3 else None
+        out = o.step(*batches[s], return_all=True)
+        o64.step(*batches[s])
+        got = e.train_step(*dbat[s], next_input=nxt)
+        torch.cuda.synchronize()
+        close(got[0], np.float32(out["loss"]), what=f"jump step {s} loss")
+        # the consumed pairs buffer of this step: negatives (q >= 1) in draw order
+        found = False
+        for buf in e.pairs:
+            pr = buf.view(1 + n, B, 2).cpu().numpy()
+            if (pr[1:, :, 0].reshape(-1) == out["neg_u"].numpy()).all() and \
+               (pr[1:, :, 1].reshape(-1) == out["neg_i"].numpy()).all():
+                found = True
+        assert found, f"step {s}: negative pairs differ from random.choices"
+        if s == 1:                                  # validation draw between steps (discards the prefetch)
+            vu, vi = batches[4]
+            vl = e.val_loss(torch.from_numpy(vu).to(dev), torch.from_numpy(vi).to(dev))
+            ref = omf.val_loss(o, vu, vi)
+            omf.val_loss(o64, vu, vi)
+            torch.cuda.synchronize()
+            close(vl[0], np.float32(ref), what="jump val loss")
+        assert (e.mt_state() == o.state).all(), f"step {s}: MT state"
+        if s == 2:
+            e.set_mt_state(o.state)                 # import (back to CPython form)
+    for k in range(4):
+        ok, msg = omf.tensor_parity(e.params()[k], o.params[k], o64.params[k])
+        assert ok, (k, msg)
