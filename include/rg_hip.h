@@ -230,7 +230,8 @@ int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf_dev, int64_t 
 
 /* ------------------------------------------------------------------------------
  * Native step runtime (rg_stepper.cpp): one call per training step enqueues
- *   side stream:  rg_mt_generate + rg_mf_prepare of the NEXT step (generated ahead)
+ *   gen stream:   rg_mt_generate of the stream chunk two steps ahead
+ *   prep stream:  rg_mf_prepare of the NEXT step (draws -> pool pairs)
  *   main stream:  rg_mf_pairs -> rg_mf_apply of the current step
  * Replaces the loop body implicit.py:290-298 / run_train_iteration :347-364.
  *
@@ -243,8 +244,8 @@ int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf_dev, int64_t 
 typedef struct rg_mf_stepper_config {
     rg_mf_tables_t tables[2];       /* tables[k]: reads set k, writes set 1 - k */
     rg_mf_work_t work;              /* plan_* fields are set per step */
-    uint32_t *mt_state, *mt_state_before;   /* [625] each */
-    uint32_t *words[2];             /* [2 * n_neg * global_cols + RG_MT_PAD] each */
+    uint32_t *mt_state;             /* [625] CPython getstate()[1] layout; the stepper owns its
+                                       word ring (3 chunks of 2*n_neg*global_cols words) */
     int32_t *pairs[2];              /* [(1 + n_neg) * cols * 2] each */
     const int32_t *pool;
     int64_t pool_len;

@@ -70,7 +70,7 @@ class Opt(ctypes.Structure):
 
 class MFStepperConfig(ctypes.Structure):
     _fields_ = [("tables", MFTables * 2), ("work", MFWork), ("mt_state", ctypes.c_void_p),
-                ("mt_state_before", ctypes.c_void_p), ("words", ctypes.c_void_p * 2), ("pairs", ctypes.c_void_p * 2),
+                ("pairs", ctypes.c_void_p * 2),
                 ("pool", ctypes.c_void_p), ("pool_len", ctypes.c_int64), ("n_neg", ctypes.c_int32),
                 ("loss", ctypes.c_int32), ("cols", ctypes.c_int64), ("col_offset", ctypes.c_int64),
                 ("global_cols", ctypes.c_int64), ("neg_cols", ctypes.c_int64), ("item_grad", ctypes.c_void_p),

@@ -79,8 +79,9 @@ extern "C" void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, 
     int lo = 0, hi = 0;
     e = hipDeviceGetStreamPriorityRange(&lo, &hi);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
+    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;   // same-device ordering only
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, evf);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, evf);
     if (e != hipSuccess) {
         rg::hip_fail("rg_comm_create", e);
         delete c;

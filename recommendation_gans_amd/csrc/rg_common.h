@@ -134,6 +134,38 @@ struct RowLayout {
         }
     }
 
+    // streaming (non-temporal) store: the line is not kept dirty in L2, so the
+    // end-of-kernel release has less to write back before the next kernel starts
+    __device__ static __forceinline__ void store_nt(float *__restrict__ base, int64_t row, int D, int sub,
+                                                    const float (&v)[EPL]) {
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f t = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(t, reinterpret_cast<v4f *>(base + row * (int64_t)(4 * LPU) + sub * 4));
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                if (c < D) __builtin_nontemporal_store(v[e], base + row * (int64_t)D + c);
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base,
+                                                   int64_t row, int D, int sub) {
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f t = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(base + row * (int64_t)(4 * LPU) + sub * 4));
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                v[e] = c < D ? __builtin_nontemporal_load(base + row * (int64_t)D + c) : 0.0f;
+            }
+        }
+    }
+
     __device__ static __forceinline__ void zero(float (&v)[EPL]) {
 #pragma unroll
         for (int e = 0; e < EPL; ++e) v[e] = 0.0f;

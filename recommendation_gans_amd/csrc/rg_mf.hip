@@ -440,7 +440,9 @@ __device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gd
 
 // Streams every row of [row_begin, row_end) once (item rows first, so the few
 // long Zipf-hot item rows start early instead of trailing the grid).
-template <class L, int MODE>
+// NT: 1 = streaming stores of the updated p, m, v; 2 = also streaming loads of the
+// pre-step p, m, v (each touched once per step)
+template <class L, int MODE, int NT = 0>
 __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
     constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW;
     const int lane = threadIdx.x & (kWave - 1);
@@ -482,9 +484,15 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
     float p[EPL], m[EPL], v[EPL], g[EPL];
     float pb = 0.0f, mb = 0.0f, vb = 0.0f;
     if (MODE != kGradOnly) {
-        L::load(p, a.w_in[t], lr_, D, sub);
-        if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
-        if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+        if (NT >= 2) {
+            L::load_nt(p, a.w_in[t], lr_, D, sub);
+            if (adam) L::load_nt(m, a.w_m[t], lr_, D, sub); else L::zero(m);
+            if (has_v) L::load_nt(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+        } else {
+            L::load(p, a.w_in[t], lr_, D, sub);
+            if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
+            if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+        }
         if (sub == 0) {
             pb = a.b_in[t][lr_];
             if (adam) mb = a.b_m[t][lr_];
@@ -563,9 +571,15 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
 
 #pragma unroll
     for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
-    L::store(a.w_out[t], lr_, D, sub, p);
-    if (adam) L::store(a.w_m[t], lr_, D, sub, m);
-    if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
+    if (NT >= 1) {
+        L::store_nt(a.w_out[t], lr_, D, sub, p);
+        if (adam) L::store_nt(a.w_m[t], lr_, D, sub, m);
+        if (has_v) L::store_nt(a.w_v[t], lr_, D, sub, v);
+    } else {
+        L::store(a.w_out[t], lr_, D, sub, p);
+        if (adam) L::store(a.w_m[t], lr_, D, sub, m);
+        if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
+    }
     if (sub == 0) {
         pb = opt_update(a.opt, pb, gb, mb, vb);
         a.b_out[t][lr_] = pb;
@@ -685,7 +699,12 @@ struct ApplyLaunchF {
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
-        if (mode == kApplyPull)
+        static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
+        if (mode == kApplyPull && nt == 1)
+            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1>), dim3(nb), dim3(kBlock), 0, s, *a);
+        else if (mode == kApplyPull && nt >= 2)
+            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 2>), dim3(nb), dim3(kBlock), 0, s, *a);
+        else if (mode == kApplyPull)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kGradOnly)
             hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly>), dim3(nb), dim3(kBlock), 0, s, *a);

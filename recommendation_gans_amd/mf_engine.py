@@ -10,9 +10,10 @@ Everything of the step lives in HBM and is only touched by librg_hip.so:
     scratch  per-row contribution counters/lists, overflow accumulators, loss partials
 
 Per step: rg_mf_pairs (forward, loss, dL/dz, contribution lists) then
-rg_mf_apply (pull gradients + optimizer over every row).  The MT words for the
-NEXT step are generated on a side stream while the current step runs
-(``DeviceSampler``), so the sequential sampler is off the critical path.
+rg_mf_apply (pull gradients + optimizer over every row).  The native stepper
+(rg_stepper.cpp) generates the MT19937 words two steps ahead on a stream of its
+own and prepares the next step's pairs on another, so the sequential sampler is
+off the critical path.
 """
 import ctypes
 from collections import namedtuple
@@ -231,9 +232,6 @@ class MFEngine:
         self.grad_buf = None
         self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
         self.mt_buf = _as_u32_tensor(mt_state, dev)
-        self.mt_before = torch.zeros(625, dtype=torch.int32, device=dev)
-        self.words = [torch.zeros(self.words_per_step + RG_MT_PAD, dtype=torch.int32, device=dev)
-                      for _ in range(2)]
         self.pairs = [torch.zeros((1 + self.n_neg) * self.batch_size * 2, dtype=torch.int32, device=dev)
                       for _ in range(2)]
         self._work = _lib.MFWork(ptr(self.row_count), ptr(self.row_list), ptr(self.hot_grad), ptr(self.hot_bias),
@@ -244,8 +242,7 @@ class MFEngine:
         cfg = _lib.MFStepperConfig()
         cfg.tables[0], cfg.tables[1] = self._tables[0], self._tables[1]
         cfg.work = self._work
-        cfg.mt_state, cfg.mt_state_before = ptr(self.mt_buf), ptr(self.mt_before)
-        cfg.words[0], cfg.words[1] = ptr(self.words[0]), ptr(self.words[1])
+        cfg.mt_state = ptr(self.mt_buf)
         cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
         cfg.pool, cfg.pool_len = ptr(self.pool), self.pool_len
         cfg.n_neg, cfg.loss = self.n_neg, LOSS_KINDS[loss]
@@ -352,7 +349,9 @@ class MFEngine:
         cur = self.step_input(pos_u, pos_i, global_pos, plan)
         return self.train_step_in(cur, next_input if self.prefetch else None, apply_events)
 
-    def train_step_in(self, cur, next_input=None, apply_events=None):
+    def train_step_in(self, cur, next_input=None, apply_events=None, loss_out=None):
+        """One native step for a prebuilt ``step_input``; the loss goes to ``loss_out``
+        (a float32 device tensor of >= 1 element) or to the engine's own slot."""
         if self.dp == "user_shard" and self.world > 1 and self.comm is None:
             raise RuntimeError("user-sharded step over several ranks needs an RcclComm (or train_step_sharded)")
         if self.dp == "global_stream" and self.world > 1:
@@ -360,10 +359,13 @@ class MFEngine:
         ev0 = ev1 = None
         if apply_events is not None:
             ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
+        out = self.loss_out if loss_out is None else loss_out
+        if out.dtype != torch.float32 or out.device != self.device:
+            raise ValueError("loss_out must be a float32 tensor on the engine's device")
         check(self.lib.rg_mf_stepper_train(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
                                            ctypes.byref(next_input) if next_input is not None else None,
-                                           ptr(self.loss_out), ev0, ev1), "rg_mf_stepper_train")
-        return self.loss_out
+                                           ptr(out), ev0, ev1), "rg_mf_stepper_train")
+        return out
 
     def _acquire(self, cur):
         batch, work = _lib.MFBatch(), _lib.MFWork()

@@ -425,13 +425,17 @@ def test_large_full_size_properties(dev):
     assert (e.mt_state() == st).all()
 
 
+@pytest.mark.parametrize("jump", [0, 1])
 @pytest.mark.parametrize("n", [5, 8])
-def test_jump_sampler_full_size_steps(dev, n):
-    """Steps of >= 41,120 words take the jump-ahead sampler (head + XOR-of-windows jump +
-    parallel tail segments; rg_mtjump.cpp).  With prefetch, a validation draw in
-    between (rolls back a prefetched step), export and re-import of the state:
-    negative pairs bit-exact, MT state exact, losses/tables as the oracle."""
+def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
+    """Full-size steps through the stepper's word ring (chunks generated two steps
+    ahead), with the plain walk or (RG_MT_JUMP=1) the jump-ahead sampler (head +
+    XOR-of-windows jump + parallel tail segments; rg_mtjump.cpp).  With prefetch, a
+    validation draw in between (takes the next chunk; the prepared pairs are redone),
+    export and re-import of the state: negative pairs bit-exact, MT state exact,
+    losses/tables as the oracle."""
     from recommendation_gans_amd.mf_engine import MFEngine
+    monkeypatch.setenv("RG_MT_JUMP", str(jump))
     U, I, d, B = 300, 200, 16, 8192
     g = torch.Generator().manual_seed(3)
     tabs = [torch.randn(U, d, generator=g) / d, torch.randn(I, d, generator=g) / d,
