@@ -22,6 +22,12 @@ Fixtures:
   mf_fit_golden.npz ImplicitFactorizationModel.fit over 2 epochs with
                     validation interleaving (shared random stream) + test-time
                     predict scores.
+  mlp_<loss>_e<E>.npz
+                    3 training steps of the reference's NCF MLP
+                    (spotlight/dnn_models/mlp.py, layers as ncf_spotlight.py:53-56)
+                    through ImplicitFactorizationModel.run_train_iteration, with
+                    every dropout mask recorded by forward hooks (the masks come
+                    from torch's CPU generator; the GPU path is fed them).
 """
 import os
 import random
@@ -42,6 +48,7 @@ from spotlight import optimizers as ref_optim  # noqa: E402
 from spotlight import sampling as ref_sampling  # noqa: E402
 from spotlight.factorization.representations import BilinearNet  # noqa: E402
 from spotlight.interactions import Interactions  # noqa: E402
+from spotlight.dnn_models.mlp import MLP as RefMLP  # noqa: E402
 
 torch.set_num_threads(1)
 
@@ -263,6 +270,109 @@ def make_fit():
     rec["meta"] = np.array([U, I, d, B, n], dtype=np.int64)
     save("mf_fit_golden.npz", **rec)
 
+
+# ------------------------------------------------------------------ NCF MLP steps
+def mlp_case(loss, E, seed=0, U=50, I=40, B=16, n=5):
+    import math
+    top = math.log2(E * 2)
+    layers = [2 ** x for x in reversed(range(3, int(top) + 1))]       # ncf_spotlight.py:53-55
+    torch.manual_seed(seed)
+    net = RefMLP(layers=layers, num_users=U, num_items=I, embedding_dim=E)
+    init = {k: v.detach().clone().numpy() for k, v in net.state_dict().items()}
+    prs = np.random.RandomState(seed + 1)
+    pool_u, pool_i = prs.randint(0, U, 300), prs.randint(0, I, 300)
+    pool = list(zip(pool_u.tolist(), pool_i.tolist()))
+    steps_pos = []
+    for s_, bp in enumerate([B, 11, B]):
+        pu, pi = prs.randint(0, U, bp), prs.randint(0, I, bp)
+        pu[0] = pu[1]
+        pi[2] = pi[3] = pi[4]
+        steps_pos.append((pu, pi))
+    masks = []
+
+    def hook(mod, inp, out):
+        if mod.training:
+            masks.append((out != 0).to(torch.uint8).clone())
+
+    for m in net.layers:
+        if isinstance(m, torch.nn.Dropout):
+            m.register_forward_hook(hook)
+    with tempfile.TemporaryDirectory() as td:
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            model = ref_implicit.ImplicitFactorizationModel(
+                loss={"pointwise": "pointwise", "adaptive_hinge": "adaptive_hinge", "bpr": "pointwise"}[loss],
+                embedding_dim=E, n_iter=1, batch_size=B, l2=1e-5, learning_rate=1e-2,
+                optimizer_func=ref_optim.adam_optimizer, representation=net,
+                random_state=np.random.RandomState(seed), neg_examples=pool, num_negative_samples=n)
+            model._initialize(Interactions(np.zeros(1, np.int32), np.zeros(1, np.int32), num_users=U, num_items=I))
+        finally:
+            os.chdir(cwd)
+    random.seed(4321 + seed)
+    rec = {"init_" + k.replace(".", "_"): v for k, v in init.items()}
+    rec["layers"] = np.array(layers, dtype=np.int64)
+    rec["pool_u"], rec["pool_i"] = pool_u.astype(np.int64), pool_i.astype(np.int64)
+    rec["meta"] = np.array([U, I, E, B, n], dtype=np.int64)
+    names = [k for k, _ in net.named_parameters()]
+    rec["param_names"] = np.array(names)
+    for s_, (pu, pi) in enumerate(steps_pos):
+        rec[f"s{s_}_mt_state"] = np.array(random.getstate()[1], dtype=np.uint32)
+        rec[f"s{s_}_pos_u"], rec[f"s{s_}_pos_i"] = pu.astype(np.int64), pi.astype(np.int64)
+        bu, bi = torch.from_numpy(pu).long(), torch.from_numpy(pi).long()
+        masks.clear()
+        captured = {}
+        if loss in ("pointwise", "adaptive_hinge"):
+            orig = model._loss_func
+
+            def spy(pos, neg, _orig=orig):
+                captured["pos"], captured["neg"] = pos.detach().clone(), neg.detach().clone()
+                out = _orig(pos, neg)
+                captured["loss"] = float(out)
+                return out
+
+            model._loss_func = spy
+            orig_step = model._optimizer.step
+
+            def step_spy(*a, **k):
+                captured["grads"] = [p.grad.detach().clone() for p in model._net.parameters()]
+                return orig_step(*a, **k)
+
+            model._optimizer.step = step_spy
+            model.run_train_iteration(bu, bi)
+            model._loss_func, model._optimizer.step = orig, orig_step
+        else:
+            # the build's BPR on the NCF scores: pos squeezed to (B,), neg.view(n, B)
+            pos = model._net(bu, bi)
+            model._optimizer.zero_grad()
+            nu, ni = zip(*random.choices(pool, k=n * B))
+            neg = model._net(torch.from_numpy(np.array(nu)).long(), torch.from_numpy(np.array(ni)).long())
+            lv = ref_losses.bpr_loss(pos.view(-1), neg.view(n, B)[:, :len(pu)])
+            lv.backward()
+            captured.update(pos=pos.detach(), neg=neg.detach(), loss=float(lv),
+                            grads=[p.grad.detach().clone() for p in model._net.parameters()])
+            model._optimizer.step()
+        nd = len(masks) // 2
+        for k, m in enumerate(masks):
+            rec[f"s{s_}_mask_{'pos' if k < nd else 'neg'}{k % nd}"] = m.numpy()
+        rec[f"s{s_}_p_pos"], rec[f"s{s_}_p_neg"] = captured["pos"].numpy(), captured["neg"].numpy()
+        rec[f"s{s_}_loss"] = np.array([captured["loss"]])
+        for nm, g in zip(names, captured["grads"]):
+            rec[f"s{s_}_grad_" + nm.replace(".", "_")] = g.numpy()
+        for nm, p in model._net.named_parameters():
+            rec[f"s{s_}_after_" + nm.replace(".", "_")] = p.detach().clone().numpy()
+    rec["end_mt_state"] = np.array(random.getstate()[1], dtype=np.uint32)
+    return rec
+
+
+def make_mlp():
+    for loss, E in (("pointwise", 16), ("pointwise", 64), ("adaptive_hinge", 16), ("bpr", 16)):
+        save(f"mlp_{loss}_e{E}.npz", **mlp_case(loss, E))
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "mlp":
+    make_mlp()
+    sys.exit(0)
 
 if __name__ == "__main__":
     make_rng()
