@@ -289,6 +289,48 @@ int rg_mf_stepper_advance(void *stepper, int32_t flip_sets, int64_t steps);
  * 1: load host_state into the device state (drops words generated ahead).  Synchronises. */
 int rg_mf_stepper_sync_mt(void *stepper, uint32_t *host_state, int32_t direction);
 
+/* ------------------------------------------------------------------------------
+ * NCF MLP (rg_ncf.hip): spotlight/dnn_models/mlp.py:5-46 trained by
+ * implicit.py:347-364, layers [2E, E, ..., 8] -> 1 (ncf_spotlight.py:53-56),
+ * E in {8, 16, 32, 64}.  A step is
+ *   rg_mf_prepare -> rg_ncf_pairs (fused forward + loss + backward, MFMA) ->
+ *   rg_ncf_update (MLP gradient reduce + optimizer) -> rg_ncf_apply (embeddings)
+ * (adaptive hinge: rg_ncf_pairs(scores) -> rg_ncf_adapt_dp -> rg_ncf_pairs(given dp)).
+ * ---------------------------------------------------------------------------- */
+typedef struct rg_ncf_model {
+    float *user_w, *item_w;                 /* [U, E], [I, E]; updated in place */
+    float *user_w_m, *user_w_v, *item_w_m, *item_w_v;
+    float *mlp, *mlp_m, *mlp_v;             /* flat MLP parameters, named_parameters() order */
+    int64_t num_users, num_items;
+    int32_t dim, pad_;
+} rg_ncf_model_t;
+
+typedef struct rg_ncf_work {
+    float *contrib;                         /* [tiles * rows_per_tile * 2E] per-example input gradients */
+    float *mlp_partials;                    /* [rg_ncf_blocks * rg_ncf_mlp_len] */
+    float *scores;                          /* [tiles * rows_per_tile] (scores phase) */
+    float *dp;                              /* [tiles * rows_per_tile] (given-dp phase) */
+    const uint8_t *mask_pos, *mask_neg;     /* recorded dropout masks [rows][rg_ncf_mask_units] or null */
+    uint64_t seed;                          /* dropout hash seed when no masks are given */
+    int32_t training, pad_;                 /* 0: eval (no dropout) */
+} rg_ncf_work_t;
+
+int64_t rg_ncf_mlp_len(int32_t dim);
+int64_t rg_ncf_mask_units(int32_t dim);
+int64_t rg_ncf_cols_per_tile(int32_t n_neg);   /* also the plan's units per block */
+int64_t rg_ncf_rows_per_tile(void);
+int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg);
+int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg);
+/* phase 0: fused step (pointwise / bpr / hinge); 1: forward scores only; 2: fused with given dL/dp */
+int rg_ncf_pairs(void *stream, const rg_ncf_model_t *model, const rg_mf_batch_t *batch, rg_mf_work_t *work,
+                 rg_ncf_work_t *ncf_work, int32_t phase);
+int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *batch, rg_ncf_work_t *ncf_work, float *loss_partials);
+int rg_ncf_update(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t *ncf_work, int64_t nparts,
+                  const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss);
+/* Embedding rows [row_begin, row_end) (users then items): pull + optimizer, in place. */
+int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
+                 const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
+
 /* Milliseconds between two timing events (hipEvent_t) recorded on a stream. */
 int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms);
 

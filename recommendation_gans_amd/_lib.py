@@ -79,6 +79,20 @@ class MFStepperConfig(ctypes.Structure):
                 ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class NCFModel(ctypes.Structure):
+    _fields_ = [("user_w", ctypes.c_void_p), ("item_w", ctypes.c_void_p), ("user_w_m", ctypes.c_void_p),
+                ("user_w_v", ctypes.c_void_p), ("item_w_m", ctypes.c_void_p), ("item_w_v", ctypes.c_void_p),
+                ("mlp", ctypes.c_void_p), ("mlp_m", ctypes.c_void_p), ("mlp_v", ctypes.c_void_p),
+                ("num_users", ctypes.c_int64), ("num_items", ctypes.c_int64), ("dim", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
+
+
+class NCFWork(ctypes.Structure):
+    _fields_ = [("contrib", ctypes.c_void_p), ("mlp_partials", ctypes.c_void_p), ("scores", ctypes.c_void_p),
+                ("dp", ctypes.c_void_p), ("mask_pos", ctypes.c_void_p), ("mask_neg", ctypes.c_void_p),
+                ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
 class MFStepIn(ctypes.Structure):
     _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
                 ("global_pos", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
@@ -87,6 +101,20 @@ class MFStepIn(ctypes.Structure):
 
 # (name, restype, argtypes) for every symbol declared in include/rg_hip.h
 SIGNATURES = [
+    ("rg_ncf_mlp_len", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_ncf_mask_units", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_ncf_rows_per_tile", ctypes.c_int64, []),
+    ("rg_ncf_tiles", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_ncf_blocks", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_ncf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFBatch),
+                                    ctypes.POINTER(MFWork), ctypes.POINTER(NCFWork), ctypes.c_int32]),
+    ("rg_ncf_adapt_dp", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(NCFWork),
+                                       ctypes.c_void_p]),
+    ("rg_ncf_update", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(NCFWork),
+                                     ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p, ctypes.POINTER(MFLoss)]),
+    ("rg_ncf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
+                                    ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("rg_mt_window_to_cpython", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("rg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),

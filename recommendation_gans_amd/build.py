@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librg_hip.so")
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp", "rg_mtjump.cpp"]
+SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp", "rg_mtjump.cpp", "rg_ncf.hip"]
 HEADERS = ["rg_common.h"]
 
 

@@ -93,6 +93,25 @@ __device__ __forceinline__ int64_t choice_index(uint32_t w0, uint32_t w1, int64_
 
 __device__ __forceinline__ float sigmoidf_ref(float z) { return 1.0f / (1.0f + expf(-z)); }
 
+// torch.optim single-tensor update of one element, in the rounding torch's CPU
+// kernels use (checked on the reference's AVX-512 build): add(alpha) and addcmul
+// fuse their final multiply-add (FMA), addcdiv rounds (value * t1) / t2 then adds,
+// lerp(w = 1 - beta1) takes ATen's two-branch form.  g is the data gradient.
+__device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gdata, float &m, float &v) {
+    const float g = fmaf(o.weight_decay, p, gdata);         // grad.add(param, alpha=wd)
+    if (o.kind == RG_OPT_ADAM) {
+        const float w = o.one_minus_beta1;                  // exp_avg.lerp_(grad, 1 - beta1)
+        m = (fabsf(w) < 0.5f) ? fmaf(w, g - m, m) : fmaf(w - 1.0f, g - m, g);
+        v = fmaf(o.one_minus_beta2 * g, g, v * o.beta2);   // mul_(beta2).addcmul_(g, g, 1 - beta2)
+        const float denom = sqrtf(v) / o.bias_correction2_sqrt + o.eps;
+        return p + ((-o.step_size) * m) / denom;           // addcdiv_(m, denom, -step_size)
+    }
+    if (o.kind == RG_OPT_SGD) return fmaf(-o.lr, g, p);     // add_(g, alpha=-lr)
+    v = fmaf(o.one_minus_alpha * g, g, v * o.alpha);        // RMSprop (centered = False)
+    return p + ((-o.lr) * g) / (sqrtf(v) + o.eps);
+}
+
+
 // ---------------------------------------------------------------- row layouts
 // A table row of D floats is spread over LPU lanes.  VEC: D == 4 * LPU and each
 // lane owns one contiguous float4 (rows are 16-B aligned when D % 4 == 0).
@@ -116,6 +135,21 @@ struct RowLayout {
             for (int e = 0; e < EPL; ++e) {
                 const int c = sub + 64 * e;
                 v[e] = c < D ? base[row * (int64_t)D + c] : 0.0f;
+            }
+        }
+    }
+
+    // row of an array with an explicit row stride (floats; a multiple of 4 for VEC)
+    __device__ static __forceinline__ void load_strided(float (&v)[EPL], const float *__restrict__ base,
+                                                        int64_t row, int64_t stride, int D, int sub) {
+        if constexpr (VEC) {
+            const float4 t = *reinterpret_cast<const float4 *>(base + row * stride + sub * 4);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                v[e] = c < D ? base[row * stride + c] : 0.0f;
             }
         }
     }

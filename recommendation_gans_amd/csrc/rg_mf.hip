@@ -413,30 +413,17 @@ struct ApplyArgs {
     double inv_a, inv_b;
     float *loss_out;
     float *grad;                  // flat [(re-rb)*D | (re-rb) | loss] (kGradOnly / kApplyDense)
+    // NCF: list entries {example slot, 1.0f} point at per-example gradient rows
+    // contrib[slot * contrib_stride + table * D ..] instead of partner rows (then no biases)
+    const float *contrib;
+    int64_t contrib_stride;
+    bool has_bias;
 };
 
 // mf_apply modes: pull the gradient from the lists and update (single GPU);
 // pull into the flat dense gradient (before an all-reduce);
 // update from the (all-reduced) flat gradient.
 enum ApplyMode : int { kApplyPull = 0, kGradOnly = 1, kApplyDense = 2 };
-
-// torch.optim single-tensor update of one element, in the rounding torch's CPU
-// kernels use (checked on the reference's AVX-512 build): add(alpha) and addcmul
-// fuse their final multiply-add (FMA), addcdiv rounds (value * t1) / t2 then adds,
-// lerp(w = 1 - beta1) takes ATen's two-branch form.  g is the data gradient.
-__device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gdata, float &m, float &v) {
-    const float g = fmaf(o.weight_decay, p, gdata);         // grad.add(param, alpha=wd)
-    if (o.kind == RG_OPT_ADAM) {
-        const float w = o.one_minus_beta1;                  // exp_avg.lerp_(grad, 1 - beta1)
-        m = (fabsf(w) < 0.5f) ? fmaf(w, g - m, m) : fmaf(w - 1.0f, g - m, g);
-        v = fmaf(o.one_minus_beta2 * g, g, v * o.beta2);   // mul_(beta2).addcmul_(g, g, 1 - beta2)
-        const float denom = sqrtf(v) / o.bias_correction2_sqrt + o.eps;
-        return p + ((-o.step_size) * m) / denom;           // addcdiv_(m, denom, -step_size)
-    }
-    if (o.kind == RG_OPT_SGD) return fmaf(-o.lr, g, p);     // add_(g, alpha=-lr)
-    v = fmaf(o.one_minus_alpha * g, g, v * o.alpha);        // RMSprop (centered = False)
-    return p + ((-o.lr) * g) / (sqrtf(v) + o.eps);
-}
 
 // Streams every row of [row_begin, row_end) once (item rows first, so the few
 // long Zipf-hot item rows start early instead of trailing the grid).
@@ -493,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
             if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
             if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
         }
-        if (sub == 0) {
+        if (sub == 0 && a.has_bias) {
             pb = a.b_in[t][lr_];
             if (adam) mb = a.b_m[t][lr_];
             if (has_v) vb = a.b_v[t][lr_];
@@ -512,11 +499,13 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
             int2 ent[kCap];
 #pragma unroll
             for (int e = 0; e < kCap; ++e) ent[e] = e < ne ? a.row_list[r * kCap + e] : make_int2(0, 0);
-            const float *other = a.w_in[t ^ 1];
+            // MF: the partner row of the other table; NCF: the stored gradient half
+            const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
+            const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
             float o[kCap][EPL];
 #pragma unroll
             for (int e = 0; e < kCap; ++e) {
-                if (e < ne) L::load(o[e], other, ent[e].x, D, sub); else L::zero(o[e]);
+                if (e < ne) L::load_strided(o[e], other, ent[e].x, ostride, D, sub); else L::zero(o[e]);
             }
 #pragma unroll
             for (int e = 0; e < kCap; ++e) {
@@ -534,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
                 for (int q = 0; q < EPL; ++q) g[q] += h[q];
                 L::zero(h);
                 L::store(a.hot_grad, r, D, sub, h);
-                if (sub == 0) {
+                if (sub == 0 && a.has_bias) {
                     gb += a.hot_bias_grad[r];
                     a.hot_bias_grad[r] = 0.0f;
                 }
@@ -550,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
                 for (int u = 0; u < 4; ++u) {
                     const int ss = sl + u < s1 ? sl + u : s0;
                     L::load(h[u], a.part_row, ss, D, sub);
-                    hb[u] = a.part_bias[ss];
+                    hb[u] = a.has_bias ? a.part_bias[ss] : 0.0f;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -580,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
         if (adam) L::store(a.w_m[t], lr_, D, sub, m);
         if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
     }
-    if (sub == 0) {
+    if (sub == 0 && a.has_bias) {
         pb = opt_update(a.opt, pb, gb, mb, vb);
         a.b_out[t][lr_] = pb;
         if (adam) a.b_m[t][lr_] = mb;
@@ -886,8 +875,37 @@ static int apply_common(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, 
         a.loss_out = loss->out;
     }
     a.grad = grad_out ? grad_out : const_cast<float *>(grad_in);
+    a.has_bias = true;
     ApplyLaunchF f{&a, (hipStream_t)stream, mode};
     return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib,
+                            const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+    if (!m || !w || !opt || !contrib || !m->user_w || !m->item_w) return fail_arg("rg_ncf_apply: null argument");
+    if (!w->row_count || !w->row_list || !w->hot_grad) return fail_arg("rg_ncf_apply: null scratch");
+    if (opt->kind == RG_OPT_ADAM && (!m->user_w_m || !m->item_w_m)) return fail_arg("rg_ncf_apply: Adam needs m");
+    if (opt->kind != RG_OPT_SGD && (!m->user_w_v || !m->item_w_v)) return fail_arg("rg_ncf_apply: needs v");
+    if (w->plan_perm && !w->part_row) return fail_arg("rg_ncf_apply: plan needs part_row");
+    const int64_t nrows = m->num_users + m->num_items;
+    if (row_begin < 0) row_begin = 0;
+    if (row_end < 0 || row_end > nrows) row_end = nrows;
+    if (row_begin > row_end) return fail_arg("rg_ncf_apply: row_begin > row_end");
+    ApplyArgs a{};
+    a.w_in[0] = m->user_w; a.w_in[1] = m->item_w;
+    a.w_out[0] = m->user_w; a.w_out[1] = m->item_w;          // in place: no partner rows are read
+    a.w_m[0] = m->user_w_m; a.w_m[1] = m->item_w_m; a.w_v[0] = m->user_w_v; a.w_v[1] = m->item_w_v;
+    a.num_users = m->num_users; a.num_items = m->num_items; a.dim = m->dim;
+    a.row_begin = row_begin; a.row_end = row_end;
+    a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
+    a.hot_grad = w->hot_grad;
+    if (w->plan_perm) { a.item_slot_off = w->plan_item_slot_off; a.part_row = w->part_row; }
+    a.opt = *opt;
+    a.contrib = contrib;
+    a.contrib_stride = 2 * (int64_t)m->dim;
+    a.has_bias = false;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
+    return dispatch_dim(m->dim, f);
 }
 
 extern "C" int rg_mf_apply(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
