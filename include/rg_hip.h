@@ -321,7 +321,8 @@ int64_t rg_ncf_cols_per_tile(int32_t n_neg);   /* also the plan's units per bloc
 int64_t rg_ncf_rows_per_tile(void);
 int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg);
 int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg);
-/* phase 0: fused step (pointwise / bpr / hinge); 1: forward scores only; 2: fused with given dL/dp */
+/* phase 0: fused step (pointwise / bpr / hinge); 1: forward scores only; 2: fused with given dL/dp;
+ * 3: forward + loss partials only (validation, run with training = 0) */
 int rg_ncf_pairs(void *stream, const rg_ncf_model_t *model, const rg_mf_batch_t *batch, rg_mf_work_t *work,
                  rg_ncf_work_t *ncf_work, int32_t phase);
 int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *batch, rg_ncf_work_t *ncf_work, float *loss_partials);

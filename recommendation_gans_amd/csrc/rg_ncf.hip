@@ -83,7 +83,7 @@ struct NcfArgs {
     int training;
 };
 
-enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2 };
+enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2, kNcfLossOnly = 3 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
     x ^= x >> 33;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     int *sU = reinterpret_cast<int *>(sDz + kRows);
     int *sI = sU + kRows;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr bool kBackward = PHASE != kNcfScores;
+    constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
     const int n = a.n_neg, NP = n + 1, tc = a.tc;
 
     // ---- parameters into LDS (row stride H_k + 1), gradient accumulator zeroed ----
@@ -291,6 +291,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             a.loss_partials[2 * tile + 1] = lb;
         }
         __syncthreads();
+        if (PHASE == kNcfLossOnly) continue;         // validation: loss only (run_val_iteration)
         // ---- backward ------------------------------------------------------------------------
         {
             // output layer: dW_out += sum_r dz_r A_NH[r], db_out += sum_r dz_r; G_NH = dz w_out^T
@@ -539,12 +540,13 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     if (b->n_neg < 1 || b->n_neg > RG_MF_MAX_NEG) return fail_arg("rg_ncf_pairs: n_neg out of range");
     if (!b->pairs || !m->user_w || !m->item_w || !m->mlp) return fail_arg("rg_ncf_pairs: null tables / pairs");
     if (b->n_pos > b->cols) return fail_arg("rg_ncf_pairs: n_pos > cols");
-    if (phase != kNcfScores && (!w->row_count || !w->row_list || !w->hot_grad || !w->loss_partials ||
-                                !nw->contrib || !nw->mlp_partials))
+    if (phase != kNcfScores && phase != kNcfLossOnly && (!w->row_count || !w->row_list || !w->hot_grad ||
+                                                         !w->loss_partials || !nw->contrib || !nw->mlp_partials))
         return fail_arg("rg_ncf_pairs: null scratch");
+    if (phase == kNcfLossOnly && !w->loss_partials) return fail_arg("rg_ncf_pairs: loss needs partials");
     if (phase == kNcfScores && !nw->scores) return fail_arg("rg_ncf_pairs: scores buffer needed");
     if (phase == kNcfGivenDp && !nw->dp) return fail_arg("rg_ncf_pairs: dp buffer needed");
-    if (phase == kNcfFused && b->loss == RG_LOSS_ADAPTIVE_HINGE)
+    if ((phase == kNcfFused || phase == kNcfLossOnly) && b->loss == RG_LOSS_ADAPTIVE_HINGE)
         return fail_arg("rg_ncf_pairs: adaptive hinge runs as scores -> rg_ncf_adapt_dp -> given-dp");
     if (nw->training && (nw->mask_pos == nullptr) != (nw->mask_neg == nullptr))
         return fail_arg("rg_ncf_pairs: give both dropout mask arrays or neither");
@@ -574,6 +576,7 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfScores) { NcfLaunchF<kNcfScores> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfGivenDp) { NcfLaunchF<kNcfGivenDp> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
+    if (phase == kNcfLossOnly) { NcfLaunchF<kNcfLossOnly> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     return fail_arg("rg_ncf_pairs: bad phase");
 }
 

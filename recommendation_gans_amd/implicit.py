@@ -33,6 +33,7 @@ import torch
 
 from . import _mtstate
 from .mf_engine import MFEngine, build_plan
+from .ncf_engine import NCFEngine
 from .spotlight.factorization.representations import BilinearNet
 from .spotlight.optimizers import describe
 from .spotlight.sampling import NegativePool
@@ -103,23 +104,35 @@ class ImplicitFactorizationModel:
         net = self._representation
         if net is None:
             net = BilinearNet(self._num_users, self._num_items, self._embedding_dim, sparse=self._sparse)
-        if not isinstance(net, BilinearNet) and type(net).__name__ != "BilinearNet":
-            raise NotImplementedError("the fused MF step trains BilinearNet representations")
         self._net = net.to(dev)
-        self._embedding_dim = net.user_embeddings.weight.shape[1]
         self._opt = describe(self._optimizer_func, self._learning_rate, self._l2)
         if not self.neg_examples:
             raise NotImplementedError("training without a negative pool (neg_examples) is not supported")
         self._pool = NegativePool.from_pairs(self.neg_examples)
         o = self._opt
-        w = [self._net.user_embeddings.weight, self._net.item_embeddings.weight,
-             self._net.user_biases.weight, self._net.item_biases.weight]
-        self._engine = MFEngine(w[0].detach(), w[1].detach(), w[2].detach().reshape(-1), w[3].detach().reshape(-1),
-                                self._pool.user_ids, self._pool.item_ids, _mtstate.current(),
-                                loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"],
-                                weight_decay=o["weight_decay"], betas=o.get("betas", (0.9, 0.999)),
-                                eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
-                                n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
+        common = dict(loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
+                      betas=o.get("betas", (0.9, 0.999)), eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
+                      n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
+        if hasattr(net, "embedding_user") and hasattr(net, "layers"):          # NCF MLP (mlp.py:5-46)
+            self._kind = "ncf"
+            self._params = [net.embedding_user.weight, net.embedding_item.weight]
+            for lin in [m_ for m_ in net.layers if isinstance(m_, torch.nn.Linear)]:
+                self._params += [lin.weight, lin.bias]
+            self._embedding_dim = net.embedding_user.weight.shape[1]
+            self._engine = NCFEngine(self._params[0].detach(), self._params[1].detach(),
+                                     [p.detach() for p in self._params[2:]], self._pool.user_ids,
+                                     self._pool.item_ids, _mtstate.current(),
+                                     seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), **common)
+        elif hasattr(net, "user_embeddings") and hasattr(net, "item_biases"):   # BilinearNet
+            self._kind = "mf"
+            self._params = [net.user_embeddings.weight, net.item_embeddings.weight, net.user_biases.weight,
+                            net.item_biases.weight]
+            self._embedding_dim = net.user_embeddings.weight.shape[1]
+            w = [p.detach() for p in self._params]
+            self._engine = MFEngine(w[0], w[1], w[2].reshape(-1), w[3].reshape(-1), self._pool.user_ids,
+                                    self._pool.item_ids, _mtstate.current(), **common)
+        else:
+            raise NotImplementedError("the fused steps train BilinearNet and the NCF MLP representations")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
@@ -151,15 +164,21 @@ class ImplicitFactorizationModel:
         vu = torch.from_numpy(np.ascontiguousarray(valid_set.user_ids, dtype=np.int64)).to(dev)
         vi = torch.from_numpy(np.ascontiguousarray(valid_set.item_ids, dtype=np.int64)).to(dev)
         nb = (len(tu) + B - 1) // B
-        # the batches repeat every epoch (one shuffle): plans and step inputs are built once
-        plans = [build_plan(ti[s * B:(s + 1) * B], B, e.units_per_block, e.I) for s in range(nb)]
-        inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
         losses = torch.zeros(nb, dtype=torch.float32, device=dev)
         total = {"train_loss": [], "validation_loss": [], "curr_epoch": []}
+        # the batches repeat every epoch (one shuffle): plans (and MF step inputs) are built once
+        if self._kind == "mf":
+            plans = [build_plan(ti[s * B:(s + 1) * B], B, e.units_per_block, e.I) for s in range(nb)]
+            inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
+        else:
+            plans = [e.make_plan(ti[s * B:(s + 1) * B]) for s in range(nb)]
         for epoch in range(self._n_iter):
             for s in range(nb):
-                nxt = inputs[s + 1] if s + 1 < nb else None
-                e.train_step_in(inputs[s], nxt, loss_out=losses[s:s + 1])
+                if self._kind == "mf":
+                    e.train_step_in(inputs[s], inputs[s + 1] if s + 1 < nb else None, loss_out=losses[s:s + 1])
+                else:
+                    e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s],
+                                 loss_out=losses[s:s + 1])
             tl = [float(x) for x in losses.cpu().numpy()]          # loss.item() per batch
             train_epoch_loss = sum(tl) / nb
             if np.isnan(train_epoch_loss) or train_epoch_loss == 0.0:
@@ -180,14 +199,16 @@ class ImplicitFactorizationModel:
                             current_epoch=epoch, continue_from_mode=(self.starting_epoch != 0 or epoch > 0))
         _mtstate.restore(e.mt_state())                 # the Python stream continues after fit
         self._load_into_net(self.best_model)
-        e.set_params(*self.best_model)
+        if self._kind == "mf":
+            e.set_params(*self.best_model)
+        else:
+            e.set_params(self.best_model)
         self.save_readable_model(self.experiment_saved_models, self._net.state_dict())
         logging.info("Model chosen from epoch %d", self.best_epoch)
 
     def _load_into_net(self, tables):
         with torch.no_grad():
-            for p, t in zip((self._net.user_embeddings.weight, self._net.item_embeddings.weight,
-                             self._net.user_biases.weight, self._net.item_biases.weight), tables):
+            for p, t in zip(self._params, tables):
                 p.copy_(t.reshape(p.shape))
 
     def run_train_iteration(self, batch_user, batch_item):
@@ -212,15 +233,20 @@ class ImplicitFactorizationModel:
         i = torch.from_numpy(np.asarray(item_ids, dtype=np.int64).reshape(-1))
         if u.numel() != i.numel():
             u = u.expand(i.numel())
-        return self._engine.scores(u, i).cpu().numpy().flatten()
+        return self._engine.scores(u, i).detach().cpu().numpy().flatten()
 
     def score_users(self, users):
         """Scores of every item for a block of users, (len(users), num_items) float32 on
-        the host: one GEMM of the current tables (evaluation helper)."""
-        U, I, ub, ib = self._engine.params()
-        u = torch.as_tensor(np.asarray(users, dtype=np.int64), device=U.device)
-        z = U[u] @ I.T + ub[u][:, None] + ib[None, :]
-        return torch.sigmoid(z).cpu().numpy()
+        the host (evaluation helper): one GEMM of the tables (MF), or the eval-mode MLP
+        over the block x items pairs (NCF)."""
+        u = torch.as_tensor(np.asarray(users, dtype=np.int64), device=self._engine.device)
+        if self._kind == "mf":
+            U, I, ub, ib = self._engine.params()
+            z = U[u] @ I.T + ub[u][:, None] + ib[None, :]
+            return torch.sigmoid(z).cpu().numpy()
+        items = torch.arange(self._num_items, device=u.device)
+        s = self._engine.scores(u.repeat_interleave(self._num_items), items.repeat(len(u)))
+        return s.reshape(len(u), self._num_items).detach().cpu().numpy()
 
     def test(self, test_set, item_popularity, k=5, rmse_flag=False, precision_recall=False, map_recall=True):
         test_results = {"k": k}

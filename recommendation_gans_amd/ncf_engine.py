@@ -168,9 +168,10 @@ class NCFEngine:
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 0), "rg_ncf_pairs")
 
-    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None):
+    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None):
         """One step; ``masks`` = (mask_pos [B, units] uint8, mask_neg [n*B, units] uint8) device
-        tensors recorded from the reference, or None for the device dropout RNG."""
+        tensors recorded from the reference, or None for the device dropout RNG.  The loss
+        goes to ``loss_out`` (float32 device tensor) or the engine's own slot."""
         n_pos = int(pos_u.numel())
         global_pos = n_pos if global_pos is None else int(global_pos)
         x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos, global_pos,
@@ -188,13 +189,53 @@ class NCFEngine:
         check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
         o = self._opt(self.t)
         parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials
+        out = self.loss_out if loss_out is None else loss_out
         check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
-                                     ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, self.loss_out))),
+                                     ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
               "rg_ncf_update")
         check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
                                     ctypes.byref(o), 0, -1), "rg_ncf_apply")
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
-        return self.loss_out
+        return out
+
+    def _step_in(self, pos_u, pos_i, global_pos):
+        n_pos = int(pos_u.numel())
+        return _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos,
+                             n_pos if global_pos is None else int(global_pos), None, None, None)
+
+    def val_loss(self, pos_u, pos_i, global_pos=None):
+        """run_val_iteration (implicit.py:366-379): eval-mode forward (no dropout) and the
+        loss on the same negative stream; no update."""
+        x = self._step_in(pos_u, pos_i, global_pos)
+        stream = _lib.stream_handle()
+        batch, work = _lib.MFBatch(), _lib.MFWork()
+        check(self.lib.rg_mf_stepper_acquire(self._stepper, stream, ctypes.byref(x), ctypes.byref(batch),
+                                             ctypes.byref(work)), "rg_mf_stepper_acquire")
+        nw = self._work(None, False)
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        l = self._loss(x.global_pos, out)
+        if self.loss == "adaptive_hinge":
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 1), "rg_ncf_pairs(scores)")
+            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
+                  "rg_ncf_adapt_dp")
+            parts = self.adapt_partials
+        else:
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 3), "rg_ncf_pairs(loss)")
+            parts = self.partials
+        check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
+        check(self.lib.rg_loss_finalize(stream, ptr(parts), l.n_partials, l.inv_a, l.inv_b, ptr(out)),
+              "rg_loss_finalize")
+        return out
+
+    def params(self):
+        """[user table, item table, MLP parameters...] (device tensors of the reference's shapes)."""
+        return [self.user_w, self.item_w] + self.mlp_params()
+
+    def set_params(self, tensors):
+        for dst, src in zip(self.params(), tensors):
+            dst.copy_(torch.as_tensor(src, dtype=torch.float32).reshape(dst.shape))
 
     def scores(self, users, items):
         """Eval-mode scores (no dropout) for (user, item) pairs, on the device."""

@@ -85,3 +85,24 @@ def test_mf_spotlight_cli_synthetic(tmp_path, monkeypatch):
     ck = torch.load(os.path.join("experiments_results", "cli", "saved_models", "best_model"), weights_only=True)
     assert ck["network"]["user_embeddings.weight"].shape == (943, 32)
     assert 0 <= model.best_epoch <= 1
+
+
+def test_ncf_fit_and_cli(tmp_path, monkeypatch):
+    from recommendation_gans_amd import ncf_spotlight
+    monkeypatch.chdir(tmp_path)
+    np.random.seed(0)
+    random.seed(0)
+    model = ncf_spotlight.main(["--use_gpu", "True", "--dataset", "100K", "--training_epochs", "2",
+                                "--batch_size", "1024", "--mlp_embedding_dim", "16", "--experiment_name", "ncf",
+                                "--k", "3"])
+    logs = os.path.join("experiments_results", "ncf", "result_outputs")
+    rows = list(csv.reader(open(os.path.join(logs, "summary.csv"))))
+    assert len(rows) == 3 and all(np.isfinite(float(x)) for x in rows[1][:2] + rows[2][:2])
+    assert float(rows[2][0]) < float(rows[1][0])            # training loss falls over the epochs
+    ck = torch.load(os.path.join("experiments_results", "ncf", "saved_models", "best_model"), weights_only=True)
+    assert ck["network"]["embedding_user.weight"].shape == (943, 16)
+    assert "layers.0.weight" in ck["network"]
+    res = json.load(open(os.path.join(logs, "test_summary.json")))
+    assert {"precision", "recall", "map"} <= set(res)
+    p = model.predict(3)
+    assert p.shape == (1682,) and np.all((p > 0) & (p < 1))
