@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true")
+    ap.add_argument("--model", default="mf", choices=["mf", "ncf"],
+                    help="mf: the BASELINE metric (MF-BPR); ncf: config 3 (NCF MLP, MFMA roofline)")
     ap.add_argument("--events-every", type=int, default=8,
                     help="record the rg_mf_apply timing events on every k-th timed step")
     return ap.parse_args()
@@ -99,8 +101,82 @@ def cpu_baseline(data, d, B, n, loss, budget_s):
                       f"(+{setup:.1f} s pool/tuple setup untimed)"}
 
 
+HIDDEN_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 (matrix), dense
+
+
+def ncf_flops_per_example(E):
+    """Forward MACs of the MLP (layers 2E -> ... -> 8 -> 1) x 2 FLOP, x 3 (forward, dW, dA)."""
+    sizes, h = [], 2 * E
+    while h >= 8:
+        sizes.append(h)
+        h //= 2
+    macs = sum(a * b for a, b in zip(sizes[:-1], sizes[1:])) + 8
+    return 3 * 2 * macs
+
+
+def bench_ncf(args):
+    """Config 3: ncf_spotlight.py MovieLens-20M, mlp_embedding_dim=64, 1 GPU (pointwise, the CLI's
+    loss; dropout from the device hash RNG)."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    dev = torch.device("cuda:0")
+    E, B, n = args.dim, args.batch, args.neg
+    data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
+    U, I = data.num_users, data.num_items
+    torch.manual_seed(0)
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    params = [p.detach() for p in net.parameters()]
+    random.seed(0)
+    mt = np.asarray(random.getstate()[1], dtype=np.uint32)
+    eng = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt, loss="pointwise",
+                    optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0)
+    tu = torch.from_numpy(data.train_u).to(dev)
+    ti = torch.from_numpy(data.train_i).to(dev)
+    nb = len(data.train_u) // B
+    nplan = min(nb, args.warmup + args.steps)
+    plans = [eng.make_plan(ti[g * B:(g + 1) * B]) for g in range(nplan)]
+    for s in range(args.warmup):
+        g = s % nplan
+        eng.train_step(tu[g * B:(g + 1) * B], ti[g * B:(g + 1) * B], plan=plans[g])
+    torch.cuda.synchronize()
+    every = max(1, args.events_every)
+    evs = []
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        g = (args.warmup + s) % nplan
+        u, i = tu[g * B:(g + 1) * B], ti[g * B:(g + 1) * B]
+        if s % every == 0:
+            a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            eng.kernel_events = (a, b_)
+            evs.append((a, b_))
+        else:
+            eng.kernel_events = None
+        eng.train_step(u, i, plan=plans[g])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+    flops = ncf_flops_per_example(E) * B * (1 + n)
+    ach = flops / (ms * 1e-3) / 1e12
+    out = {"metric": "train interactions/sec, NCF MLP dim=64 MovieLens-20M (config 3)", "value": args.steps * B / el,
+           "unit": "interactions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": f"synthetic ML-20M-shaped (U={U}, I={I}); MLP init as the reference",
+           "config": {"workload": f"NCF MLP {mlp_layers(E)}->1, batch {B}, {n} negatives, pointwise, adam, "
+                                  f"dropout 0.5 (device hash RNG)", "global_batch": B, "embedding_dim": E,
+                      "parallelism": "dp1"},
+           "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (ncf_pairs_kernel)", "achieved": ach,
+                        "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
+                        "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
+           "final_loss": float(eng.loss_out[0])}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.model == "ncf":
+        return bench_ncf(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

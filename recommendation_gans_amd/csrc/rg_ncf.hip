@@ -56,7 +56,7 @@ struct NcfShape {
         for (int k = 1; k <= NH; ++k) u += H(k);
         return u;
     }
-    static constexpr int LDS = SW + SA + SA + P + 4 * kRows + 8;   // W, A, M(=A layout), dW, misc
+    static constexpr int LDS = SW + SA + SA + P + 11 * kRows + 8;   // W, A, M(=A layout), dW, misc
 };
 
 struct NcfArgs {
@@ -94,21 +94,36 @@ __device__ __forceinline__ uint32_t hash32(uint64_t x) {
     return (uint32_t)x;
 }
 
+// murmur3 fmix32: the per-unit dropout bit from the row's key
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bU;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35U;
+    h ^= h >> 16;
+    return h;
+}
+
 // C tile (16x16 at i0, j0) of A.B on LDS operands, K a multiple of 4.
 // A(i, k) = A[i * ai + k * ak], B(k, j) = B[k * bk + j * bj]; rows >= imax / cols >= jmax read 0.
 __device__ __forceinline__ v4f mma16(const float *A, int ai, int ak, const float *B, int bk, int bj, int i0, int j0,
                                      int K, int imax, int jmax, int lane) {
-    v4f acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    // called with compile-time shapes (the layer loops are unrolled): the k loop
+    // unrolls, LDS reads get immediate offsets and issue ahead of the MFMAs, and
+    // two accumulators alternate so the 40-cycle dependency does not serialise them
+    v4f acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
     const int li = lane & 15, lk = lane >> 4;
     const bool iv = i0 + li < imax, jv = j0 + li < jmax;
     const float *pa = A + (iv ? (i0 + li) : 0) * ai + lk * ak;
     const float *pb = B + lk * bk + (jv ? (j0 + li) : 0) * bj;
-    for (int k = 0; k < K; k += 4) {
-        const float x = iv ? pa[k * ak] : 0.0f;
-        const float y = jv ? pb[k * bk] : 0.0f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, acc, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < K; k += 8) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[k * ak] : 0.0f, jv ? pb[k * bk] : 0.0f, acc0, 0, 0, 0);
+        if (k + 4 < K)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[(k + 4) * ak] : 0.0f, jv ? pb[(k + 4) * bk] : 0.0f,
+                                                        acc1, 0, 0, 0);
     }
-    return acc;
+    return acc0 + acc1;
 }
 
 template <int E, int PHASE>
@@ -124,6 +139,15 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     float *sDz = sP + kRows;              // dL/dlogit per row
     int *sU = reinterpret_cast<int *>(sDz + kRows);
     int *sI = sU + kRows;
+    int *sR = sI + kRows;                 // per row: reference row of its mask (pos: column, neg: draw j)
+    uint32_t *sK = reinterpret_cast<uint32_t *>(sR + kRows);   // per row: dropout hash key
+    float *sLa = reinterpret_cast<float *>(sK + kRows);        // per column loss terms
+    float *sLb = sLa + kRows;
+    int *sLu = reinterpret_cast<int *>(sLb + kRows);          // per row: user list slot (-1: none)
+    int *sLi = sLu + kRows;                                   // per row: item list slot (-1: none / planned)
+    int *sPs = sLi + kRows;                                   // per row: plan slot of a positive (-1: none)
+    float *sX = sM + S::sa_off(0);                            // dX rows [kRows][IN0 + 1] (M_0 is unused)
+    constexpr int cl_base = 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
     const int n = a.n_neg, NP = n + 1, tc = a.tc;
@@ -158,6 +182,29 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
             sU[r] = u;
             sI[r] = i;
+            // the example's identity for dropout: recorded-mask row, or the hash key
+            const int64_t colid = a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
+            const int64_t gj = q == 0 ? colid : (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
+            sR[r] = (int)gj;
+            sK[r] = hash32(a.seed ^ ((uint64_t)(q == 0 ? 0 : 1) << 40) ^ ((uint64_t)gj * 0x9E3779B97F4A7C15ULL));
+            // list slots are claimed now (the entry does not depend on the gradient), so the
+            // atomics' round trip overlaps the gather; overflow rows add from LDS at the end
+            int lu = -1, li = -1, ps = -1;
+            if (kBackward && u >= 0) {
+                const int64_t ex = tile * kRows + r;
+                lu = atomicAdd(a.row_count + u, 1);
+                if (lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+                if (q == 0 && a.pos_slot != nullptr) {
+                    ps = a.pos_slot[s];
+                } else {
+                    const int64_t row = a.num_users + i;
+                    li = atomicAdd(a.row_count + row, 1);
+                    if (li < kNcfCap) a.row_list[row * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+                }
+            }
+            sLu[r] = lu;
+            sLi[r] = li;
+            sPs[r] = ps;
         }
         __syncthreads();
         // ---- gather A_0 = [U[u] | I[i]] ------------------------------------------------
@@ -173,6 +220,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         __syncthreads();
         // ---- forward hidden layers ---------------------------------------------------------
         int mask_base = 0;
+#pragma unroll
         for (int k = 0; k < NH; ++k) {
             const int in = S::H(k), out = S::H(k + 1);
             const float *Ak = sA + S::sa_off(k);
@@ -193,21 +241,12 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                         float m = zz > 0.0f ? 1.0f : 0.1f;
                         if (a.training) {
                             bool keep;
-                            const int q = row / tc;
-                            const int64_t s = c0 + row % tc;
-                            const int64_t colid = a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
                             if (a.mask_pos) {
                                 const int units = S::mask_units();
-                                if (sU[row] < 0) keep = false;
-                                else if (q == 0) keep = a.mask_pos[colid * units + mask_base + col] != 0;
-                                else {
-                                    const int64_t j = (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
-                                    keep = a.mask_neg[j * units + mask_base + col] != 0;
-                                }
+                                const uint8_t *mk = row < tc ? a.mask_pos : a.mask_neg;
+                                keep = sU[row] >= 0 && mk[(int64_t)sR[row] * units + mask_base + col] != 0;
                             } else {
-                                const uint64_t key = ((uint64_t)(q * a.global_cols + a.col_offset + colid) << 12) |
-                                                     (uint64_t)(mask_base + col);
-                                keep = hash32(a.seed ^ (key * 0x9E3779B97F4A7C15ULL)) & 1U;
+                                keep = (mix32(sK[row] + (uint32_t)(mask_base + col) * 0x85EBCA6BU) >> 7) & 1U;
                             }
                             m = keep ? 2.0f * m : 0.0f;
                         }
@@ -237,9 +276,10 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         // dL/dlogit per row (columns: one thread each) and the tile's loss partials
         if (tid < kRows) sDz[tid] = 0.0f;
         __syncthreads();
-        if (tid == 0) {
+        if (tid < tc) {
             float la = 0.0f, lb = 0.0f;
-            for (int cl = 0; cl < tc; ++cl) {
+            {
+                const int cl = tid;
                 float dp[RG_MF_MAX_NEG + 1];
                 for (int q = 0; q < NP; ++q) dp[q] = 0.0f;
                 const int r0 = cl;
@@ -287,6 +327,13 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                     sDz[r] = sU[r] >= 0 ? (dp[q] * (1.0f - p)) * p : 0.0f;
                 }
             }
+            sLa[cl_base + tid] = la;
+            sLb[cl_base + tid] = lb;
+        }
+        __syncthreads();
+        if (tid == 0) {     // column order, as the one-thread loop summed them
+            float la = 0.0f, lb = 0.0f;
+            for (int cl = 0; cl < tc; ++cl) { la += sLa[cl]; lb += sLb[cl]; }
             a.loss_partials[2 * tile] = la;
             a.loss_partials[2 * tile + 1] = lb;
         }
@@ -309,6 +356,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
             __syncthreads();
         }
+#pragma unroll
         for (int k = NH - 1; k >= 0; --k) {
             const int in = S::H(k), out = S::H(k + 1);
             const float *Ak = sA + S::sa_off(k);
@@ -346,39 +394,29 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                         Mk[row * (in + 1) + col] = c[rr] * Mk[row * (in + 1) + col];
                     } else {
                         a.contrib[(tile * kRows + row) * (int64_t)IN0 + col] = c[rr];
+                        sX[row * (IN0 + 1) + col] = c[rr];
                     }
                 }
             }
             __syncthreads();
         }
-        // ---- embedding gradient routing: list entries, planned item partials -------------------
-        if (tid < 2 * kRows) {
-            const int r = tid >> 1, half = tid & 1, q = r / tc;
-            if (sU[r] >= 0) {
-                const bool planned = half == 1 && q == 0 && a.pos_slot != nullptr;
-                if (!planned) {
-                    const int64_t row = half ? a.num_users + sI[r] : (int64_t)sU[r];
-                    const int sl = atomicAdd(a.row_count + row, 1);
-                    if (sl < kNcfCap) {
-                        a.row_list[row * kNcfCap + sl] = make_int2((int)(tile * kRows + r), __float_as_int(1.0f));
-                    } else {
-                        const float *g = a.contrib + (tile * kRows + r) * (int64_t)IN0 + half * E;
-                        for (int e = 0; e < E; ++e) atomicAdd(a.hot_grad + row * E + e, g[e]);
-                    }
-                }
+        // ---- embedding gradient: overflow rows (hot users/items), planned item partials -----------
+        for (int e = tid; e < 2 * kRows * E; e += kNcfThreads) {
+            const int r = e / (2 * E), half = (e / E) & 1, c = e % E;
+            const int sl = half ? sLi[r] : sLu[r];
+            if (sl >= kNcfCap) {
+                const int64_t row = half ? a.num_users + sI[r] : (int64_t)sU[r];
+                atomicAdd(a.hot_grad + row * E + c, sX[r * (IN0 + 1) + half * E + c]);
             }
         }
         if (a.pos_slot != nullptr) {
             // positives' item halves, same plan slot -> one partial row (fixed order, plain stores)
             for (int e = tid; e < tc * E; e += kNcfThreads) {
                 const int cl = e / E, c = e % E;
-                const int64_t s = c0 + cl;
-                if (sU[cl] < 0 || s >= a.n_pos) continue;
-                const int slot = a.pos_slot[s];
-                if (cl > 0 && s - 1 >= c0 && a.pos_slot[s - 1] == slot) continue;   // not the segment head
+                const int slot = sPs[cl];
+                if (slot < 0 || (cl > 0 && sPs[cl - 1] == slot)) continue;   // not the segment head
                 float acc = 0.0f;
-                for (int cc = cl; cc < tc && c0 + cc < a.n_pos && a.pos_slot[c0 + cc] == slot; ++cc)
-                    acc += a.contrib[(tile * kRows + cc) * (int64_t)IN0 + E + c];
+                for (int cc = cl; cc < tc && sPs[cc] == slot; ++cc) acc += sX[cc * (IN0 + 1) + E + c];
                 a.part_row[(int64_t)slot * E + c] = acc;
             }
         }
@@ -389,16 +427,19 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         for (int e = tid; e < P; e += kNcfThreads) a.wpart[(int64_t)blockIdx.x * P + e] = sG[e];
 }
 
-// reduce the weight-gradient partials (fixed order) + optimizer update of the MLP
-// parameters in place; block 0 also finalises the loss
+// reduce the weight-gradient partials + optimizer update of the MLP parameters in
+// place: a block owns 64 parameters, its 4 waves sum fixed quarters of the
+// partials (coalesced 256-B loads) and combine in LDS in a fixed order
+// (deterministic); block 0 also finalises the loss
 __global__ __launch_bounds__(256) void ncf_update_kernel(float *mlp, float *m, float *v, const float *wpart,
                                                         int nparts, int P, rg_opt_t opt, const float *loss_partials,
                                                         int64_t n_partials, double inv_a, double inv_b,
                                                         float *loss_out) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (loss_out && blockIdx.x == 0 && threadIdx.x < 64) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (loss_out && blockIdx.x == 0 && wave == 0) {
         double sa = 0.0, sb = 0.0;
-        for (int64_t i = threadIdx.x; i < n_partials; i += 64) {
+        for (int64_t i = lane; i < n_partials; i += 64) {
             sa += (double)loss_partials[2 * i];
             sb += (double)loss_partials[2 * i + 1];
         }
@@ -406,11 +447,17 @@ __global__ __launch_bounds__(256) void ncf_update_kernel(float *mlp, float *m, f
             sa += __shfl_xor(sa, off);
             sb += __shfl_xor(sb, off);
         }
-        if (threadIdx.x == 0) *loss_out = (float)(sa * inv_a + sb * inv_b);
+        if (lane == 0) *loss_out = (float)(sa * inv_a + sb * inv_b);
     }
-    if (e >= P) return;
+    const int e = blockIdx.x * 64 + lane;
+    const int q = (nparts + 3) / 4, k0 = wave * q, k1 = min(nparts, k0 + q);
     float g = 0.0f;
-    for (int k = 0; k < nparts; ++k) g += wpart[(int64_t)k * P + e];
+    if (e < P)
+        for (int k = k0; k < k1; ++k) g += wpart[(int64_t)k * P + e];
+    red[wave][lane] = g;
+    __syncthreads();
+    if (wave != 0 || e >= P) return;
+    g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
     float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
     const float p = opt_update(opt, mlp[e], g, mm, vv);
     mlp[e] = p;
@@ -530,7 +577,7 @@ extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg) {
 extern "C" int64_t rg_ncf_rows_per_tile(void) { return kRows; }
 extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg) {
     const int64_t t = rg_ncf_tiles(cols, n_neg);
-    return t <= 0 ? -1 : (t < 512 ? t : 512);
+    return t <= 0 ? -1 : (t < 256 ? t : 256);      // one resident workgroup per CU (LDS-bound)
 }
 
 extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_batch_t *b, rg_mf_work_t *w,
@@ -598,7 +645,7 @@ extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf
     const int P = ncf_mlp_len(m->dim);
     if (P < 0) return fail_arg("rg_ncf_update: bad dim");
     const bool with_loss = loss && loss->out;
-    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, m->mlp,
+    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(256), 0, (hipStream_t)stream, m->mlp,
                        opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,
                        nw->mlp_partials, (int)nparts, P, *opt, with_loss ? loss_partials : nullptr,
                        with_loss ? loss->n_partials : 0, with_loss ? loss->inv_a : 0.0,

@@ -80,6 +80,7 @@ class NCFEngine:
         self.mt_buf = torch.from_numpy(np.ascontiguousarray(np.asarray(mt_state, np.uint32)).view(np.int32)).to(dev)
         self.seed = int(seed)
         self.t = 0
+        self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
                                     self.U, self.I, E, 0)
@@ -185,7 +186,11 @@ class NCFEngine:
                                              ctypes.byref(work)), "rg_mf_stepper_acquire")
         self.t += 1
         nw = self._work(masks, True)
+        if self.kernel_events is not None:
+            self.kernel_events[0].record()
         self._forward_backward(batch, work, nw, stream)
+        if self.kernel_events is not None:
+            self.kernel_events[1].record()
         check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
         o = self._opt(self.t)
         parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials

@@ -60,7 +60,9 @@ def test_ncf_steps_match_reference(golden_dir, case):
 
 
 def test_ncf_device_dropout_trains():
-    """Device dropout RNG: deterministic for a seed, and a fixed batch's loss falls."""
+    """Device dropout RNG: reproducible for a seed (to float-atomic order: these tiny tables
+    overflow the per-row lists, whose overflow path adds with atomics), and a fixed
+    batch's loss falls."""
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from oracle import rng as orng
     dev = torch.device("cuda:0")
@@ -82,5 +84,5 @@ def test_ncf_device_dropout_trains():
         ls = [float(e.train_step(pu, pi, plan=e.make_plan(pi))[0]) for _ in range(6)]
         losses.append(ls)
         assert all(np.isfinite(ls))
-    assert losses[0] == losses[1]
+    np.testing.assert_allclose(losses[0], losses[1], rtol=1e-6)
     assert losses[0][-1] < losses[0][0]
