@@ -28,6 +28,15 @@ Fixtures:
                     through ImplicitFactorizationModel.run_train_iteration, with
                     every dropout mask recorded by forward hooks (the masks come
                     from torch's CPU generator; the GPU path is fed them).
+  gan_<opt>_n<N>.npz
+                    6 discriminator steps and the generator step after the 5th
+                    (n_critic = 5, CGANs.py:290-301) of the reference's own CGAN
+                    (CGANs.py:370-457) on its generator / discriminator
+                    (cGAN_models.py), slate_generation.py's layer shapes at a small
+                    size: every z, every dropout mask (forward hooks), BatchNorm
+                    running stats, d_loss / g_loss, D outputs, the generator's
+                    inference slates and training precision/recall, and all G / D
+                    parameters after every step.
 """
 import os
 import random
@@ -49,6 +58,8 @@ from spotlight import sampling as ref_sampling  # noqa: E402
 from spotlight.factorization.representations import BilinearNet  # noqa: E402
 from spotlight.interactions import Interactions  # noqa: E402
 from spotlight.dnn_models.mlp import MLP as RefMLP  # noqa: E402
+from spotlight.dnn_models import cGAN_models as ref_gan_models  # noqa: E402
+import CGANs as ref_cgans  # noqa: E402
 
 torch.set_num_threads(1)
 
@@ -369,6 +380,165 @@ def make_mlp():
     for loss, E in (("pointwise", 16), ("pointwise", 64), ("adaptive_hinge", 16), ("bpr", 16)):
         save(f"mlp_{loss}_e{E}.npz", **mlp_case(loss, E))
 
+
+def gan_case(opt="rms", seed=0, N=50, S=5, H=16, E=5, B=8, L=7, z_dim=100, nb=3, d_steps=6, lr=1e-3,
+             d_max=None):
+    """slate_generation.py:46-54 shapes: G hidden [H//2, H], D hidden [2H, H, H//2].
+
+    ``d_max``: scale each initial D tensor to max |x| = d_max.  At these sizes the
+    reference's Xavier bound (~0.09) is far outside the +-0.01 clamp, so nearly every
+    clamped D weight is exactly +-0.01 and pre-activations cancel to within rounding
+    of the LeakyReLU kink, where the slope (1 or 0.2) is decided by summation order
+    and no two implementations agree.  At the C4 size W1's Xavier bound is 0.0077,
+    inside the clamp; scaled tensors plus a small lr keep the goldens in that regime."""
+    torch.manual_seed(seed)
+    G = ref_gan_models.generator(num_items=N, noise_dim=z_dim, embedding_dim=E, hidden_layer=[H // 2, H],
+                                 output_dim=S)
+    D = ref_gan_models.discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
+    if d_max is not None:
+        with torch.no_grad():
+            for p_ in D.parameters():
+                p_.mul_(d_max / float(p_.abs().max()))
+    rs = np.random.RandomState(seed + 7)
+    # user histories: ragged, padded with N (slate_data_provider.py:226-234); one all-padding row
+    hist = np.full((nb * B, L), N, np.float32)
+    for r in range(nb * B):
+        ln = 0 if r == 5 else rs.randint(1, L + 1)
+        hist[r, :ln] = rs.choice(N, ln, replace=False)
+    slates = np.stack([rs.choice(N, S, replace=False) for _ in range(nb * B)]).astype(np.float32)
+    slates[3, 1] = slates[4, 1]             # two rows share an item in the same slot
+    g_init = {k: v.detach().clone().numpy() for k, v in G.state_dict().items()}
+    d_init = {k: v.detach().clone().numpy() for k, v in D.state_dict().items()}
+    zs, masks, bn = [], [], []
+
+    def z_hook(mod, args):
+        zs.append(args[0].detach().clone())
+
+    # torch's CPU dropout is the composite bernoulli_(1 - p) -> div_(1 - p) -> input * noise
+    # (ATen _dropout_impl); the same ops here (bit-identical output, gradient and generator
+    # position — checked below) so the noise itself is recorded: the discriminator's
+    # ±0.01 clamp makes exact-zero inputs common, whose mask the output would hide
+    orig_dropout = torch.nn.functional.dropout
+
+    def rec_dropout(input, p=0.5, training=True, inplace=False):
+        if not training or p == 0.0:
+            return orig_dropout(input, p, training, inplace)
+        noise = torch.empty_like(input).bernoulli_(1 - p)
+        noise.div_(1 - p)
+        masks.append((noise != 0).to(torch.uint8).clone())
+        return input * noise
+
+    x = torch.randn(16, 9)
+    gs = torch.get_rng_state()
+    ref_out = orig_dropout(x, 0.3, True)
+    r1 = torch.rand(2)
+    torch.set_rng_state(gs)
+    assert torch.equal(rec_dropout(x, 0.3, True), ref_out) and torch.equal(torch.rand(2), r1)
+    torch.set_rng_state(gs)
+    masks.clear()
+    torch.nn.functional.dropout = rec_dropout
+
+    G.register_forward_pre_hook(z_hook)
+    with tempfile.TemporaryDirectory() as td:
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            model = ref_cgans.CGAN(G=G, D=D, z_dim=z_dim, n_iter=1, batch_size=B, loss_fun="bce", learning_rate=lr,
+                                   slate_size=S, G_optimizer_func=getattr(ref_optim, opt + "_optimizer"),
+                                   D_optimizer_func=getattr(ref_optim, opt + "_optimizer"), embedding_dim=E,
+                                   hidden_layer=H, experiment_name="g")
+            model.num_users, model.num_items = nb * B, N
+            model._initialize()
+        finally:
+            os.chdir(cwd)
+    rec = {"g_init_" + k.replace(".", "_"): v for k, v in g_init.items()}
+    rec.update({"d_init_" + k.replace(".", "_"): v for k, v in d_init.items()})
+    rec["g_param_names"] = np.array([k for k, _ in G.named_parameters()])
+    rec["d_param_names"] = np.array([k for k, _ in D.named_parameters()])
+    rec["g_buffer_names"] = np.array([k for k, _ in G.named_buffers()])
+    rec["meta"] = np.array([N, S, H, E, B, L, z_dim, nb, d_steps], np.int64)
+    rec["lr"] = np.array([lr])
+    rec["hist"], rec["slates"] = hist, slates
+    rec["drop_scale"] = np.array([float(torch.ones(1).div_(1 - p)) for p in (0.1, 0.3)], np.float32)
+    hist_t, slates_t = torch.from_numpy(hist), torch.from_numpy(slates)
+    steps_performed = 0
+    for k in range(d_steps):
+        b = k % nb
+        bu, bs = hist_t[b * B:(b + 1) * B], slates_t[b * B:(b + 1) * B]
+        zs.clear()
+        masks.clear()
+        steps_performed += 1
+        rec[f"d{k}_batch"] = np.array([b])
+        dcap = []
+        orig_d = D.forward
+
+        def d_spy(x, c, _o=orig_d):
+            out = _o(x, c)
+            dcap.append((out.detach().clone(), x.detach().clone()))
+            return out
+
+        D.forward = d_spy
+        d_loss = model.train_discriminator_iteration(bu, bs)
+        D.forward = orig_d
+        rec[f"d{k}_d_real"], rec[f"d{k}_d_fake"] = dcap[0][0].numpy(), dcap[1][0].numpy()
+        rec[f"d{k}_fake"] = dcap[1][1].numpy()
+        rec[f"d{k}_z"] = zs[0].numpy()
+        for j, m in enumerate(masks):        # D(real) x3, G x2, D(fake) x3
+            rec[f"d{k}_mask{j}"] = m.numpy()
+        rec[f"d{k}_loss"] = np.array([d_loss])
+        for nm, p in D.named_parameters():
+            rec[f"d{k}_after_D_" + nm.replace(".", "_")] = p.detach().clone().numpy()
+        for nm, t in G.named_buffers():
+            rec[f"d{k}_after_G_" + nm.replace(".", "_")] = t.detach().clone().numpy()
+        if steps_performed % model.n_critic == 0:
+            zs.clear()
+            masks.clear()
+            cap = {}
+            orig_d = D.forward
+
+            def d_spy(x, c, _o=orig_d):
+                out = _o(x, c)
+                cap["d_fake"] = out.detach().clone()
+                cap["fake"] = x.detach().clone()
+                return out
+
+            D.forward = d_spy
+            g_loss, prec, recl = model.train_generator_iteration(bu, bs)
+            D.forward = orig_d
+            rec[f"g{k}_z"] = zs[0].numpy()
+            assert torch.equal(zs[0], zs[1]), "inference runs on the training z"
+            for j, m in enumerate(masks):    # G x2, D(fake) x3
+                rec[f"g{k}_mask{j}"] = m.numpy()
+            rec[f"g{k}_loss"] = np.array([g_loss])
+            rec[f"g{k}_d_fake"] = cap["d_fake"].numpy()
+            rec[f"g{k}_fake"] = cap["fake"].numpy()
+            rec[f"g{k}_precision"], rec[f"g{k}_recall"] = np.array(prec), np.array(recl)
+            G.eval()
+            with torch.no_grad():
+                rec[f"g{k}_slates_after"] = G(zs[0], bu, inference=True).numpy()
+            G.train()
+            for nm, p in G.named_parameters():
+                rec[f"g{k}_after_G_" + nm.replace(".", "_")] = p.detach().clone().numpy()
+            for nm, t in G.named_buffers():
+                rec[f"g{k}_after_G_" + nm.replace(".", "_")] = t.detach().clone().numpy()
+            rec["g_step_at"] = np.array([k])
+    if "g_step_at" not in rec:
+        rec["g_step_at"] = np.array([-1])
+    torch.nn.functional.dropout = orig_dropout
+    return rec
+
+
+def make_gan():
+    save("gan_rms_n50.npz", **gan_case("rms", lr=1e-4, d_max=0.004))
+    save("gan_adam_n50.npz", **gan_case("adam", seed=1, nb=2, lr=1e-4, d_max=0.004))
+    save("gan_sgd_n64.npz", **gan_case("sgd", seed=2, N=64, H=32, E=8, B=16, L=9, nb=2, d_steps=5, lr=1e-2,
+                                       d_max=0.004))
+    save("gan_rms_refinit.npz", **gan_case("rms", seed=3, d_steps=1))
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gan":
+    make_gan()
+    sys.exit(0)
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "mlp":
     make_mlp()
