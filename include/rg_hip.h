@@ -332,6 +332,106 @@ int rg_ncf_update(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t
 int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
                  const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
 
+/* ---------------------------------------------------------------- cGAN (C4)
+ * The generator / discriminator of spotlight/dnn_models/cGAN_models.py as
+ * slate_generation.py:46-54 builds them (G hidden [H/2, H], D hidden [2H, H, H/2])
+ * and the two training iterations of CGANs.py (rg_gan.hip, GEMMs in rg_gemm.hip):
+ *   rg_gan_d_step  replaces CGAN.train_discriminator_iteration (CGANs.py:410-457)
+ *   rg_gan_g_step  replaces CGAN.train_generator_iteration     (CGANs.py:370-408)
+ *   rg_gan_generate replaces generator.forward(inference=True) (cGAN_models.py:52-62)
+ * Parameters live in two flat fp32 buffers laid out by rg_gan_layout (blocks in the
+ * reference's tensor order; D's layers.0.weight is split into its E history
+ * columns W1E and its S*N slate columns W1S, row stride ks); optimizer state
+ * buffers (m, v) cover [0, g_off[RG_GAN_G_RM1]) and [0, d_off[RG_GAN_D_END]). */
+typedef struct rg_gan_dims {
+    int32_t num_items;   /* N; the padding id (history) is N */
+    int32_t slate_size;  /* S */
+    int32_t hidden;      /* H (gan_hidden_layer) */
+    int32_t emb_dim;     /* E (gan_embedding_dim) */
+    int32_t z_dim;       /* Z (noise_dim, 100) */
+    int32_t batch_max;   /* largest batch a workspace serves */
+} rg_gan_dims_t;
+
+enum rg_gan_g_block {
+    RG_GAN_G_WH = 0,   /* mult_heads.head_s.weight stacked: [S*N][H] (+ zero rows up to ks) */
+    RG_GAN_G_BH,       /* mult_heads.head_s.bias stacked: [S*N] (+ zeros up to ks) */
+    RG_GAN_G_EMB,      /* embedding_layer.weight [N+1][E] */
+    RG_GAN_G_W1,       /* layers.0.weight [H/2][kz] (kz = Z+E rounded up to 4, zero pad) */
+    RG_GAN_G_B1, RG_GAN_G_GAMMA1, RG_GAN_G_BETA1,
+    RG_GAN_G_W2,       /* layers.4.weight [H][H/2] */
+    RG_GAN_G_B2, RG_GAN_G_GAMMA2, RG_GAN_G_BETA2,
+    RG_GAN_G_RM1, RG_GAN_G_RV1, RG_GAN_G_RM2, RG_GAN_G_RV2,   /* BatchNorm buffers (not optimized) */
+    RG_GAN_G_END
+};
+enum rg_gan_d_block {
+    RG_GAN_D_W1S = 0,  /* layers.0.weight[:, E:] [2H][ks] (ks = S*N rounded up to 4) */
+    RG_GAN_D_EMB,      /* embedding_layer.weight [N+1][E] */
+    RG_GAN_D_W1E,      /* layers.0.weight[:, :E] [2H][E] */
+    RG_GAN_D_B1, RG_GAN_D_W2, RG_GAN_D_B2, RG_GAN_D_W3, RG_GAN_D_B3, RG_GAN_D_W4, RG_GAN_D_B4,
+    RG_GAN_D_END
+};
+enum rg_gan_ws_view {
+    RG_GAN_WS_FAKE = 0,   /* G(z) of the last step: [rows][ks] */
+    RG_GAN_WS_DOUT,       /* D outputs of the last step: D step [real rows | fake rows], G step [fake rows] */
+    RG_GAN_WS_END
+};
+
+/* Offsets (floats) of the blocks; g_off[RG_GAN_G_END] / d_off[RG_GAN_D_END] are the
+ * buffer lengths.  strides[0] = kz, strides[1] = ks. */
+int rg_gan_layout(const rg_gan_dims_t *dims, int64_t *g_off, int64_t *d_off, int64_t *strides);
+/* The workspace must be zero-filled once before its first use (padding columns are
+ * read as zeros and never written). */
+int64_t rg_gan_workspace_bytes(const rg_gan_dims_t *dims);
+/* Offset (bytes) of a named intermediate inside the workspace. */
+int64_t rg_gan_workspace_offset(const rg_gan_dims_t *dims, int32_t view);
+
+typedef struct rg_gan_model {
+    rg_gan_dims_t dims;
+    float *g, *g_m, *g_v;   /* m / v may be NULL when the optimizer does not use them */
+    float *d, *d_m, *d_v;
+} rg_gan_model_t;
+
+typedef struct rg_gan_batch {
+    int32_t rows;                  /* <= dims.batch_max */
+    int32_t hist_len;              /* L */
+    const int32_t *hist;           /* [rows][L] item ids, padding = N */
+    const int32_t *slates;         /* [rows][S] real slates (D step) */
+    /* history items grouped for the embedding backward (deterministic order):
+     * unique items [n_hist_items], offsets [n_hist_items + 1], batch rows */
+    const int32_t *hist_items, *hist_off, *hist_rows;
+    int32_t n_hist_items;
+    int32_t n_hits;                /* rows * S */
+    /* real-slate columns s*N + slates[b][s], sorted by (column, b), and their rows */
+    const int32_t *hit_col, *hit_row;
+} rg_gan_batch_t;
+
+typedef struct rg_gan_noise {
+    const float *z;                /* [rows][Z] uniform [0, 1) (torch.rand) */
+    /* recorded dropout masks [rows][width] in the reference's call order
+     * (D step: D(real) x3, G x2, D(fake) x3; G step: G x2, D(fake) x3), or NULL:
+     * then a counter-based hash of (seed, call, layer, row, unit) keeps with 1 - p */
+    const uint8_t *masks[8];
+    uint64_t seed;
+} rg_gan_noise_t;
+
+/* out: [0] d_loss = mean D(fake) - mean D(real), [1] mean D(real), [2] mean D(fake). */
+int rg_gan_d_step(void *stream, const rg_gan_model_t *model, void *workspace, const rg_gan_batch_t *batch,
+                  const rg_gan_noise_t *noise, const rg_opt_t *opt, float *out);
+/* out: [0] g_loss = -mean D(G(z)).  slates (optional, [rows][S] float item ids): the
+ * eval-mode generator on the same z after the update (CGANs.py:404-406). */
+int rg_gan_g_step(void *stream, const rg_gan_model_t *model, void *workspace, const rg_gan_batch_t *batch,
+                  const rg_gan_noise_t *noise, const rg_opt_t *opt, float *out, float *slates);
+/* Eval-mode generator (BatchNorm running stats, no dropout): argmax slates [rows][S]. */
+int rg_gan_generate(void *stream, const rg_gan_model_t *model, void *workspace, const rg_gan_batch_t *batch,
+                    const float *z, float *slates);
+
+/* fp32 MFMA GEMM used by the cGAN (test entry): C = A B^T with A [M][K] (a_kmajor) or
+ * [K][M], B [N][K] (b_kmajor) or [K][N]; post 0 none / 1 tanh; splits > 1 uses work
+ * [splits * M * N] and a fixed-order reduction. */
+int rg_gemm_f32(void *stream, const float *A, int64_t lda, int32_t a_kmajor, const float *B, int64_t ldb,
+                int32_t b_kmajor, int64_t M, int64_t N, int64_t K, float *C, int64_t ldc, const float *bias,
+                int32_t post, int32_t splits, float *work);
+
 /* Milliseconds between two timing events (hipEvent_t) recorded on a stream. */
 int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms);
 

@@ -93,6 +93,34 @@ class NCFWork(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class GANDims(ctypes.Structure):
+    _fields_ = [("num_items", ctypes.c_int32), ("slate_size", ctypes.c_int32), ("hidden", ctypes.c_int32),
+                ("emb_dim", ctypes.c_int32), ("z_dim", ctypes.c_int32), ("batch_max", ctypes.c_int32)]
+
+
+class GANModel(ctypes.Structure):
+    _fields_ = [("dims", GANDims), ("g", ctypes.c_void_p), ("g_m", ctypes.c_void_p), ("g_v", ctypes.c_void_p),
+                ("d", ctypes.c_void_p), ("d_m", ctypes.c_void_p), ("d_v", ctypes.c_void_p)]
+
+
+class GANBatch(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_int32), ("hist_len", ctypes.c_int32), ("hist", ctypes.c_void_p),
+                ("slates", ctypes.c_void_p), ("hist_items", ctypes.c_void_p), ("hist_off", ctypes.c_void_p),
+                ("hist_rows", ctypes.c_void_p), ("n_hist_items", ctypes.c_int32), ("n_hits", ctypes.c_int32),
+                ("hit_col", ctypes.c_void_p), ("hit_row", ctypes.c_void_p)]
+
+
+class GANNoise(ctypes.Structure):
+    _fields_ = [("z", ctypes.c_void_p), ("masks", ctypes.c_void_p * 8), ("seed", ctypes.c_uint64)]
+
+
+# rg_gan_layout block indices (include/rg_hip.h enum rg_gan_g_block / rg_gan_d_block)
+GAN_G_BLOCKS = ["WH", "BH", "EMB", "W1", "B1", "GAMMA1", "BETA1", "W2", "B2", "GAMMA2", "BETA2",
+                "RM1", "RV1", "RM2", "RV2"]
+GAN_D_BLOCKS = ["W1S", "EMB", "W1E", "B1", "W2", "B2", "W3", "B3", "W4", "B4"]
+GAN_WS_FAKE, GAN_WS_DOUT = 0, 1
+
+
 class MFStepIn(ctypes.Structure):
     _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
                 ("global_pos", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
@@ -101,6 +129,22 @@ class MFStepIn(ctypes.Structure):
 
 # (name, restype, argtypes) for every symbol declared in include/rg_hip.h
 SIGNATURES = [
+    ("rg_gan_layout", ctypes.c_int, [ctypes.POINTER(GANDims), ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    ("rg_gan_workspace_bytes", ctypes.c_int64, [ctypes.POINTER(GANDims)]),
+    ("rg_gan_workspace_offset", ctypes.c_int64, [ctypes.POINTER(GANDims), ctypes.c_int32]),
+    ("rg_gan_d_step", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GANModel), ctypes.c_void_p,
+                                     ctypes.POINTER(GANBatch), ctypes.POINTER(GANNoise), ctypes.POINTER(Opt),
+                                     ctypes.c_void_p]),
+    ("rg_gan_g_step", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GANModel), ctypes.c_void_p,
+                                     ctypes.POINTER(GANBatch), ctypes.POINTER(GANNoise), ctypes.POINTER(Opt),
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_gan_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GANModel), ctypes.c_void_p,
+                                       ctypes.POINTER(GANBatch), ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_gemm_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                   ctypes.c_int32, ctypes.c_void_p]),
     ("rg_ncf_mlp_len", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_ncf_mask_units", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32]),

@@ -18,8 +18,9 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librg_hip.so")
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp", "rg_mtjump.cpp", "rg_ncf.hip"]
-HEADERS = ["rg_common.h"]
+SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp", "rg_mtjump.cpp", "rg_ncf.hip",
+           "rg_gemm.hip", "rg_gan.hip"]
+HEADERS = ["rg_common.h", "rg_gemm.h"]
 
 
 def _hipcc():

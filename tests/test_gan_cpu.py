@@ -1,0 +1,57 @@
+"""cGAN host logic on the CPU: the rg_gan layout ABI (block sizes / padding), the
+device-batch grouping (history items -> batch rows, real-slate column hits) and the
+no-CPU-fallback guard."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from recommendation_gans_amd import _lib
+
+
+def layout(N, S, H, E, Z=100, B=8):
+    L = _lib.load()
+    dims = _lib.GANDims(N, S, H, E, Z, B)
+    go = (ctypes.c_int64 * (len(_lib.GAN_G_BLOCKS) + 1))()
+    do = (ctypes.c_int64 * (len(_lib.GAN_D_BLOCKS) + 1))()
+    st = (ctypes.c_int64 * 2)()
+    assert L.rg_gan_layout(ctypes.byref(dims), go, do, st) == 0
+    return list(go), list(do), list(st), L.rg_gan_workspace_bytes(ctypes.byref(dims))
+
+
+@pytest.mark.parametrize("N,S,H,E", [(50, 5, 16, 5), (20108, 5, 256, 5), (1682, 3, 10, 5)])
+def test_gan_layout(N, S, H, E):
+    go, do, (kz, ks), ws = layout(N, S, H, E)
+    assert kz % 4 == 0 and kz >= 100 + E and ks % 4 == 0 and ks >= S * N
+    H1 = H // 2
+    sizes_g = [ks * H, ks, (N + 1) * E, H1 * kz, H1, H1, H1, H * H1, H, H, H, H1, H1, H, H]
+    for i, n in enumerate(sizes_g):
+        assert go[i + 1] - go[i] >= n and go[i] % 64 == 0
+    sizes_d = [2 * H * ks, (N + 1) * E, 2 * H * E, 2 * H, H * 2 * H, H, H1 * H, H1, H1, 1]
+    for i, n in enumerate(sizes_d):
+        assert do[i + 1] - do[i] >= n and do[i] % 64 == 0
+    assert ws > 0 and ws % 4 == 0
+
+
+def test_gan_batch_grouping():
+    from recommendation_gans_amd.gan_engine import GANBatch
+    N, S = 20, 3
+    hist = np.array([[3, 7, 20, 20], [7, 1, 3, 20], [20, 20, 20, 20], [5, 7, 3, 2]])
+    slates = np.array([[1, 2, 3], [1, 9, 3], [4, 2, 0], [19, 2, 3]])
+    b = GANBatch(hist, slates, N, S, "cpu")
+    items, off, rows = b.hist_items.numpy(), b.hist_off.numpy(), b.hist_rows.numpy()
+    got = {int(it): list(rows[off[i]:off[i + 1]]) for i, it in enumerate(items)}
+    assert got == {1: [1], 2: [3], 3: [0, 1, 3], 5: [3], 7: [0, 1, 3]}
+    col, row = b.hit_col.numpy(), b.hit_row.numpy()
+    assert list(zip(col, row)) == sorted((s * N + slates[r, s], r) for r in range(4) for s in range(S))
+    with pytest.raises(ValueError):
+        GANBatch(hist, slates + 30, N, S, "cpu")
+    with pytest.raises(ValueError):
+        GANBatch(hist + 1, slates, N, S, "cpu")
+
+
+def test_gan_engine_is_gpu_only():
+    from recommendation_gans_amd.gan_engine import GANEngine
+    with pytest.raises(RuntimeError, match="GPU only"):
+        GANEngine({}, {}, 50, 5, 16, 5, device="cpu")
