@@ -63,8 +63,13 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true")
-    ap.add_argument("--model", default="mf", choices=["mf", "ncf"],
-                    help="mf: the BASELINE metric (MF-BPR); ncf: config 3 (NCF MLP, MFMA roofline)")
+    ap.add_argument("--model", default="mf", choices=["mf", "ncf", "gan"],
+                    help="mf: the BASELINE metric (MF-BPR); ncf: config 3 (NCF MLP, MFMA roofline); "
+                         "gan: config 4 (cGAN slate generation, MFMA roofline)")
+    ap.add_argument("--gan-batch", type=int, default=256, help="cGAN batch (arg_extractor.py --batch_size)")
+    ap.add_argument("--gan-hidden", type=int, default=256)
+    ap.add_argument("--gan-slate", type=int, default=5)
+    ap.add_argument("--gan-emb", type=int, default=5)
     ap.add_argument("--events-every", type=int, default=8,
                     help="record the rg_mf_apply timing events on every k-th timed step")
     return ap.parse_args()
@@ -173,10 +178,106 @@ def bench_ncf(args):
     print(json.dumps(out), flush=True)
 
 
+def gan_flops(N, S, H, E, Z, B):
+    """Algorithmic FLOPs of one discriminator and one generator iteration:
+    2 * multiply-adds of every dense contraction, the real slates' one-hot layer counted
+    by its S nonzeros per row (structural zeros are not work)."""
+    SN, H1, H2 = S * N, H // 2, 2 * H
+    g_fwd = 2 * B * ((Z + E) * H1 + H1 * H + H * SN)
+    d_l1 = 2 * B * (SN + E) * H2
+    d_up = 2 * B * (H2 * H + H * H1 + H1)                 # layers 2..4, per pass
+    d_real_l1 = 2 * B * (S + E) * H2
+    d_step = (d_real_l1 + d_l1 + 2 * d_up + g_fwd          # forward: D(real), G(z), D(fake)
+              + 2 * (2 * d_up)                             # upper layers: dW + dX, both passes
+              + 2 * B * H2 * SN + 2 * 2 * B * H2 * E)      # layer-1 dW (fake dense; real sparse ~0) + history cols
+    g_step = (g_fwd + d_l1 + d_up                          # G(z), D(fake)
+              + 2 * d_up + 2 * B * H2 * SN                  # D backward to the slate input
+              + 2 * 2 * B * SN * H                          # heads: dWH and dA2
+              + 2 * 2 * B * (H * H1 + H1 * (Z + E))         # G small layers dW + dX
+              + g_fwd)                                      # eval inference on the same z
+    return d_step, g_step
+
+
+def bench_gan(args):
+    """Config 4: slate_generation.py cGAN, MovieLens-20M, slate_size 5, gan_hidden_layer 256,
+    batch 256, RMSprop (optim_gan default), n_critic 5: one step = one discriminator
+    iteration plus, every 5th step, one generator iteration (CGANs.py:288-301)."""
+    from recommendation_gans_amd.gan_engine import GANBatch, GANEngine
+    from recommendation_gans_amd.spotlight.dnn_models.cGAN_models import discriminator, generator
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    dev = torch.device("cuda:0")
+    B, H, S, E, Z = args.gan_batch, args.gan_hidden, args.gan_slate, args.gan_emb, 100
+    data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
+    N = data.num_items
+    # per-user training lists; the last S items are the user's target slate (create_slates,
+    # dataset_manilupation.py:270-316), the rest the padded history (slate_data_provider.py:226-234)
+    order = np.argsort(data.train_u, kind="stable")
+    uu, ii = data.train_u[order], data.train_i[order]
+    starts = np.searchsorted(uu, np.arange(data.num_users + 1))
+    counts = np.diff(starts)
+    users = np.nonzero(counts > S)[0]
+    L = int((counts[users] - S).max())
+    nb = min(len(users) // B, 40)
+    batches = []
+    for g in range(nb):
+        hist = np.full((B, L), N, np.int64)
+        sl = np.zeros((B, S), np.int64)
+        for r, u in enumerate(users[g * B:(g + 1) * B]):
+            items = ii[starts[u]:starts[u + 1]]
+            hist[r, :len(items) - S] = items[:-S]
+            sl[r] = items[-S:]
+        batches.append(GANBatch(hist, sl, N, S, dev))
+    torch.manual_seed(0)
+    G = generator(num_items=N, noise_dim=Z, embedding_dim=E, hidden_layer=[H // 2, H], output_dim=S)
+    D = discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
+    eng = GANEngine(G.state_dict(), D.state_dict(), N, S, H, E, Z, batch_max=B, optimizer="rms", lr=1e-3, device=dev)
+    del G, D
+    steps = max(5, args.steps // 5 * 5)
+
+    def step(k):
+        bt = batches[k % nb]
+        eng.d_step(bt)
+        if (k + 1) % 5 == 0:
+            eng.g_step(bt, slates=True)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for k in range(steps):
+        step(args.warmup + k)
+    b_.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms_ev = a.elapsed_time(b_)
+    fd, fg = gan_flops(N, S, H, E, Z, B)
+    flops = steps * fd + steps // 5 * fg
+    ach = flops / (ms_ev * 1e-3) / 1e12
+    out = {"metric": "train slates/sec, cGAN slate_size=5 gan_hidden_layer=256 MovieLens-20M (config 4)",
+           "value": steps * B / el, "unit": "slates/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+           "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": f"synthetic ML-20M-shaped histories (N={N}, L_max={L}); reference init",
+           "config": {"workload": f"cGAN G hidden [{H // 2}, {H}], D hidden [{2 * H}, {H}, {H // 2}], S={S}, E={E}, "
+                                  f"z=100, batch {B}, RMSprop lr 1e-3, n_critic 5 (1 D iteration per step, 1 G "
+                                  f"iteration per 5 steps)", "global_batch": B, "parallelism": "dp1"},
+           "roofline": {"bound": "mfma", "kernel": "whole D/G iterations (gemm_kernel + small kernels)",
+                        "achieved": ach, "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / HIDDEN_FP32_MFMA_TFLOPS, "traffic": None,
+                        "algorithmic_flops_per_step": flops / steps, "d_iter_gflop": fd / 1e9,
+                        "g_iter_gflop": fg / 1e9},
+           "cpu_baseline": None,
+           "final": [float(x) for x in eng.d_step(batches[0]).cpu()]}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     if args.model == "ncf":
         return bench_ncf(args)
+    if args.model == "gan":
+        return bench_gan(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

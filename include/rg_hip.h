@@ -401,8 +401,9 @@ typedef struct rg_gan_batch {
     const int32_t *hist_items, *hist_off, *hist_rows;
     int32_t n_hist_items;
     int32_t n_hits;                /* rows * S */
-    /* real-slate columns s*N + slates[b][s], sorted by (column, b), and their rows */
-    const int32_t *hit_col, *hit_row;
+    /* real-slate columns s*N + slates[b][s], sorted by (column, b), and their rows;
+     * hit_tile_off[t] = first hit with column >= 128 t, t = 0 .. ceil(S*N / 128) */
+    const int32_t *hit_col, *hit_row, *hit_tile_off;
 } rg_gan_batch_t;
 
 typedef struct rg_gan_noise {

@@ -107,7 +107,7 @@ class GANBatch(ctypes.Structure):
     _fields_ = [("rows", ctypes.c_int32), ("hist_len", ctypes.c_int32), ("hist", ctypes.c_void_p),
                 ("slates", ctypes.c_void_p), ("hist_items", ctypes.c_void_p), ("hist_off", ctypes.c_void_p),
                 ("hist_rows", ctypes.c_void_p), ("n_hist_items", ctypes.c_int32), ("n_hits", ctypes.c_int32),
-                ("hit_col", ctypes.c_void_p), ("hit_row", ctypes.c_void_p)]
+                ("hit_col", ctypes.c_void_p), ("hit_row", ctypes.c_void_p), ("hit_tile_off", ctypes.c_void_p)]
 
 
 class GANNoise(ctypes.Structure):

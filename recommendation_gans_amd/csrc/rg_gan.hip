@@ -140,19 +140,44 @@ __device__ __forceinline__ float drop_mult(const Drop &q, int64_t row, int64_t u
 __device__ __forceinline__ float lrelu(float x) { return x > 0.0f ? x : x * kSlope; }
 
 // ------------------------------------------------------------------ kernels
-// emb(hist).sum(1): one wave per row, lanes over history slots, fixed-order tree
+constexpr int kEChunk = 8;   // embedding columns accumulated per pass
+
+// fixed-order tree over a block's 256 partials in LDS (all threads call it)
+__device__ __forceinline__ float block_sum256(float v, float *red) {
+    const int t = threadIdx.x;
+    red[t] = v;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// emb(hist).sum(1): one block per row, threads over history slots, fixed-order tree
 __global__ __launch_bounds__(256) void hist_sum_kernel(const float *__restrict__ emb, const int32_t *__restrict__ hist,
                                                        int L, int rows, int E, int pad, float *__restrict__ out) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= rows) return;
-    for (int e = 0; e < E; ++e) {
-        float s = 0.0f;
-        for (int l = lane; l < L; l += 64) {
+    __shared__ float red[256];
+    const int row = blockIdx.x, t = threadIdx.x;
+    for (int e0 = 0; e0 < E; e0 += kEChunk) {
+        float acc[kEChunk];
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) acc[e] = 0.0f;
+        for (int l = t; l < L; l += 256) {
             const int it = hist[(int64_t)row * L + l];
-            if (it != pad) s += emb[(int64_t)it * E + e];
+            if (it == pad) continue;
+#pragma unroll
+            for (int e = 0; e < kEChunk; ++e)
+                if (e0 + e < E) acc[e] += emb[(int64_t)it * E + e0 + e];
         }
-        s = group_sum<64>(s);
-        if (lane == 0) out[(int64_t)row * E + e] = s;
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) {
+            if (e0 + e >= E) break;
+            const float v = block_sum256(acc[e], red);
+            if (t == 0) out[(int64_t)row * E + e0 + e] = v;
+        }
     }
 }
 
@@ -252,7 +277,8 @@ __global__ __launch_bounds__(256) void d_real_l1_kernel(const float *__restrict_
 }
 
 // split-K reduction + bias (+ history-embedding columns of W1) -> Dropout -> LeakyReLU
-__global__ __launch_bounds__(256) void reduce_act_kernel(const float *__restrict__ part, int splits, int rows, int C,
+__global__ __launch_bounds__(256) void reduce_act_kernel(const float *__restrict__ part, int splits, int64_t zstride,
+                                                         int rows, int C,
                                                          const float *__restrict__ bias,
                                                          const float *__restrict__ c, const float *__restrict__ we,
                                                          int E, Drop q, float *__restrict__ u,
@@ -263,7 +289,7 @@ __global__ __launch_bounds__(256) void reduce_act_kernel(const float *__restrict
     const int64_t r = e / C;
     const int un = (int)(e % C);
     float v = 0.0f;
-    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * total + e];
+    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * zstride + e];
     if (we)
         for (int k = 0; k < E; ++k) v = fmaf(we[(int64_t)un * E + k], c[r * E + k], v);
     v += bias[un];
@@ -339,78 +365,157 @@ __global__ __launch_bounds__(256) void d_loss_kernel(const float *__restrict__ d
     }
 }
 
-// backward of the last D layer: dW4 / db4 (column sums weighted by dout, fixed row
-// order) and dl3 = dout * w4 * LeakyReLU'(u3) * mult3
-__global__ __launch_bounds__(256) void d_out_bwd_kernel(const float *__restrict__ h3, const float *__restrict__ u3,
-                                                        const float *__restrict__ q3, const float *__restrict__ dout,
-                                                        int rows, int K, const float *__restrict__ w4,
-                                                        float *__restrict__ gw4, float *__restrict__ gb4,
-                                                        float *__restrict__ dl3) {
+// backward of the last D layer, elementwise: dl3 = dout * w4 * LeakyReLU'(u3) * mult3
+// (dW4 / db4 are weighted column sums: colsum_kernel)
+__global__ __launch_bounds__(256) void d_out_bwd_kernel(const float *__restrict__ u3, const float *__restrict__ q3,
+                                                        const float *__restrict__ dout, int rows, int K,
+                                                        const float *__restrict__ w4, float *__restrict__ dl3) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e < (int64_t)rows * K) {
-        const int k = (int)(e % K);
-        const float v = dout[e / K] * w4[k];
-        dl3[e] = v * (u3[e] > 0.0f ? 1.0f : kSlope) * q3[e];
-    }
-    if (gw4 && blockIdx.x == 0) {
-        for (int k = threadIdx.x; k <= K; k += 256) {
-            float s = 0.0f;
-            for (int r = 0; r < rows; ++r) s = fmaf(dout[r], k < K ? h3[(int64_t)r * K + k] : 1.0f, s);
-            if (k < K) gw4[k] = s;
-            else gb4[0] = s;
-        }
-    }
+    if (e >= (int64_t)rows * K) return;
+    const int k = (int)(e % K);
+    const float v = dout[e / K] * w4[k];
+    dl3[e] = v * (u3[e] > 0.0f ? 1.0f : kSlope) * q3[e];
 }
 
-// out[c] = sum_r X[r][c] in row order (bias gradients)
-__global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ X, int64_t rows, int64_t C,
-                                                     int64_t ld, float *__restrict__ out) {
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+// split-K reduction + bias + post op (small GEMMs split for parallelism)
+__global__ __launch_bounds__(256) void reduce_post_kernel(const float *__restrict__ part, int splits, int64_t M,
+                                                          int64_t N, float *__restrict__ C, int64_t ldc,
+                                                          const float *__restrict__ bias, int post,
+                                                          const float *__restrict__ T, int64_t ldt,
+                                                          const float *__restrict__ Mult) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= M * N) return;
+    const int64_t m = e / N, n = e % N;
+    float v = 0.0f;
+    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * M * N + e];
+    if (bias) v += bias[n];
+    if (post == kPostTanh) {
+        v = tanhf(v);
+    } else if (post == kPostLreluGrad) {
+        v = v * (T[m * ldt + n] > 0.0f ? 1.0f : kSlope);
+        if (Mult) v = v * Mult[m * ldt + n];
+    }
+    C[m * ldc + n] = v;
+}
+
+// out[c] = sum_r w[r] X[r][c] (w null: 1; X null: a column of ones), 64 columns per
+// block, 16 waves over interleaved rows, combined in wave order (deterministic)
+__global__ __launch_bounds__(1024) void colsum_kernel(const float *__restrict__ X, int64_t rows, int64_t C,
+                                                      int64_t ld, const float *__restrict__ w,
+                                                      float *__restrict__ out) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
     float s = 0.0f;
-    for (int64_t r = 0; r < rows; ++r) s += X[r * ld + c];
-    out[c] = s;
+    if (c < C) {
+#pragma unroll 4
+        for (int64_t r = wave; r < rows; r += 16) {
+            const float x = X ? X[r * ld + c] : 1.0f;
+            s = w ? fmaf(w[r], x, s) : s + x;
+        }
+    }
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && c < C) {
+        float v = red[0][lane];
+        for (int k = 1; k < 16; ++k) v += red[k][lane];
+        out[c] = v;
+    }
 }
 
-// D layer 1, history columns: dW1e[u][e] = sum_r dl1[r][u] c[r mod B][e] (real rows, then
-// fake rows) and dc[b][e] = dl1_real[b] . W1e[:, e] + dl1_fake[b] . W1e[:, e]
-__global__ __launch_bounds__(256) void d_l1_emb_grad_kernel(const float *__restrict__ dl1, int B, int H2,
-                                                            const float *__restrict__ c, int E,
-                                                            const float *__restrict__ w1e,
-                                                            float *__restrict__ gw1e, float *__restrict__ dc) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t < (int64_t)H2 * E) {
-        const int un = (int)(t / E), e = (int)(t % E);
-        float s = 0.0f;
-        for (int r = 0; r < 2 * B; ++r) s = fmaf(dl1[(int64_t)r * H2 + un], c[(int64_t)(r % B) * E + e], s);
-        gw1e[t] = s;
-    }
-    const int64_t t2 = t - (int64_t)H2 * E;
-    if (t2 >= 0 && t2 < (int64_t)B * E) {
-        const int b = (int)(t2 / E), e = (int)(t2 % E);
-        float sr = 0.0f, sf = 0.0f;
-        for (int un = 0; un < H2; ++un) {
-            const float w = fminf(fmaxf(w1e[(int64_t)un * E + e], -kClamp), kClamp);
-            sr = fmaf(dl1[(int64_t)b * H2 + un], w, sr);
-            sf = fmaf(dl1[(int64_t)(B + b) * H2 + un], w, sf);
+// D layer 1, history columns: dW1e[u][e] = sum_r dl1[r][u] c[r mod B][e] over the 2B
+// stacked rows (real, then fake); 64 units per block, 16 waves over rows
+__global__ __launch_bounds__(1024) void d_l1_w1e_grad_kernel(const float *__restrict__ dl1, int B, int H2,
+                                                             const float *__restrict__ c, int E,
+                                                             float *__restrict__ gw1e) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int un = blockIdx.x * 64 + lane;
+    for (int e0 = 0; e0 < E; e0 += kEChunk) {
+        float acc[kEChunk];
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) acc[e] = 0.0f;
+        if (un < H2)
+            for (int r = wave; r < 2 * B; r += 16) {
+                const float g = dl1[(int64_t)r * H2 + un];
+                const float *cr = c + (int64_t)(r % B) * E + e0;
+#pragma unroll
+                for (int e = 0; e < kEChunk; ++e)
+                    if (e0 + e < E) acc[e] = fmaf(g, cr[e], acc[e]);
+            }
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) {
+            if (e0 + e >= E) break;
+            red[wave][lane] = acc[e];
+            __syncthreads();
+            if (wave == 0 && un < H2) {
+                float v = red[0][lane];
+                for (int k = 1; k < 16; ++k) v += red[k][lane];
+                gw1e[(int64_t)un * E + e0 + e] = v;
+            }
+            __syncthreads();
         }
-        dc[t2] = sr + sf;
+    }
+}
+
+// dc[b][e] = dl1_real[b] . W1e[:, e] + dl1_fake[b] . W1e[:, e] (each pass its own sum, as
+// autograd accumulates the two embedding lookups); one block per row
+__global__ __launch_bounds__(256) void d_l1_dc_kernel(const float *__restrict__ dl1, int B, int H2, int E,
+                                                      const float *__restrict__ w1e, float *__restrict__ dc) {
+    __shared__ float red[256];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int e0 = 0; e0 < E; e0 += kEChunk) {
+        float ar[kEChunk], af[kEChunk];
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) ar[e] = af[e] = 0.0f;
+        for (int un = t; un < H2; un += 256) {
+            const float gr = dl1[(int64_t)b * H2 + un], gf = dl1[(int64_t)(B + b) * H2 + un];
+#pragma unroll
+            for (int e = 0; e < kEChunk; ++e)
+                if (e0 + e < E) {
+                    const float w = w1e[(int64_t)un * E + e0 + e];
+                    ar[e] = fmaf(gr, w, ar[e]);
+                    af[e] = fmaf(gf, w, af[e]);
+                }
+        }
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) {
+            if (e0 + e >= E) break;
+            const float sr = block_sum256(ar[e], red);
+            const float sf = block_sum256(af[e], red);
+            if (t == 0) dc[(int64_t)b * E + e0 + e] = sr + sf;
+        }
     }
 }
 
 // embedding backward with padding_idx: grad[item] = sum over the batch rows whose
-// history holds it (grouped host-side, fixed order) of src[row]
+// history holds it (grouped host-side) of src[row]; one wave per item, lanes over its
+// rows, fixed-order DPP tree
 __global__ __launch_bounds__(256) void emb_grad_kernel(const int32_t *__restrict__ items,
                                                        const int32_t *__restrict__ off,
                                                        const int32_t *__restrict__ brow, int n_items,
                                                        const float *__restrict__ src, int64_t src_ld, int E,
                                                        float *__restrict__ grad) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (int64_t)n_items * E) return;
-    const int i = (int)(t / E), e = (int)(t % E);
-    float s = 0.0f;
-    for (int j = off[i]; j < off[i + 1]; ++j) s += src[(int64_t)brow[j] * src_ld + e];
-    grad[(int64_t)items[i] * E + e] = s;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= n_items) return;
+    const int j0 = off[i], j1 = off[i + 1];
+    for (int e0 = 0; e0 < E; e0 += kEChunk) {
+        float acc[kEChunk];
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) acc[e] = 0.0f;
+        for (int j = j0 + lane; j < j1; j += 64) {
+            const float *sr = src + (int64_t)brow[j] * src_ld + e0;
+#pragma unroll
+            for (int e = 0; e < kEChunk; ++e)
+                if (e0 + e < E) acc[e] += sr[e];
+        }
+#pragma unroll
+        for (int e = 0; e < kEChunk; ++e) {
+            if (e0 + e >= E) break;
+            const float v = group_sum<64>(acc[e]);
+            if (lane == 0) grad[(int64_t)items[i] * E + e0 + e] = v;
+        }
+    }
 }
 
 // BatchNorm backward per channel (train mode): do = dL/d(gamma*yhat+beta) after the
@@ -484,24 +589,29 @@ __global__ __launch_bounds__(256) void opt_flat_kernel(float *__restrict__ p, co
     if (v) v[e] = vv;
 }
 
-// per (row, head): best (value, index) over the column tiles overlapping the head,
-// in column order (first maximum, as torch.max)
+// per (row, head): best (value, index) over the column tiles overlapping the head
+// (first maximum, as torch.max): one wave per (row, head), lanes over tiles
 __global__ __launch_bounds__(256) void argmax_final_kernel(const float2 *__restrict__ amax, int rows, int64_t ntile,
                                                            int S, int64_t N, float *__restrict__ slates) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (t >= (int64_t)rows * S) return;
     const int64_t m = t / S;
     const int s = (int)(t % S);
     const int64_t c0 = (int64_t)s * N, c1 = c0 + N;
+    const int64_t t0 = c0 / kGemmBN, t1 = std::min<int64_t>((c1 + kGemmBN - 1) / kGemmBN, ntile);
     float bv = -INFINITY, bi = INFINITY;
-    for (int64_t tile = c0 / kGemmBN; tile * kGemmBN < c1 && tile < ntile; ++tile) {
-        const int64_t h0 = tile * kGemmBN / N;
-        const int seg = (int)(s - h0);
+    for (int64_t tile = t0 + lane; tile < t1; tile += 64) {
+        const int seg = (int)(s - tile * kGemmBN / N);
         if (seg < 0 || seg > 1) continue;
         const float2 o = amax[(m * ntile + tile) * 2 + seg];
         if (o.x > bv || (o.x == bv && o.y < bi)) { bv = o.x; bi = o.y; }
     }
-    slates[t] = bi;
+    for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(bv, off), oi = __shfl_xor(bi, off);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) slates[t] = bi;
 }
 
 // per (row, head): first maximum of the tanh outputs T[row][s*N .. (s+1)*N) (heads
@@ -521,6 +631,39 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const float *__restric
 }
 
 unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+void colsum(hipStream_t st, const float *X, int64_t rows, int64_t C, int64_t ld, const float *w, float *out) {
+    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((C + 63) / 64)), dim3(1024), 0, st, X, rows, C, ld, w, out);
+}
+
+void hist_sum(hipStream_t st, const float *emb, const rg_gan_batch_t *bt, int rows, int E, int pad, float *out) {
+    hipLaunchKernelGGL(hist_sum_kernel, dim3(rows), dim3(256), 0, st, emb, bt->hist, bt->hist_len, rows, E, pad, out);
+}
+
+void emb_grad(hipStream_t st, const rg_gan_batch_t *bt, const float *src, int64_t ld, int E, float *grad) {
+    if (bt->n_hist_items <= 0) return;
+    hipLaunchKernelGGL(emb_grad_kernel, dim3((unsigned)((bt->n_hist_items + 3) / 4)), dim3(256), 0, st,
+                       bt->hist_items, bt->hist_off, bt->hist_rows, bt->n_hist_items, src, ld, E, grad);
+}
+
+// a GEMM with few output tiles (the small layers): split K over more workgroups and
+// reduce in split order with the same bias / post op
+int gemm_small(hipStream_t st, GemmDesc d, float *part) {
+    const int64_t tiles = gemm_tiles_m(d.M) * gemm_tiles_n(d.N);
+    int splits = (int)std::min<int64_t>(std::max<int64_t>(1, 64 / tiles), std::max<int64_t>(1, d.K / 64));
+    if (d.epi != kEpiStore || d.post == kPostTanhGrad || splits <= 1) return gemm(st, d);
+    GemmDesc p = d;
+    p.epi = kEpiPartial;
+    p.splits = splits;
+    p.C = part;
+    p.bias = nullptr;
+    p.post = kPostNone;
+    const int rc = gemm(st, p);
+    if (rc) return rc;
+    hipLaunchKernelGGL(reduce_post_kernel, dim3(blocks(d.M * d.N)), dim3(256), 0, st, part, splits, d.M, d.N, d.C,
+                       d.ldc, d.bias, d.post, d.T, d.ldt, d.Mult);
+    return check_launch("reduce_post_kernel");
+}
 
 int pick_splits(int64_t M, int64_t N, int64_t K) {
     const int64_t tiles = gemm_tiles_m(M) * gemm_tiles_n(N);
@@ -563,8 +706,7 @@ int g_forward(const Ctx &x, const rg_gan_model_t *mdl, const rg_gan_batch_t *bt,
     const Dims &m = x.m;
     const int rows = bt->rows;
     float *G = mdl->g;
-    hipLaunchKernelGGL(hist_sum_kernel, dim3((rows + 3) / 4), dim3(256), 0, x.st, G + x.go[RG_GAN_G_EMB], bt->hist,
-                       bt->hist_len, rows, (int)m.E, (int)m.N, x.f(x.w.cg));
+    hist_sum(x.st, G + x.go[RG_GAN_G_EMB], bt, rows, (int)m.E, (int)m.N, x.f(x.w.cg));
     hipLaunchKernelGGL(g_input_kernel, dim3(blocks((int64_t)rows * m.kz)), dim3(256), 0, x.st, z, (int)m.Z,
                        x.f(x.w.cg), (int)m.E, rows, (int)m.kz, x.f(x.w.a0));
     // layer 1
@@ -573,7 +715,7 @@ int g_forward(const Ctx &x, const rg_gan_model_t *mdl, const rg_gan_batch_t *bt,
     d.B = G + x.go[RG_GAN_G_W1]; d.ldb = m.kz;
     d.M = rows; d.N = m.H1; d.K = m.kz;
     d.C = x.f(x.w.y1); d.ldc = m.H1; d.bias = G + x.go[RG_GAN_G_B1];
-    RG_TRY(gemm(x.st, d));
+    RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     Drop q1 = make_drop(nz, slot0, m.H1, kDropG, 0);
     q1.train = train ? 1 : 0;
     // running stats: eval reads them; train updates them (the reference's every train-mode forward)
@@ -588,7 +730,7 @@ int g_forward(const Ctx &x, const rg_gan_model_t *mdl, const rg_gan_batch_t *bt,
     d.B = G + x.go[RG_GAN_G_W2]; d.ldb = m.H1;
     d.M = rows; d.N = m.H; d.K = m.H1;
     d.C = x.f(x.w.y2); d.ldc = m.H; d.bias = G + x.go[RG_GAN_G_B2];
-    RG_TRY(gemm(x.st, d));
+    RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     Drop q2 = make_drop(nz, slot0 + 1, m.H, kDropG, 0);
     q2.train = train ? 1 : 0;
     hipLaunchKernelGGL(bn_fwd_kernel, dim3((unsigned)m.H), dim3(256), 0, x.st, x.f(x.w.y2), rows, (int)m.H,
@@ -624,16 +766,18 @@ int d_upper_forward(const Ctx &x, const rg_gan_model_t *mdl, int rows, const Dro
         d.A = x.f(hin[k]); d.lda = in[k];
         d.B = D + x.dof[wblk[k]]; d.ldb = in[k];
         d.M = rows; d.N = out[k]; d.K = in[k];
-        d.epi = kEpiPartial; d.splits = 1; d.C = x.f(x.w.part);
-        RG_TRY(gemm(x.st, d));
+        const int64_t tiles = gemm_tiles_m(rows) * gemm_tiles_n(out[k]);
+        d.epi = kEpiPartial; d.C = x.f(x.w.part);
+        d.splits = (int)std::min<int64_t>(std::max<int64_t>(1, 64 / tiles), std::max<int64_t>(1, in[k] / 64));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
         // per pass (real / fake rows have their own dropout draws)
         for (int p = 0; p < n_pass; ++p) {
             const Drop &q = k == 0 ? qs2[p] : qs3[p];
             const int64_t r0 = (int64_t)p * B;
             hipLaunchKernelGGL(reduce_act_kernel, dim3(blocks((int64_t)B * out[k])), dim3(256), 0, x.st,
-                               x.f(x.w.part) + r0 * out[k], 1, B, (int)out[k], D + x.dof[bblk[k]], nullptr,
-                               nullptr, 0, q, x.f(uout[k]) + r0 * out[k], x.f(hout[k]) + r0 * out[k],
-                               x.f(qout[k]) + r0 * out[k]);
+                               x.f(x.w.part) + r0 * out[k], d.splits, (int64_t)rows * out[k], B, (int)out[k],
+                               D + x.dof[bblk[k]], nullptr, nullptr, 0, q, x.f(uout[k]) + r0 * out[k],
+                               x.f(hout[k]) + r0 * out[k], x.f(qout[k]) + r0 * out[k]);
         }
     }
     hipLaunchKernelGGL(d_out_kernel, dim3((rows + 3) / 4), dim3(256), 0, x.st, x.f(x.w.h3), rows, (int)m.H1,
@@ -646,9 +790,12 @@ int d_upper_backward(const Ctx &x, const rg_gan_model_t *mdl, int rows, float *d
     const Dims &m = x.m;
     float *D = mdl->d;
     auto gslot = [&](int blk) { return dgrad ? dgrad + (x.dof[blk] - x.dof[RG_GAN_D_EMB]) : nullptr; };
-    hipLaunchKernelGGL(d_out_bwd_kernel, dim3(blocks((int64_t)rows * m.H1)), dim3(256), 0, x.st, x.f(x.w.h3),
-                       x.f(x.w.u3), x.f(x.w.q3), x.f(x.w.dout), rows, (int)m.H1, D + x.dof[RG_GAN_D_W4],
-                       gslot(RG_GAN_D_W4), gslot(RG_GAN_D_B4), x.f(x.w.dl3));
+    hipLaunchKernelGGL(d_out_bwd_kernel, dim3(blocks((int64_t)rows * m.H1)), dim3(256), 0, x.st, x.f(x.w.u3),
+                       x.f(x.w.q3), x.f(x.w.dout), rows, (int)m.H1, D + x.dof[RG_GAN_D_W4], x.f(x.w.dl3));
+    if (dgrad) {
+        colsum(x.st, x.f(x.w.h3), rows, m.H1, m.H1, x.f(x.w.dout), gslot(RG_GAN_D_W4));
+        colsum(x.st, nullptr, rows, 1, 1, x.f(x.w.dout), gslot(RG_GAN_D_B4));
+    }
     const int64_t in[2] = {m.H, m.H2}, out[2] = {m.H1, m.H};      // layer 3 then layer 2
     const int64_t wblk[2] = {RG_GAN_D_W3, RG_GAN_D_W2}, bblk[2] = {RG_GAN_D_B3, RG_GAN_D_B2};
     const int64_t dl[2] = {x.w.dl3, x.w.dl2}, dlin[2] = {x.w.dl2, x.w.dl1}, hin[2] = {x.w.h2, x.w.h1},
@@ -661,9 +808,8 @@ int d_upper_backward(const Ctx &x, const rg_gan_model_t *mdl, int rows, float *d
             d.B = x.f(hin[k]); d.ldb = in[k]; d.b_kmajor = false;
             d.M = out[k]; d.N = in[k]; d.K = rows;
             d.C = gslot(wblk[k]); d.ldc = in[k];
-            RG_TRY(gemm(x.st, d));
-            hipLaunchKernelGGL(colsum_kernel, dim3(blocks(out[k])), dim3(256), 0, x.st, x.f(dl[k]), (int64_t)rows,
-                               out[k], out[k], gslot(bblk[k]));
+            RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
+            colsum(x.st, x.f(dl[k]), rows, out[k], out[k], nullptr, gslot(bblk[k]));
         }
         // dh_in = dl W, then * LeakyReLU'(u_in) * mult_in
         GemmDesc d;
@@ -672,7 +818,7 @@ int d_upper_backward(const Ctx &x, const rg_gan_model_t *mdl, int rows, float *d
         d.M = rows; d.N = in[k]; d.K = out[k];
         d.C = x.f(dlin[k]); d.ldc = in[k];
         d.post = kPostLreluGrad; d.T = x.f(uin[k]); d.ldt = in[k]; d.Mult = x.f(qin[k]);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     }
     return check_launch("d_upper_backward");
 }
@@ -727,7 +873,7 @@ extern "C" int64_t rg_gan_workspace_offset(const rg_gan_dims_t *dims, int32_t vi
 extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *workspace, const rg_gan_batch_t *bt,
                              const rg_gan_noise_t *nz, const rg_opt_t *opt, float *out) {
     RG_TRY(check_common(mdl, workspace, bt));
-    if (!bt->slates || !bt->hit_col || !bt->hit_row || !nz || !nz->z || !opt || !out)
+    if (!bt->slates || !bt->hit_col || !bt->hit_row || !bt->hit_tile_off || !nz || !nz->z || !opt || !out)
         return fail_arg("rg_gan_d_step: slates, hits, noise, opt and out are required");
     const Dims m(mdl->dims);
     if (bt->n_hits != bt->rows * m.S) return fail_arg("rg_gan_d_step: n_hits != rows * S");
@@ -744,8 +890,7 @@ extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *work
     //    optimizer epilogue before its update), so it is never rewritten just for this
     hipLaunchKernelGGL(clamp_kernel, dim3(blocks(small_n)), dim3(256), 0, x.st, D + small0, small_n, kClamp);
     // 2. D(real): history sums, sparse layer 1 (rows [0, B))
-    hipLaunchKernelGGL(hist_sum_kernel, dim3((B + 3) / 4), dim3(256), 0, x.st, D + dof[RG_GAN_D_EMB], bt->hist,
-                       bt->hist_len, B, (int)m.E, (int)m.N, x.f(w.cd));
+    hist_sum(x.st, D + dof[RG_GAN_D_EMB], bt, B, (int)m.E, (int)m.N, x.f(w.cd));
     const Drop qr1 = make_drop(nz, 0, m.H2, kDropD, 0);
     hipLaunchKernelGGL(d_real_l1_kernel, dim3(B), dim3(256), 0, x.st, D + dof[RG_GAN_D_W1S], m.ks,
                        D + dof[RG_GAN_D_W1E], D + dof[RG_GAN_D_B1], x.f(w.cd), (int)m.E, bt->slates, (int)m.S, m.N,
@@ -760,11 +905,11 @@ extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.B = D + dof[RG_GAN_D_W1S]; d.ldb = m.ks; d.clamp_b = kClamp;
         d.M = B; d.N = m.H2; d.K = m.ks;    // pad columns of fake and W1S are zero
         d.epi = kEpiPartial; d.splits = pick_splits(B, m.H2, m.ks); d.C = x.f(w.part);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
         const Drop qf1 = make_drop(nz, 5, m.H2, kDropD, 0);
         hipLaunchKernelGGL(reduce_act_kernel, dim3(blocks((int64_t)B * m.H2)), dim3(256), 0, x.st, x.f(w.part),
-                           d.splits, B, (int)m.H2, D + dof[RG_GAN_D_B1], x.f(w.cd), D + dof[RG_GAN_D_W1E],
-                           (int)m.E, qf1, x.f(w.u1) + (int64_t)B * m.H2, x.f(w.h1) + (int64_t)B * m.H2,
+                           d.splits, (int64_t)B * m.H2, B, (int)m.H2, D + dof[RG_GAN_D_B1], x.f(w.cd),
+                           D + dof[RG_GAN_D_W1E], (int)m.E, qf1, x.f(w.u1) + (int64_t)B * m.H2, x.f(w.h1) + (int64_t)B * m.H2,
                            x.f(w.q1) + (int64_t)B * m.H2);
     }
     // 5. layers 2..4 on the stacked [real; fake] rows, losses
@@ -775,15 +920,12 @@ extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *work
     // 6. backward: small-parameter gradients, dl1 for both passes
     hipMemsetAsync(dgrad, 0, (size_t)small_n * 4, x.st);
     RG_TRY(d_upper_backward(x, mdl, 2 * B, dgrad));
-    hipLaunchKernelGGL(colsum_kernel, dim3(blocks(m.H2)), dim3(256), 0, x.st, x.f(w.dl1), (int64_t)2 * B, m.H2,
-                       m.H2, dgrad + (dof[RG_GAN_D_B1] - small0));
-    hipLaunchKernelGGL(d_l1_emb_grad_kernel, dim3(blocks(m.H2 * m.E + (int64_t)B * m.E)), dim3(256), 0, x.st,
-                       x.f(w.dl1), B, (int)m.H2, x.f(w.cd), (int)m.E, D + dof[RG_GAN_D_W1E],
-                       dgrad + (dof[RG_GAN_D_W1E] - small0), x.f(w.dc));
-    if (bt->n_hist_items > 0)
-        hipLaunchKernelGGL(emb_grad_kernel, dim3(blocks((int64_t)bt->n_hist_items * m.E)), dim3(256), 0, x.st,
-                           bt->hist_items, bt->hist_off, bt->hist_rows, bt->n_hist_items, x.f(w.dc), m.E, (int)m.E,
-                           dgrad);
+    colsum(x.st, x.f(w.dl1), 2 * B, m.H2, m.H2, nullptr, dgrad + (dof[RG_GAN_D_B1] - small0));
+    hipLaunchKernelGGL(d_l1_w1e_grad_kernel, dim3((unsigned)((m.H2 + 63) / 64)), dim3(1024), 0, x.st, x.f(w.dl1), B,
+                       (int)m.H2, x.f(w.cd), (int)m.E, dgrad + (dof[RG_GAN_D_W1E] - small0));
+    hipLaunchKernelGGL(d_l1_dc_kernel, dim3(B), dim3(256), 0, x.st, x.f(w.dl1), B, (int)m.H2, (int)m.E,
+                       D + dof[RG_GAN_D_W1E], x.f(w.dc));
+    emb_grad(x.st, bt, x.f(w.dc), m.E, (int)m.E, dgrad);
     // 7. W1S: gradient GEMM over the fake rows + the real rows' sparse column hits,
     //    fused with clamp + optimizer update in place
     {
@@ -796,9 +938,9 @@ extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.Ms = mdl->d_m ? mdl->d_m + dof[RG_GAN_D_W1S] : nullptr;
         d.Vs = mdl->d_v ? mdl->d_v + dof[RG_GAN_D_W1S] : nullptr;
         d.opt = *opt; d.clamp_p = kClamp;
-        d.hit_col = bt->hit_col; d.hit_row = bt->hit_row; d.n_hits = bt->n_hits;
+        d.hit_col = bt->hit_col; d.hit_row = bt->hit_row; d.n_hits = bt->n_hits; d.hit_tile_off = bt->hit_tile_off;
         d.hit_src = x.f(w.dl1); d.hit_ld = m.H2;
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     }
     // 8. the small D parameters (clamped above)
     hipLaunchKernelGGL(opt_flat_kernel, dim3(blocks(small_n)), dim3(256), 0, x.st, D + small0, dgrad,
@@ -824,19 +966,18 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
     // 1. fake = G(z) (train), D(fake) with D frozen and in train mode (dropout slots 2..4)
     RG_TRY(g_forward(x, mdl, bt, nz->z, nz, 0, true, true));
     RG_TRY(g_heads(x, mdl, B));
-    hipLaunchKernelGGL(hist_sum_kernel, dim3((B + 3) / 4), dim3(256), 0, x.st, D + dof[RG_GAN_D_EMB], bt->hist,
-                       bt->hist_len, B, (int)m.E, (int)m.N, x.f(w.cd));
+    hist_sum(x.st, D + dof[RG_GAN_D_EMB], bt, B, (int)m.E, (int)m.N, x.f(w.cd));
     {
         GemmDesc d;
         d.A = x.f(w.fake); d.lda = m.ks;
         d.B = D + dof[RG_GAN_D_W1S]; d.ldb = m.ks;
         d.M = B; d.N = m.H2; d.K = m.ks;
         d.epi = kEpiPartial; d.splits = pick_splits(B, m.H2, m.ks); d.C = x.f(w.part);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
         const Drop q1 = make_drop(nz, 2, m.H2, kDropD, 8);
         hipLaunchKernelGGL(reduce_act_kernel, dim3(blocks((int64_t)B * m.H2)), dim3(256), 0, x.st, x.f(w.part),
-                           d.splits, B, (int)m.H2, D + dof[RG_GAN_D_B1], x.f(w.cd), D + dof[RG_GAN_D_W1E],
-                           (int)m.E, q1, x.f(w.u1), x.f(w.h1), x.f(w.q1));
+                           d.splits, (int64_t)B * m.H2, B, (int)m.H2, D + dof[RG_GAN_D_B1], x.f(w.cd),
+                           D + dof[RG_GAN_D_W1E], (int)m.E, q1, x.f(w.u1), x.f(w.h1), x.f(w.q1));
     }
     const Drop q2 = make_drop(nz, 3, m.H, kDropD, 8), q3 = make_drop(nz, 4, m.H1, kDropD, 8);
     RG_TRY(d_upper_forward(x, mdl, B, &q2, &q3, 1, B));
@@ -851,7 +992,7 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.M = B; d.N = m.SN; d.K = m.H2;
         d.C = x.f(w.dlogit); d.ldc = m.ks;
         d.post = kPostTanhGrad; d.T = x.f(w.fake); d.ldt = m.ks; d.colsum = x.f(w.colsum);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
         hipLaunchKernelGGL(sum_rows_kernel, dim3(blocks(m.SN)), dim3(256), 0, x.st, x.f(w.colsum),
                            (int)gemm_tiles_m(B), m.SN, m.SN, gslot(RG_GAN_G_BH));
     }
@@ -862,7 +1003,7 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.B = G + go[RG_GAN_G_WH]; d.ldb = m.H; d.b_kmajor = false;
         d.M = B; d.N = m.H; d.K = m.ks;     // pad columns of dlogit and pad rows of WH are zero
         d.epi = kEpiPartial; d.splits = pick_splits(B, m.H, m.ks); d.C = x.f(w.part);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
         hipLaunchKernelGGL(reduce_lrelu_grad_kernel, dim3(blocks((int64_t)B * m.H)), dim3(256), 0, x.st,
                            x.f(w.part), d.splits, (int64_t)B * m.H, x.f(w.d2), x.f(w.q2g), x.f(w.do2));
     }
@@ -877,7 +1018,7 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.Ms = mdl->g_m ? mdl->g_m + go[RG_GAN_G_WH] : nullptr;
         d.Vs = mdl->g_v ? mdl->g_v + go[RG_GAN_G_WH] : nullptr;
         d.opt = *opt;
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     }
     // 5. BatchNorm 2 backward, layer 2 weights, back through layer 1
     hipLaunchKernelGGL(bn_bwd_kernel, dim3((unsigned)m.H), dim3(256), 0, x.st, x.f(w.do2), x.f(w.yh2), x.f(w.rs2),
@@ -889,16 +1030,15 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.B = x.f(w.a1); d.ldb = m.H1; d.b_kmajor = false;
         d.M = m.H; d.N = m.H1; d.K = B;
         d.C = gslot(RG_GAN_G_W2); d.ldc = m.H1;
-        RG_TRY(gemm(x.st, d));
-        hipLaunchKernelGGL(colsum_kernel, dim3(blocks(m.H)), dim3(256), 0, x.st, x.f(w.dy2), (int64_t)B, m.H, m.H,
-                           gslot(RG_GAN_G_B2));
+        RG_TRY(gemm_small(x.st, d, x.f(w.part)));
+        colsum(x.st, x.f(w.dy2), B, m.H, m.H, nullptr, gslot(RG_GAN_G_B2));
         d = GemmDesc();  // do1 = (dy2 W2) * LeakyReLU'(d1) * mult1
         d.A = x.f(w.dy2); d.lda = m.H;
         d.B = G + go[RG_GAN_G_W2]; d.ldb = m.H1; d.b_kmajor = false;
         d.M = B; d.N = m.H1; d.K = m.H;
         d.C = x.f(w.do1); d.ldc = m.H1;
         d.post = kPostLreluGrad; d.T = x.f(w.d1); d.ldt = m.H1; d.Mult = x.f(w.q1g);
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     }
     hipLaunchKernelGGL(bn_bwd_kernel, dim3((unsigned)m.H1), dim3(256), 0, x.st, x.f(w.do1), x.f(w.yh1), x.f(w.rs1),
                        G + go[RG_GAN_G_GAMMA1], B, (int)m.H1, gslot(RG_GAN_G_GAMMA1), gslot(RG_GAN_G_BETA1),
@@ -909,22 +1049,18 @@ extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *work
         d.B = x.f(w.a0); d.ldb = m.kz; d.b_kmajor = false;
         d.M = m.H1; d.N = m.kz; d.K = B;
         d.C = gslot(RG_GAN_G_W1); d.ldc = m.kz;
-        RG_TRY(gemm(x.st, d));
-        hipLaunchKernelGGL(colsum_kernel, dim3(blocks(m.H1)), dim3(256), 0, x.st, x.f(w.dy1), (int64_t)B, m.H1, m.H1,
-                           gslot(RG_GAN_G_B1));
+        RG_TRY(gemm_small(x.st, d, x.f(w.part)));
+        colsum(x.st, x.f(w.dy1), B, m.H1, m.H1, nullptr, gslot(RG_GAN_G_B1));
         d = GemmDesc();  // dx0 = (dy1 W1) * LeakyReLU'(x0)  (a0 > 0 iff x0 > 0)
         d.A = x.f(w.dy1); d.lda = m.H1;
         d.B = G + go[RG_GAN_G_W1]; d.ldb = m.kz; d.b_kmajor = false;
         d.M = B; d.N = m.kz; d.K = m.H1;
         d.C = x.f(w.dx0); d.ldc = m.kz;
         d.post = kPostLreluGrad; d.T = x.f(w.a0); d.ldt = m.kz;
-        RG_TRY(gemm(x.st, d));
+        RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
     }
     // 6. history embedding of G: the e columns of dx0, grouped per item
-    if (bt->n_hist_items > 0)
-        hipLaunchKernelGGL(emb_grad_kernel, dim3(blocks((int64_t)bt->n_hist_items * m.E)), dim3(256), 0, x.st,
-                           bt->hist_items, bt->hist_off, bt->hist_rows, bt->n_hist_items, x.f(w.dx0) + m.Z, m.kz,
-                           (int)m.E, gslot(RG_GAN_G_EMB));
+    emb_grad(x.st, bt, x.f(w.dx0) + m.Z, m.kz, (int)m.E, gslot(RG_GAN_G_EMB));
     // 7. the remaining G parameters
     hipLaunchKernelGGL(opt_flat_kernel, dim3(blocks(small_n)), dim3(256), 0, x.st, G + small0, ggrad,
                        mdl->g_m ? mdl->g_m + small0 : nullptr, mdl->g_v ? mdl->g_v + small0 : nullptr, small_n,
@@ -957,8 +1093,8 @@ extern "C" int rg_gan_generate(void *stream, const rg_gan_model_t *mdl, void *wo
     d.M = B; d.N = m.SN; d.K = m.H;
     d.epi = kEpiArgmax; d.bias = mdl->g + go[RG_GAN_G_BH]; d.seg = m.N;
     d.amax = reinterpret_cast<float2 *>(x.f(w.amax));
-    RG_TRY(gemm(x.st, d));
-    hipLaunchKernelGGL(argmax_final_kernel, dim3(blocks((int64_t)B * m.S)), dim3(256), 0, x.st, d.amax, B,
+    RG_TRY(gemm_small(x.st, d, x.f(x.w.part)));
+    hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)(((int64_t)B * m.S + 3) / 4)), dim3(256), 0, x.st, d.amax, B,
                        gemm_tiles_n(m.SN), (int)m.S, m.N, slates);
     return check_launch("rg_gan_generate");
 }

@@ -8,6 +8,8 @@
 // dimension and K are multiples of 4 and base pointers are 16-B aligned (the
 // launcher checks), so a float4 is either wholly inside or wholly outside.
 #pragma once
+#include <algorithm>
+
 #include "rg_common.h"
 
 namespace rg {
@@ -56,6 +58,7 @@ struct GemmDesc {
     // sparse extra rows of the gradient: hit h adds hit_src[hit_row[h] * hit_ld + m] to
     // column hit_col[h] (hits sorted by column, then row)
     const int32_t *hit_col = nullptr, *hit_row = nullptr;
+    const int32_t *hit_tile_off = nullptr;   // [column tiles + 1]: hits of tile t are [off[t], off[t+1])
     int32_t n_hits = 0;
     const float *hit_src = nullptr;
     int64_t hit_ld = 0;

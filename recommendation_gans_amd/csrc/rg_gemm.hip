@@ -87,19 +87,56 @@ __device__ __forceinline__ void frag(float (&f)[16], const float *s, int row, in
     }
 }
 
+struct TileMap {
+    int64_t tm, tn, t_small, t_big, tg, nbb, gsize, groups;
+    bool m_small;
+    __host__ __device__ explicit TileMap(const GemmDesc &d) {
+        tm = gemm_tiles_m(d.M);
+        tn = gemm_tiles_n(d.N);
+        m_small = tm <= tn;
+        t_small = m_small ? tm : tn;
+        t_big = m_small ? tn : tm;
+        tg = t_small >= 16 ? 1 : 16 / t_small;
+        if (tg > t_big) tg = t_big;
+        nbb = (t_big + tg - 1) / tg;
+        gsize = tg * t_small;
+        groups = d.splits * nbb;
+    }
+    __host__ __device__ int64_t blocks() const { return 8 * gsize * ((groups + 7) / 8); }
+    __device__ bool decode(int64_t L, int64_t &mt, int64_t &nt, int64_t &z) const {
+        const int64_t local = L >> 3, w = local % gsize, P = (local / gsize) * 8 + (L & 7);
+        if (P >= groups) return false;
+        z = P / nbb;
+        const int64_t major = (P % nbb) * tg + w / t_small, minor = w % t_small;
+        if (major >= t_big) return false;
+        mt = m_small ? minor : major;
+        nt = m_small ? major : minor;
+        return true;
+    }
+};
+
 __device__ __forceinline__ bool better(float v, float i, float bv, float bi) {
     return v > bv || (v == bv && i < bi);
 }
 
 template <bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
-    __shared__ __attribute__((aligned(16))) float sA[2][Stage<AK>::kFloats];
-    __shared__ __attribute__((aligned(16))) float sB[2][Stage<BKM>::kFloats];
+    constexpr int kSA = Stage<AK>::kFloats, kSB = Stage<BKM>::kFloats;
+    __shared__ __attribute__((aligned(16))) float smem[2 * kSA + 2 * kSB];
+    auto sA = [&](int b) { return smem + b * kSA; };
+    auto sB = [&](int b) { return smem + 2 * kSA + b * kSB; };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
     const int h = lane >> 5, l32 = lane & 31;
-    const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+    // XCD-aware order (blocks L, L + 8, L + 16, ... share an XCD and its L2): tiles are
+    // grouped as (split z, block of tg long-dimension tiles) x every short-dimension
+    // tile; a group's blocks run consecutively on one XCD, so the group's A and B
+    // panels (for this K chunk) come from HBM once and are reused from L2
+    const TileMap tmap(d);
+    int64_t mt, nt, zz;
+    if (!tmap.decode(blockIdx.x, mt, nt, zz)) return;
+    const int64_t m0 = mt * BM, n0 = nt * BN;
     const int64_t kc = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
-    const int64_t k_begin = (int64_t)blockIdx.z * kc, k_end = min(d.K, k_begin + kc);
+    const int64_t k_begin = zz * kc, k_end = min(d.K, k_begin + kc);
     const int nk = k_end > k_begin ? (int)((k_end - k_begin + BK - 1) / BK) : 0;
 
     v16f acc[2][2];
@@ -114,8 +151,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
     if (nk > 0) {
         gload<AK>(ra, d.A, d.lda, m0, d.M, k_begin, k_end, 0.0f, tid);
         gload<BKM>(rb, d.B, d.ldb, n0, d.N, k_begin, k_end, d.clamp_b, tid);
-        sstore<AK>(sA[0], ra, tid);
-        sstore<BKM>(sB[0], rb, tid);
+        sstore<AK>(sA(0), ra, tid);
+        sstore<BKM>(sB(0), rb, tid);
     }
     __syncthreads();
     for (int it = 0; it < nk; ++it) {
@@ -127,9 +164,9 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
         }
         float a[2][16], b[2][16];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) frag<AK>(a[i], sA[buf], wm * 64 + i * 32 + l32, h);
+        for (int i = 0; i < 2; ++i) frag<AK>(a[i], sA(buf), wm * 64 + i * 32 + l32, h);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) frag<BKM>(b[j], sB[buf], wn * 64 + j * 32 + l32, h);
+        for (int j = 0; j < 2; ++j) frag<BKM>(b[j], sB(buf), wn * 64 + j * 32 + l32, h);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
 #pragma unroll
@@ -138,8 +175,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
         if (it + 1 < nk) {
-            sstore<AK>(sA[buf ^ 1], ra, tid);
-            sstore<BKM>(sB[buf ^ 1], rb, tid);
+            sstore<AK>(sA(buf ^ 1), ra, tid);
+            sstore<BKM>(sB(buf ^ 1), rb, tid);
         }
         __syncthreads();
     }
@@ -150,7 +187,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
     auto col_of = [&](int j) -> int64_t { return n0 + wn * 64 + j * 32 + l32; };
 
     if constexpr (EPI == kEpiPartial) {
-        float *C = d.C + (int64_t)blockIdx.z * d.M * d.N;
+        float *C = d.C + zz * d.M * d.N;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -164,7 +201,11 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                 }
             }
     } else if constexpr (EPI == kEpiStore) {
+        // per 16-row fragment: every operand load of the fragment is issued before any
+        // store (C may alias T / Mult as far as the compiler knows: interleaving would
+        // serialise one memory round trip per element)
         float cs[2] = {0.0f, 0.0f};
+        const bool two = d.post == kPostTanhGrad || d.post == kPostLreluGrad;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -172,23 +213,29 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                 const int64_t n = col_of(j);
                 if (n >= d.N) continue;
                 const float bn = d.bias ? d.bias[n] : 0.0f;
+                float t[16], q[16];
+                if (two) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t m = row_of(i, r);
+                        t[r] = m < d.M ? d.T[m * d.ldt + n] : 0.0f;
+                        q[r] = (m < d.M && d.Mult) ? d.Mult[m * d.ldt + n] : 1.0f;
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int64_t m = row_of(i, r);
-                    if (m >= d.M) continue;
                     float v = acc[i][j][r] + bn;
                     if (d.post == kPostTanh) {
                         v = tanhf(v);
                     } else if (d.post == kPostTanhGrad) {
-                        const float t = d.T[m * d.ldt + n];
-                        v = v * (1.0f - t * t);
-                        cs[j] += v;
+                        v = v * (1.0f - t[r] * t[r]);
+                        if (m < d.M) cs[j] += v;
                     } else if (d.post == kPostLreluGrad) {
-                        const float u = d.T[m * d.ldt + n];
-                        v = v * (u > 0.0f ? 1.0f : 0.2f);
-                        if (d.Mult) v = v * d.Mult[m * d.ldt + n];
+                        v = v * (t[r] > 0.0f ? 1.0f : 0.2f);
+                        if (d.Mult) v = v * q[r];
                     }
-                    d.C[m * d.ldc + n] = v;
+                    if (m < d.M) d.C[m * d.ldc + n] = v;
                 }
             }
         if (d.post == kPostTanhGrad && d.colsum) {
@@ -206,23 +253,13 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int64_t n = col_of(j);
-                    if (n < d.N) d.colsum[(int64_t)blockIdx.y * d.N + n] = cs[j] + red[wn][j][l32];
+                    if (n < d.N) d.colsum[mt * d.N + n] = cs[j] + red[wn][j][l32];
                 }
             }
         }
     } else if constexpr (EPI == kEpiOpt) {
         // sparse extra gradient rows of this column tile (hits sorted by column)
-        int lo = 0, hi = d.n_hits;
-        if (d.n_hits > 0) {
-            int a = 0, b = d.n_hits;
-            while (a < b) { const int c = (a + b) >> 1; if (d.hit_col[c] < n0) a = c + 1; else b = c; }
-            lo = a;
-            b = d.n_hits;
-            while (a < b) { const int c = (a + b) >> 1; if (d.hit_col[c] < n0 + BN) a = c + 1; else b = c; }
-            hi = a;
-        } else {
-            hi = 0;
-        }
+        const int lo = d.n_hits > 0 ? d.hit_tile_off[nt] : 0, hi = d.n_hits > 0 ? d.hit_tile_off[nt + 1] : 0;
         for (int x = lo; x < hi; ++x) {
             const int64_t c = d.hit_col[x];
             const float *src = d.hit_src + (int64_t)d.hit_row[x] * d.hit_ld;
@@ -238,96 +275,83 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                     }
             }
         }
+        // per 16-row fragment: load p (and m, v) for all rows, update, then store
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int64_t n = col_of(j);
                 if (n >= d.N) continue;
+                float pp[16], mm[16], vv[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t m = row_of(i, r);
+                    const int64_t e = m * d.ldp + n;
+                    const bool ok = m < d.M;
+                    pp[r] = ok ? d.P[e] : 0.0f;
+                    mm[r] = (ok && d.Ms) ? d.Ms[e] : 0.0f;
+                    vv[r] = (ok && d.Vs) ? d.Vs[e] : 0.0f;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float p = pp[r];
+                    if (d.clamp_p > 0.0f) p = fminf(fmaxf(p, -d.clamp_p), d.clamp_p);
+                    pp[r] = opt_update(d.opt, p, acc[i][j][r], mm[r], vv[r]);
+                }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int64_t m = row_of(i, r);
                     if (m >= d.M) continue;
                     const int64_t e = m * d.ldp + n;
-                    float p = d.P[e];
-                    if (d.clamp_p > 0.0f) p = fminf(fmaxf(p, -d.clamp_p), d.clamp_p);
-                    float mm = d.Ms ? d.Ms[e] : 0.0f, vv = d.Vs ? d.Vs[e] : 0.0f;
-                    d.P[e] = opt_update(d.opt, p, acc[i][j][r], mm, vv);
-                    if (d.Ms) d.Ms[e] = mm;
-                    if (d.Vs) d.Vs[e] = vv;
+                    d.P[e] = pp[r];
+                    if (d.Ms) d.Ms[e] = mm[r];
+                    if (d.Vs) d.Vs[e] = vv[r];
                 }
             }
     } else if constexpr (EPI == kEpiArgmax) {
-        // best (value, index) per row and head segment (the tile spans heads h0, h0 + 1)
-        const int64_t h0 = n0 / d.seg;
-        float bv[2][16][2], bi[2][16][2];
+        // tanh(acc + bias) of the 128 x 128 tile into LDS (the operand buffers are free
+        // now), then two threads per row scan 64 columns each: the first maximum per row
+        // and head segment (the tile spans heads h0 and h0 + 1)
+        constexpr int LDT = BN + 1;
+        static_assert(2 * kSA + 2 * kSB >= BM * LDT, "LDS reuse");
+        float *tile = smem;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) { bv[i][r][s] = -INFINITY; bi[i][r][s] = INFINITY; }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t n = col_of(j);
-            if (n >= d.N) continue;
-            const float bn = d.bias ? d.bias[n] : 0.0f;
-            const int s = (int)(n / d.seg - h0);
-            const float idx = (float)(n - (h0 + s) * d.seg);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 2; ++j) {
+                const int64_t n = col_of(j);
+                const float bn = (n < d.N && d.bias) ? d.bias[n] : 0.0f;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float v = tanhf(acc[i][j][r] + bn);
-                    if (s == 0) {
-                        if (better(v, idx, bv[i][r][0], bi[i][r][0])) { bv[i][r][0] = v; bi[i][r][0] = idx; }
-                    } else {
-                        if (better(v, idx, bv[i][r][1], bi[i][r][1])) { bv[i][r][1] = v; bi[i][r][1] = idx; }
-                    }
+                    const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    tile[rl * LDT + wn * 64 + j * 32 + l32] = tanhf(acc[i][j][r] + bn);
                 }
-        }
-        // across the 32 columns of a lane half (same rows)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-#pragma unroll
-                    for (int off = 16; off > 0; off >>= 1) {
-                        const float ov = __shfl_xor(bv[i][r][s], off), oi = __shfl_xor(bi[i][r][s], off);
-                        if (better(ov, oi, bv[i][r][s], bi[i][r][s])) { bv[i][r][s] = ov; bi[i][r][s] = oi; }
-                    }
-        // across the two column waves (wn) through LDS, then one store per row
-        __shared__ float2 red[2][64][2];          // [wm][row in wave tile][segment]
-        if (wn == 1 && l32 == 0) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int rr = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    red[wm][rr][0] = make_float2(bv[i][r][0], bi[i][r][0]);
-                    red[wm][rr][1] = make_float2(bv[i][r][1], bi[i][r][1]);
-                }
-        }
+            }
         __syncthreads();
-        if (wn == 0 && l32 == 0) {
+        const int rl = tid >> 1, half = tid & 1;
+        const int64_t h0 = n0 / d.seg;
+        float bv[2] = {-INFINITY, -INFINITY}, bi[2] = {INFINITY, INFINITY};
+        for (int c = half * 64; c < half * 64 + 64; ++c) {
+            const int64_t n = n0 + c;
+            if (n >= d.N) break;
+            const int sg = (int)(n / d.seg - h0);
+            const float v = tile[rl * LDT + c], ix = (float)(n - (h0 + sg) * d.seg);
+            if (sg == 0) {
+                if (better(v, ix, bv[0], bi[0])) { bv[0] = v; bi[0] = ix; }
+            } else {
+                if (better(v, ix, bv[1], bi[1])) { bv[1] = v; bi[1] = ix; }
+            }
+        }
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+            const float ov = __shfl_xor(bv[sg], 1), oi = __shfl_xor(bi[sg], 1);
+            if (better(ov, oi, bv[sg], bi[sg])) { bv[sg] = ov; bi[sg] = oi; }
+        }
+        const int64_t m = m0 + rl;
+        if (half == 0 && m < d.M) {
             const int64_t ntile = gemm_tiles_n(d.N);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int rr = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int64_t m = row_of(i, r);
-                    if (m >= d.M) continue;
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        float v = bv[i][r][s], ix = bi[i][r][s];
-                        const float2 o = red[wm][rr][s];
-                        if (better(o.x, o.y, v, ix)) { v = o.x; ix = o.y; }
-                        d.amax[(m * ntile + blockIdx.x) * 2 + s] = make_float2(v, ix);
-                    }
-                }
+            d.amax[(m * ntile + nt) * 2 + 0] = make_float2(bv[0], bi[0]);
+            d.amax[(m * ntile + nt) * 2 + 1] = make_float2(bv[1], bi[1]);
         }
     }
 }
@@ -377,8 +401,10 @@ int gemm(hipStream_t stream, const GemmDesc &d) {
     if (d.splits < 1 || (d.splits > 1 && d.epi != kEpiPartial)) return fail_arg("gemm: split-K needs kEpiPartial");
     if (d.epi == kEpiArgmax && (d.seg < kGemmBN || !d.amax)) return fail_arg("gemm: argmax needs seg >= 128");
     if (d.epi == kEpiOpt && !d.P) return fail_arg("gemm: optimizer epilogue needs P");
+    if (d.n_hits > 0 && (!d.hit_tile_off || !d.hit_col || !d.hit_row || !d.hit_src))
+        return fail_arg("gemm: hits need hit_col, hit_row, hit_src and per-tile offsets");
     if ((d.epi == kEpiStore || d.epi == kEpiPartial) && !d.C) return fail_arg("gemm: no C");
-    const dim3 grid((unsigned)gemm_tiles_n(d.N), (unsigned)gemm_tiles_m(d.M), (unsigned)d.splits);
+    const dim3 grid((unsigned)TileMap(d).blocks());
     if (d.a_kmajor) {
         if (d.b_kmajor) launch_epi<true, true>(stream, d, grid);
         else launch_epi<true, false>(stream, d, grid);

@@ -68,6 +68,8 @@ class GANBatch:
             o = np.lexsort((row, col))
             self.hit_col = torch.from_numpy(col[o].astype(np.int32)).to(device)
             self.hit_row = torch.from_numpy(row[o].astype(np.int32)).to(device)
+            edges = np.arange(0, (S * N + 127) // 128 + 1, dtype=np.int64) * 128      # GEMM column tiles
+            self.hit_tile_off = torch.from_numpy(np.searchsorted(col[o], edges).astype(np.int32)).to(device)
             self.n_hits = B * S
 
     def c_struct(self):
@@ -78,7 +80,7 @@ class GANBatch:
         b.n_hist_items = self.n_items
         b.n_hits = self.n_hits
         if self.n_hits:
-            b.hit_col, b.hit_row = ptr(self.hit_col), ptr(self.hit_row)
+            b.hit_col, b.hit_row, b.hit_tile_off = ptr(self.hit_col), ptr(self.hit_row), ptr(self.hit_tile_off)
         return b
 
 

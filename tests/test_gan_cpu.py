@@ -55,3 +55,34 @@ def test_gan_engine_is_gpu_only():
     from recommendation_gans_amd.gan_engine import GANEngine
     with pytest.raises(RuntimeError, match="GPU only"):
         GANEngine({}, {}, 50, 5, 16, 5, device="cpu")
+
+
+def test_gan_modules_reproduce_reference_init(golden_dir):
+    """torch.manual_seed(s) + construction in the reference's order (generator, then
+    discriminator, as make_golden.gan_case) gives the reference's tensors exactly."""
+    import os
+    from recommendation_gans_amd.spotlight.dnn_models.cGAN_models import discriminator, generator
+    z = np.load(os.path.join(golden_dir, "gan_rms_refinit.npz"))
+    N, S, H, E, B, L, Z, nb, dsteps = (int(x) for x in z["meta"])
+    torch.manual_seed(3)
+    G = generator(num_items=N, noise_dim=Z, embedding_dim=E, hidden_layer=[H // 2, H], output_dim=S)
+    D = discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
+    for prefix, mod in (("g_init_", G), ("d_init_", D)):
+        sd = mod.state_dict()
+        names = {k for k in z.files if k.startswith(prefix)}
+        assert {prefix + k.replace(".", "_") for k in sd} == names
+        for k, v in sd.items():
+            assert np.array_equal(v.numpy(), z[prefix + k.replace(".", "_")]), k
+
+
+def test_gan_batch_hit_tiles():
+    from recommendation_gans_amd.gan_engine import GANBatch
+    N, S = 300, 5
+    rs = np.random.RandomState(0)
+    hist = rs.randint(0, N + 1, (16, 7))
+    slates = np.stack([rs.choice(N, S, replace=False) for _ in range(16)])
+    b = GANBatch(hist, slates, N, S, "cpu")
+    col, off = b.hit_col.numpy(), b.hit_tile_off.numpy()
+    assert len(off) == (S * N + 127) // 128 + 1 and off[0] == 0 and off[-1] == len(col)
+    for t in range(len(off) - 1):
+        assert ((col[off[t]:off[t + 1]] // 128) == t).all()
