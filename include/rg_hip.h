@@ -433,6 +433,12 @@ int rg_gemm_f32(void *stream, const float *A, int64_t lda, int32_t a_kmajor, con
                 int32_t b_kmajor, int64_t M, int64_t N, int64_t K, float *C, int64_t ldc, const float *bias,
                 int32_t post, int32_t splits, float *work);
 
+/* The cGAN's weight-gradient GEMM fused with an in-place RMSprop update of P [M][N]
+ * (row stride ldp) and its square average V (test / measurement entry). */
+int rg_gemm_f32_rms(void *stream, const float *A, int64_t lda, int32_t a_kmajor, const float *B, int64_t ldb,
+                    int32_t b_kmajor, int64_t M, int64_t N, int64_t K, float *P, float *V, int64_t ldp, float lr,
+                    float alpha, float eps);
+
 /* Milliseconds between two timing events (hipEvent_t) recorded on a stream. */
 int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms);
 

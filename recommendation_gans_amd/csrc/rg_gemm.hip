@@ -438,3 +438,20 @@ extern "C" int rg_gemm_f32(void *stream, const float *A, int64_t lda, int32_t a_
     if (rc) return rc;
     return rg::reduce_partials((hipStream_t)stream, work, splits, M, N, C, ldc, bias);
 }
+
+// test / measurement entry: C-shaped gradient GEMM fused with an RMSprop (alpha, eps)
+// update of P [M][N] (row stride ldp) and its square average V
+extern "C" int rg_gemm_f32_rms(void *stream, const float *A, int64_t lda, int32_t a_kmajor, const float *B,
+                               int64_t ldb, int32_t b_kmajor, int64_t M, int64_t N, int64_t K, float *P, float *V,
+                               int64_t ldp, float lr, float alpha, float eps) {
+    rg::GemmDesc d;
+    d.A = A; d.lda = lda; d.a_kmajor = a_kmajor != 0;
+    d.B = B; d.ldb = ldb; d.b_kmajor = b_kmajor != 0;
+    d.M = M; d.N = N; d.K = K;
+    d.epi = rg::kEpiOpt;
+    d.P = P; d.Vs = V; d.ldp = ldp;
+    d.opt.kind = RG_OPT_RMSPROP;
+    d.opt.lr = lr; d.opt.alpha = alpha; d.opt.eps = eps;
+    d.opt.one_minus_alpha = (float)(1.0 - (double)alpha);
+    return rg::gemm((hipStream_t)stream, d);
+}

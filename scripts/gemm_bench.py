@@ -48,3 +48,35 @@ run("D1 dW (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, SN, B, KS)
 run("heads dW (AM,BN)", fake, KS, 0, a2, H, 0, SN, H, B, H)
 for sp in (64, 128):
     run(f"heads dA split{sp} (AK,BN)", fake, KS, 1, wh, H, 0, B, H, KS, H, splits=sp)
+
+
+def run_rms(name, A, lda, akm, Bm, ldb, bkm, M, N, K, reps=10):
+    P = torch.rand(M, N, device=dev) * 0.01
+    V = torch.rand(M, N, device=dev) * 1e-6
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    args = (st, ptr(A), lda, akm, ptr(Bm), ldb, bkm, M, N, K, ptr(P), ptr(V), N, 1e-3, 0.99, 1e-8)
+    _lib.check(L.rg_gemm_f32_rms(*args), name)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        L.rg_gemm_f32_rms(*args)
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) / reps * 1e3
+    print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "us": round(us, 1),
+                      "pv_GBps": round(4 * 4 * M * N / (us * 1e-6) / 1e9, 1)}), flush=True)
+    # the same P / V traffic as a plain streaming update (torch ops, reference point)
+    g = torch.rand(M, N, device=dev)
+    a.record()
+    for _ in range(reps):
+        V.mul_(0.99).addcmul_(g, g, value=0.01)
+        P.addcdiv_(g, V.sqrt().add_(1e-8), value=-1e-3)
+    b.record()
+    torch.cuda.synchronize()
+    us2 = a.elapsed_time(b) / reps * 1e3
+    print(json.dumps({"shape": "torch rmsprop same size", "us": round(us2, 1)}), flush=True)
+
+
+run_rms("D1 dW + RMSprop (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, KS - 4, B)
+run_rms("heads dW + RMSprop (AM,BN)", fake, KS, 0, a2, H, 0, KS - 4, H, B)
