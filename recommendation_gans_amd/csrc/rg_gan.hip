@@ -834,7 +834,7 @@ int check_common(const rg_gan_model_t *mdl, void *ws, const rg_gan_batch_t *bt) 
     if (dm.num_items <= 0 || dm.slate_size <= 0 || dm.hidden < 2 || dm.hidden % 8 || dm.emb_dim <= 0 ||
         dm.z_dim <= 0 || dm.batch_max <= 0)
         return fail_arg("rg_gan: bad dims (hidden must be a positive multiple of 8)");
-    if (bt->rows < 2 || bt->rows > dm.batch_max) return fail_arg("rg_gan: rows must be in [2, batch_max]");
+    if (bt->rows < 1 || bt->rows > dm.batch_max) return fail_arg("rg_gan: rows must be in [1, batch_max]");
     if (bt->hist_len <= 0 || !bt->hist) return fail_arg("rg_gan: empty history");
     return 0;
 }
@@ -873,6 +873,7 @@ extern "C" int64_t rg_gan_workspace_offset(const rg_gan_dims_t *dims, int32_t vi
 extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *workspace, const rg_gan_batch_t *bt,
                              const rg_gan_noise_t *nz, const rg_opt_t *opt, float *out) {
     RG_TRY(check_common(mdl, workspace, bt));
+    if (bt->rows < 2) return fail_arg("rg_gan_d_step: training needs >= 2 rows (BatchNorm batch statistics)");
     if (!bt->slates || !bt->hit_col || !bt->hit_row || !bt->hit_tile_off || !nz || !nz->z || !opt || !out)
         return fail_arg("rg_gan_d_step: slates, hits, noise, opt and out are required");
     const Dims m(mdl->dims);
@@ -952,6 +953,7 @@ extern "C" int rg_gan_d_step(void *stream, const rg_gan_model_t *mdl, void *work
 extern "C" int rg_gan_g_step(void *stream, const rg_gan_model_t *mdl, void *workspace, const rg_gan_batch_t *bt,
                              const rg_gan_noise_t *nz, const rg_opt_t *opt, float *out, float *slates) {
     RG_TRY(check_common(mdl, workspace, bt));
+    if (bt->rows < 2) return fail_arg("rg_gan_g_step: training needs >= 2 rows (BatchNorm batch statistics)");
     if (!nz || !nz->z || !opt || !out) return fail_arg("rg_gan_g_step: noise, opt and out are required");
     const Dims m(mdl->dims);
     int64_t go[RG_GAN_G_END + 1], dof[RG_GAN_D_END + 1];

@@ -110,3 +110,34 @@ def evaluate_random(item_popularity, test, k=10):
         precision.append(p)
         recall.append(r)
     return np.mean(np.array(precision).squeeze()), np.mean(np.array(recall).squeeze())
+
+
+def precision_recall_score_slates(slates, test, k=3):
+    """spotlight/evaluation.py:355-382: precision / recall@k of each test user's
+    generated slate (row u of ``slates`` belongs to row u of the CSR ``test``)."""
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    test = test.tocsr()
+    precision, recall = [], []
+    for user_id in range(test.shape[0]):
+        targets = test.indices[test.indptr[user_id]:test.indptr[user_id + 1]]
+        if not len(targets):
+            continue
+        pred = slates[user_id].numpy() if hasattr(slates[user_id], "numpy") else np.asarray(slates[user_id])
+        p, r = zip(*[_get_precision_recall(pred, targets, x) for x in ks])
+        precision.append(p[0])
+        recall.append(r[0])
+    return precision, recall
+
+
+def precision_recall_slates_atk(fake_slates, real_slates, k=3):
+    """spotlight/evaluation.py:394-412, the generator's training precision / recall.
+    The reference intersects sets of 0-d torch tensors (rows of the two slate
+    tensors), which hash by identity, so every user scores 0; the same operations on
+    the same tensor types are kept here so summary.csv matches the reference."""
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    precision, recall = [], []
+    for user_id in range(fake_slates.shape[0]):
+        p, r = zip(*[_get_precision_recall(fake_slates[user_id, :], real_slates[user_id, :], x) for x in ks])
+        precision.append(p[0])
+        recall.append(r[0])
+    return precision, recall

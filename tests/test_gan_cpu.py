@@ -86,3 +86,59 @@ def test_gan_batch_hit_tiles():
     assert len(off) == (S * N + 127) // 128 + 1 and off[0] == 0 and off[-1] == len(col)
     for t in range(len(off) - 1):
         assert ((col[off[t]:off[t + 1]] // 128) == t).all()
+
+
+def _create_slates_loop(user_ids, item_ids, timestamps, U, n):
+    """The reference's per-user loop (dataset_manilupation.py:290-316), restated."""
+    slates = np.zeros((U, n))
+    delete = []
+    for u in range(U):
+        idx = np.where(user_ids == u)[0]
+        if len(idx) == 0:
+            continue
+        if len(idx) < n:
+            delete += list(idx)
+            continue
+        srt = idx[np.argsort(timestamps[idx], kind="stable")]
+        slates[u] = item_ids[srt[-n:]]
+        delete += list(srt[-n:])
+    keep = np.setdiff1d(np.arange(len(user_ids)), delete)
+    zero = np.where(~slates.any(axis=1))[0]
+    return keep, np.delete(slates, zero, axis=0), zero
+
+
+def test_create_slates_matches_reference_loop():
+    from recommendation_gans_amd.spotlight.dataset_manilupation import create_slates
+    from recommendation_gans_amd.spotlight.interactions import Interactions
+    rs = np.random.RandomState(0)
+    U, I, n = 40, 30, 3
+    u = rs.randint(0, U, 400).astype(np.int32)
+    i = rs.randint(0, I, 400).astype(np.int32)
+    t = rs.permutation(400).astype(np.int64)
+    keep, slates_ref, zero = _create_slates_loop(u, i, t, U, n)
+    inter = Interactions(u.copy(), i.copy(), ratings=np.ones(400, np.float32), timestamps=t.copy(), num_users=U,
+                         num_items=I)
+    hist, slates = create_slates(inter, n=n, padding_value=I)
+    assert np.array_equal(slates, slates_ref)
+    assert np.array_equal(np.sort(inter.timestamps), np.sort(t[keep]))
+    assert hist.shape == (U - len(zero), I)
+
+
+def test_slate_provider_synthetic_and_restricted_cache(tmp_path):
+    import pickle
+    import scipy.sparse as sp
+    from recommendation_gans_amd.utils.slate_data_provider import _load, slate_data_provider
+    d = slate_data_provider(str(tmp_path) + "/", "100K", slate_size=3)
+    tv, ts, tev, tes, U, N, vv, vcs, vs = d.get_data()
+    assert (U, N) == (943, 1682) and tv.shape[0] == ts.shape[0] and ts.shape[1] == 3
+    assert float(tv.max()) <= N and vv.shape[0] == vs.shape[0] and tev.shape[0] == tes.shape[0]
+    # the cache reader admits NumPy arrays / CSR matrices only
+    ok = tmp_path / "ok.pkl"
+    with open(ok, "wb") as f:
+        pickle.dump(sp.csr_matrix(np.eye(3)), f)
+    assert _load(str(ok)).shape == (3, 3)
+    bad = tmp_path / "bad.pkl"
+    with open(bad, "wb") as f:
+        pickle.dump(slate_data_provider.exists, f)
+    with pytest.raises(pickle.UnpicklingError):
+        _load(str(bad))
