@@ -21,7 +21,7 @@ int comm_end(void *comm, hipStream_t stream);
 // ---------------------------------------------------------------- MT jump-ahead
 // One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,
 // rg_sampler.hip).  Device buffers are owned by the plan.
-constexpr int kMtMaxTail = 8;
+constexpr int kMtMaxTail = 32;
 struct MtTailSegs {
     int64_t start[kMtMaxTail], len[kMtMaxTail];
     int n;

@@ -171,8 +171,9 @@ MtJumpPlan *mt_jump_plan_create(int64_t words) {
     using namespace mtj;
     const int64_t head = kDeg + kN - 1;          // windows S_i, i < 19937, need x[0 .. 20560)
     if (words < 2 * head || mtj::charpoly().empty()) return nullptr;
+    // tail segments of ~20k words: each walks about as long as the head does
     const char *env = getenv("RG_MT_TAIL");
-    int n = env ? atoi(env) : 4;
+    int n = env ? atoi(env) : (int)((words - head + 19999) / 20000);
     n = n < 1 ? 1 : (n > kMtMaxTail ? kMtMaxTail : n);
     MtJumpPlan *p = new MtJumpPlan();
     p->words = words;
@@ -240,5 +241,20 @@ extern "C" int rg_mt_window_to_cpython(const uint32_t *window, int32_t pos, uint
     std::memcpy(state_out, window + (kN - pos), (size_t)pos * sizeof(uint32_t));
     std::memcpy(state_out + pos, ahead.data(), ahead.size() * sizeof(uint32_t));
     state_out[kN] = (uint32_t)pos;
+    return RG_OK;
+}
+
+extern "C" int rg_mt_advance_host(uint32_t *state, int64_t k) {
+    using namespace rg::mtj;
+    if (!state || k < 0 || state[kN] > (uint32_t)kN)
+        return rg::fail_arg("rg_mt_advance_host: bad argument");
+    const int64_t P = (int64_t)state[kN] + k;        // stream index of the next word, block 0 = state
+    if (P <= kN) { state[kN] = (uint32_t)P; return RG_OK; }
+    const int64_t fb = (P - 1) / kN;                 // block holding the last consumed word
+    std::vector<uint32_t> x((size_t)(kN * (fb + 1)));
+    std::memcpy(x.data(), state, kN * sizeof(uint32_t));
+    for (size_t n = kN; n < x.size(); ++n) x[n] = x[n - (kN - kM)] ^ mix(x[n - kN], x[n - kN + 1]);
+    std::memcpy(state, x.data() + kN * fb, kN * sizeof(uint32_t));
+    state[kN] = (uint32_t)(P - kN * fb);
     return RG_OK;
 }

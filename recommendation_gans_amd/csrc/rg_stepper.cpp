@@ -2,27 +2,34 @@
 //
 // Replaces the Python-side loop body of ImplicitFactorizationModel.fit
 // (implicit.py:290-298 -> run_train_iteration :347-364) so that one call per step
-// enqueues everything, without per-step Python/ctypes overhead:
+// enqueues everything, without per-step Python/ctypes overhead.
 //
-//   gen stream   rg_mt_generate of stream chunk g (+2 ahead)   -> gen_done[g % 3]
-//   prep stream  [gen_done] rg_mf_prepare of the NEXT step     -> ready[buf]
-//   main stream  [ready] rg_mf_pairs -> consumed -> rg_mf_apply (-> exchange)
+// Word stream.  The words a step consumes do not depend on the step's input: draw
+// j of any consumer (training step or validation batch) is just the next 2 words
+// of CPython's stream, and every consumer of this stepper takes the same number of
+// words W = 2 * n_neg * global_cols (one "unit").  The stream is cut into ring
+// slots of G units, generated up to two slots ahead of consumption into a ring of
+// three slot buffers on a stream of its own (the sequential MT19937 walk, or the
+// jump-ahead head + parallel tails, stays off the critical path; one generation
+// launch and two events per G steps).  The state CPython would hold after the
+// consumed units is the start state of their slot advanced by the units consumed
+// inside it (rg_mf_stepper_sync_mt).
 //
-// The words a step consumes do not depend on the step's input: draw j of any
-// consumer (training step or validation batch) is just the next 2 words of
-// CPython's stream, and every consumer of this stepper takes the same number of
-// words (n_neg * global_cols draws).  So the stream is cut into fixed chunks,
-// generated up to two chunks ahead of consumption into a ring of three buffers
-// on their own stream (the sequential MT19937 walk is off the critical path),
-// while the input-dependent part (rg_mf_prepare: draws -> pool pairs, in the
-// plan's column order) runs on a second stream once the next input is known.
-// A prefetch for a different input only redoes rg_mf_prepare; the MT stream is
-// never rolled back.  The state CPython would hold after the consumed chunks is
-// the start state of the oldest unconsumed chunk (kept per ring slot).
+// Overlapped step (default; pointwise / bpr / hinge):
+//   main  rg_mf_step_front(pairs of t | marked prepare of t+1 | cold-row update of t)
+//         -> rg_mf_step_hot(touched rows of t, loss)
+// Two launches per step on one stream and no per-step event: the prepare of the
+// next step rides in the front grid, so the only cross-stream dependency left is
+// one wait per ring slot for the generated words.
+//
+// Split step (adaptive hinge, RG_FUSED=0, and the external consumers that go
+// through acquire / release: validation, NCF, the Python split DP steps):
+//   prep  rg_mf_prepare of the next unit (after the current pairs kernel)
+//   main  rg_mf_pairs -> rg_mf_apply (-> exchange)
 //
 // Device memory: the caller (PyTorch) owns tables, scratch, pool and pairs; the
-// stepper owns its word ring, the per-slot start states and (jump path) the jump
-// tables.
+// stepper owns its word ring, the per-slot start states, the row stamps of the
+// overlapped step and (jump path) the jump tables.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -34,33 +41,45 @@
 
 namespace {
 
-constexpr int kSlots = 3;        // word chunks in the ring
-constexpr int kAhead = 2;        // chunks generated ahead of consumption
+constexpr int kSlots = 3;        // word slots in the ring
+constexpr int kAheadSlots = 2;   // slots generated ahead of the one being consumed
 
 struct Stepper {
     rg_mf_stepper_config_t cfg;
     hipStream_t gen = nullptr, prep = nullptr;
+    int64_t W = 0;                        // words per unit
+    int64_t G = 1;                        // units per ring slot
     uint32_t *words[kSlots] = {nullptr, nullptr, nullptr};
-    uint32_t *start_state[kSlots] = {nullptr, nullptr, nullptr};   // [625] state before chunk
+    uint32_t *start_state[kSlots] = {nullptr, nullptr, nullptr};   // [625] state before the slot
     hipEvent_t gen_done[kSlots] = {nullptr, nullptr, nullptr};
-    hipEvent_t consumed[kSlots] = {nullptr, nullptr, nullptr};     // after the chunk's pairs kernel
+    hipEvent_t consumed[kSlots] = {nullptr, nullptr, nullptr};     // after the slot's last consumer
     bool consumed_valid[kSlots] = {false, false, false};
-    hipEvent_t ready[2] = {nullptr, nullptr};                      // prepared pairs buffers
-    int64_t generated = 0, taken = 0;     // chunks generated / consumed
-    // prepared pairs of chunk `prep_chunk` for input `prep_in` in pairs buffer prep_chunk % 2
+    hipEvent_t ready[2] = {nullptr, nullptr};                      // side-stream prepared pairs buffers
+    bool side_pending[2] = {false, false};                         // ready[b] not yet waited by the consumer
+    hipEvent_t mark = nullptr;                                     // consumer-stream point a side prepare follows
+    int64_t unit_base = 0;                // unit of relative slot 0 (reset when the state is loaded)
+    int64_t gen_slots = 0;                // relative slots generated
+    int64_t taken = 0;                    // units consumed
+    hipStream_t waited_stream = nullptr;  // the consumer stream has waited for gen_done of slots <= waited_slot
+    int64_t waited_slot = -1;
+    // prepared pairs of unit prep_unit for input prep_in, in pairs buffer prep_unit % 2
     bool prepared = false;
-    int64_t prep_chunk = -1;
+    int64_t prep_unit = -1;
     rg_mf_step_in_t prep_in{};
+    int32_t prep_serial = 0;              // nonzero: prepared with row marks (stamp array prep_arr)
+    int prep_arr = 0;
+    int32_t serial = 0;                   // last mark serial issued
+    int32_t *stamp[2] = {nullptr, nullptr};   // [U + I] each, lazily allocated
     int set = 0;                          // ping-pong set holding the current tables
-    int64_t words_per_step = 0;
-    // MT jump-ahead path (opt-in): the device state is in window form after a jump
-    // chunk; cp_pos tracks CPython's position-in-block of the same stream point
+    bool fused = true;
+    bool hot_scan = true;
+    // MT jump-ahead path: the device state is in window form after a jump slot;
+    // cp_pos tracks CPython's position-in-block of the same stream point
     rg::MtJumpPlan *jump = nullptr;
     bool window_form = false;
     int32_t cp_pos = 624;
     bool win_at[kSlots] = {false, false, false};   // form / position at each slot's start
     int32_t pos_at[kSlots] = {624, 624, 624};
-    bool release_late = false, prep_after_pairs = true;
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -68,7 +87,14 @@ int hip_fail(const char *what, hipError_t e) {
     return RG_E_LAUNCH;
 }
 
-rg_mf_batch_t make_batch(const Stepper &st, const rg_mf_step_in_t &in, int64_t chunk) {
+int64_t rel_slot(const Stepper &st, int64_t unit) { return (unit - st.unit_base) / st.G; }
+
+uint32_t *unit_words(const Stepper &st, int64_t unit) {
+    const int64_t rel = unit - st.unit_base;
+    return st.words[(rel / st.G) % kSlots] + (rel % st.G) * st.W;
+}
+
+rg_mf_batch_t make_batch(const Stepper &st, const rg_mf_step_in_t &in, int64_t unit) {
     rg_mf_batch_t x{};
     x.pos_user = in.pos_user;
     x.pos_item = in.pos_item;
@@ -78,12 +104,12 @@ rg_mf_batch_t make_batch(const Stepper &st, const rg_mf_step_in_t &in, int64_t c
     x.global_cols = st.cfg.global_cols;
     x.global_pos = in.global_pos;
     x.neg_cols = st.cfg.neg_cols;
-    x.words = st.words[chunk % kSlots];
+    x.words = unit_words(st, unit);
     x.pool = st.cfg.pool;
     x.pool_len = st.cfg.pool_len;
     x.n_neg = st.cfg.n_neg;
     x.loss = st.cfg.loss;
-    x.pairs = st.cfg.pairs[chunk % 2];
+    x.pairs = st.cfg.pairs[unit % 2];
     return x;
 }
 
@@ -93,88 +119,143 @@ void set_plan(rg_mf_work_t &w, const rg_mf_step_in_t &in) {
     w.plan_item_slot_off = in.plan_item_slot_off;
 }
 
+rg_mf_work_t work_for(const Stepper &st, const rg_mf_step_in_t &in) {
+    rg_mf_work_t w = st.cfg.work;
+    set_plan(w, in);
+    return w;
+}
+
 bool same_input(const rg_mf_step_in_t &a, const rg_mf_step_in_t &b) {
     return std::memcmp(&a, &b, sizeof(a)) == 0;
 }
 
-// generate the next chunk of the stream into its ring slot on the gen stream
+// generate the next ring slot (G units) on the gen stream
 int generate_one(Stepper &st) {
-    const int slot = (int)(st.generated % kSlots);
+    const int slot = (int)(st.gen_slots % kSlots);
     hipError_t e;
     if (st.consumed_valid[slot] && (e = hipStreamWaitEvent(st.gen, st.consumed[slot], 0)) != hipSuccess)
         return hip_fail("stepper: wait consumed", e);
     st.win_at[slot] = st.window_form;
     st.pos_at[slot] = st.cp_pos;
+    const int64_t nwords = st.G * st.W;
     int rc;
     if (st.jump) {
         rc = rg::mt_produce_jump(st.gen, *st.jump, st.cfg.mt_state, st.words[slot], st.start_state[slot]);
         st.window_form = true;
     } else {
-        rc = rg_mt_generate(st.gen, st.cfg.mt_state, st.words[slot], st.words_per_step, st.start_state[slot]);
+        rc = rg_mt_generate(st.gen, st.cfg.mt_state, st.words[slot], nwords, st.start_state[slot]);
     }
     if (rc) return rc;
-    st.cp_pos = (int32_t)((st.cp_pos + st.words_per_step - 1) % 624 + 1);
+    st.cp_pos = (int32_t)((st.cp_pos + nwords - 1) % 624 + 1);
     if ((e = hipEventRecord(st.gen_done[slot], st.gen)) != hipSuccess) return hip_fail("stepper: record gen", e);
-    ++st.generated;
+    ++st.gen_slots;
     return RG_OK;
 }
 
-int ensure_generated(Stepper &st, int64_t upto) {
-    while (st.generated < upto) {
+// slots up to the one holding `unit`, plus kAheadSlots more, are generated (or queued)
+int keep_ahead(Stepper &st, int64_t unit) {
+    const int64_t upto = rel_slot(st, unit) + 1 + kAheadSlots;
+    while (st.gen_slots < upto) {
         int rc = generate_one(st);
         if (rc) return rc;
     }
     return RG_OK;
 }
 
-// rg_mf_prepare of chunk `chunk` for input `in` on the prep stream.  `after`: an
-// event (or null) the preparation must also follow (the current pairs kernel:
-// then it runs beside the HBM-bound apply rather than the latency-bound pairs)
-int prepare(Stepper &st, int64_t chunk, const rg_mf_step_in_t &in, hipEvent_t after) {
-    const int slot = (int)(chunk % kSlots), buf = (int)(chunk % 2);
-    hipError_t e = hipStreamWaitEvent(st.prep, st.gen_done[slot], 0);
+// make the words of `unit` visible to `stream` (one event wait per slot and stream)
+int wait_words(Stepper &st, hipStream_t stream, int64_t unit) {
+    const int64_t rel = rel_slot(st, unit);
+    if (st.waited_stream == stream && st.waited_slot >= rel) return RG_OK;
+    hipError_t e = hipStreamWaitEvent(stream, st.gen_done[rel % kSlots], 0);
     if (e != hipSuccess) return hip_fail("stepper: wait gen", e);
-    if (chunk >= 2) {   // pairs buffer `buf` was read by chunk - 2's pairs kernel
-        const int prev = (int)((chunk - 2) % kSlots);
-        if (st.consumed_valid[prev] && (e = hipStreamWaitEvent(st.prep, st.consumed[prev], 0)) != hipSuccess)
-            return hip_fail("stepper: wait pairs buffer", e);
-    }
-    if (after && (e = hipStreamWaitEvent(st.prep, after, 0)) != hipSuccess)
-        return hip_fail("stepper: wait pairs", e);
-    rg_mf_work_t w = st.cfg.work;
-    set_plan(w, in);
-    rg_mf_batch_t batch = make_batch(st, in, chunk);
-    int rc = rg_mf_prepare(st.prep, &batch, &w);
-    if (rc) return rc;
-    if ((e = hipEventRecord(st.ready[buf], st.prep)) != hipSuccess) return hip_fail("stepper: record ready", e);
-    st.prepared = true;
-    st.prep_chunk = chunk;
-    st.prep_in = in;
+    st.waited_stream = stream;
+    st.waited_slot = rel;
     return RG_OK;
 }
 
-// make the next chunk's words + pairs for `in` visible to `stream`; returns the chunk
-int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t *chunk_out) {
-    const int64_t chunk = st.taken;
-    int rc = ensure_generated(st, chunk + 1);
-    if (rc) return rc;
-    if (!(st.prepared && st.prep_chunk == chunk && same_input(st.prep_in, in))) {
-        if ((rc = prepare(st, chunk, in, nullptr))) return rc;
-    }
-    hipError_t e = hipStreamWaitEvent(stream, st.ready[chunk % 2], 0);
+// an outstanding side-stream write of pairs buffer b must land before `stream` uses it
+int wait_side(Stepper &st, hipStream_t stream, int b) {
+    if (!st.side_pending[b]) return RG_OK;
+    hipError_t e = hipStreamWaitEvent(stream, st.ready[b], 0);
     if (e != hipSuccess) return hip_fail("stepper: wait ready", e);
-    *chunk_out = chunk;
+    st.side_pending[b] = false;
     return RG_OK;
 }
 
-// the consumer of chunk `taken` has been enqueued on `stream`
+// unmarked rg_mf_prepare of `unit` for `in` on the prep stream, ordered after everything
+// the consumer stream holds so far (in a training call: the current pairs kernel, so it
+// runs beside the HBM-bound apply)
+int prepare_side(Stepper &st, hipStream_t consumer, int64_t unit, const rg_mf_step_in_t &in) {
+    int rc = keep_ahead(st, unit);
+    if (rc) return rc;
+    hipError_t e = hipEventRecord(st.mark, consumer);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st.prep, st.mark, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st.prep, st.gen_done[rel_slot(st, unit) % kSlots], 0);
+    if (e != hipSuccess) return hip_fail("stepper: order prepare", e);
+    const rg_mf_work_t w = work_for(st, in);
+    const rg_mf_batch_t batch = make_batch(st, in, unit);
+    if ((rc = rg_mf_prepare(st.prep, &batch, &w))) return rc;
+    const int b = (int)(unit % 2);
+    if ((e = hipEventRecord(st.ready[b], st.prep)) != hipSuccess) return hip_fail("stepper: record ready", e);
+    st.side_pending[b] = true;
+    st.prepared = true;
+    st.prep_unit = unit;
+    st.prep_in = in;
+    st.prep_serial = 0;
+    return RG_OK;
+}
+
+int ensure_stamps(Stepper &st) {
+    if (st.stamp[0]) return RG_OK;
+    const rg_mf_tables_t &t = st.cfg.tables[0];
+    const size_t bytes = (size_t)(t.num_users + t.num_items) * sizeof(int32_t);
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        e = hipMalloc(&st.stamp[k], bytes);
+        if (e == hipSuccess) e = hipMemset(st.stamp[k], 0, bytes);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e == hipSuccess ? RG_OK : hip_fail("stepper: stamps", e);
+}
+
+rg_mf_mark_t mark_of(const Stepper &st, int arr, int32_t serial) {
+    rg_mf_mark_t m{};
+    m.stamp = st.stamp[arr];
+    m.num_users = st.cfg.tables[0].num_users;
+    m.serial = serial;
+    return m;
+}
+
+int32_t next_serial(Stepper &st) {
+    st.serial = st.serial == 0x7fffffff ? 1 : st.serial + 1;
+    return st.serial;
+}
+
+// the consumer of `taken` has been enqueued on `stream`
 int release(Stepper &st, hipStream_t stream) {
-    const int slot = (int)(st.taken % kSlots);
-    hipError_t e = hipEventRecord(st.consumed[slot], stream);
-    if (e != hipSuccess) return hip_fail("stepper: record consumed", e);
-    st.consumed_valid[slot] = true;
+    const int64_t rel = st.taken - st.unit_base;
     ++st.taken;
-    if (st.prepared && st.prep_chunk < st.taken) st.prepared = false;
+    if (st.prepared && st.prep_unit < st.taken) st.prepared = false;
+    if ((rel + 1) % st.G == 0) {                         // the slot's last unit
+        const int slot = (int)((rel / st.G) % kSlots);
+        hipError_t e = hipEventRecord(st.consumed[slot], stream);
+        if (e != hipSuccess) return hip_fail("stepper: record consumed", e);
+        st.consumed_valid[slot] = true;
+    }
+    return keep_ahead(st, st.taken);
+}
+
+// words + pairs of unit `taken` for `in`, visible to `stream` (split-step consumers)
+int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t *unit_out) {
+    const int64_t unit = st.taken;
+    int rc = keep_ahead(st, unit);
+    if (rc) return rc;
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, in))) {
+        if ((rc = prepare_side(st, stream, unit, in))) return rc;
+    }
+    if ((rc = wait_side(st, stream, (int)(unit % 2)))) return rc;
+    if ((rc = wait_words(st, stream, unit))) return rc;   // the adaptive-max kernel reads them
+    *unit_out = unit;
     return RG_OK;
 }
 
@@ -212,17 +293,140 @@ bool env_flag(const char *name, bool dflt) {
     return e ? atoi(e) != 0 : dflt;
 }
 
+int record(void *ev, hipStream_t s) {
+    if (!ev) return RG_OK;
+    hipError_t e = hipEventRecord((hipEvent_t)ev, s);
+    return e == hipSuccess ? RG_OK : hip_fail("stepper: record event", e);
+}
+
+// the update half of a step after the pair pass: user-sharded DP exchange or loss
+int finish_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, rg_mf_work_t &w, float *loss_out,
+                 void *ev0, void *ev1) {
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    const int64_t U = tb->num_users, R = tb->num_users + tb->num_items;
+    int rc;
+    if (st.cfg.item_grad) {                     // user-sharded data parallel
+        if ((rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l))) return rc;
+        if (st.cfg.comm && (rc = rg::comm_begin(st.cfg.comm, s, st.cfg.item_grad,
+                                                tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+            return rc;
+    }
+    if ((rc = record(ev0, s))) return rc;
+    if ((rc = st.cfg.item_grad ? rg_mf_apply(s, tb, &w, &o, 0, U, nullptr) : rg_mf_apply(s, tb, &w, &o, 0, -1, &l)))
+        return rc;
+    if ((rc = record(ev1, s))) return rc;
+    if (st.cfg.item_grad) {
+        if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
+        if ((rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out))) return rc;
+    }
+    return RG_OK;
+}
+
+int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+                float *loss_out, void *ev0, void *ev1) {
+    int64_t unit;
+    int rc = acquire(st, s, cur, &unit);
+    if (rc) return rc;
+    rg_mf_work_t w = work_for(st, cur);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if ((rc = rg_mf_pairs(s, &st.cfg.tables[st.set], &batch, &w, 1))) return rc;
+    if ((rc = release(st, s))) return rc;
+    if (next && (rc = prepare_side(st, s, unit + 1, *next))) return rc;
+    if ((rc = finish_split(st, s, cur, w, loss_out, ev0, ev1))) return rc;
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
+// the touched rows of the hot pass: a stamp scan (RG_HOT_SCAN=1, default) or the owner flags
+const rg_mf_mark_t *hot_mark(const Stepper &st, const rg_mf_mark_t &m) { return st.hot_scan ? &m : nullptr; }
+
+int train_fused(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+                float *loss_out, void *ev0, void *ev1) {
+    int rc = ensure_stamps(st);
+    if (rc) return rc;
+    const int64_t unit = st.taken;
+    if ((rc = keep_ahead(st, unit))) return rc;
+    rg_mf_work_t w = work_for(st, cur);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if (!(st.prepared && st.prep_unit == unit && st.prep_serial != 0 && same_input(st.prep_in, cur))) {
+        // first step, or the prefetched pairs were for another input: marked prepare here
+        if ((rc = wait_side(st, s, (int)(unit % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit))) return rc;
+        st.prep_arr = 1 - st.prep_arr;
+        st.prep_serial = next_serial(st);
+        const rg_mf_mark_t m = mark_of(st, st.prep_arr, st.prep_serial);
+        if ((rc = rg_mf_prepare_marked(s, &batch, &w, &m))) return rc;
+        st.prepared = true;
+        st.prep_unit = unit;
+        st.prep_in = cur;
+    }
+    const rg_mf_mark_t cur_mark = mark_of(st, st.prep_arr, st.prep_serial);
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    const int64_t U = tb->num_users, R = tb->num_users + tb->num_items;
+    const int64_t cold_end = st.cfg.item_grad ? U : R;    // DP: items go through the exchange
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+
+    rg_mf_batch_t nbatch{};
+    rg_mf_work_t nw{};
+    rg_mf_mark_t nmark{};
+    const int narr = 1 - st.prep_arr;
+    if (next) {
+        if ((rc = keep_ahead(st, unit + 1))) return rc;
+        if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        nbatch = make_batch(st, *next, unit + 1);
+        nw = work_for(st, *next);
+        nmark = mark_of(st, narr, next_serial(st));
+    }
+    if ((rc = record(ev0, s))) return rc;
+    if ((rc = rg_mf_step_front(s, tb, &batch, &w, &cur_mark, &o, 0, cold_end, next ? &nbatch : nullptr,
+                               next ? &nw : nullptr, next ? &nmark : nullptr)))
+        return rc;
+    if ((rc = release(st, s))) return rc;               // clears `prepared` for this unit
+    if (next) {
+        st.prepared = true;
+        st.prep_unit = unit + 1;
+        st.prep_in = *next;
+        st.prep_serial = nmark.serial;
+        st.prep_arr = narr;
+    }
+    if (st.cfg.item_grad) {
+        if ((rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l))) return rc;
+        if (st.cfg.comm && (rc = rg::comm_begin(st.cfg.comm, s, st.cfg.item_grad,
+                                                tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+            return rc;
+        if ((rc = rg_mf_step_hot(s, tb, &batch, &w, hot_mark(st, cur_mark), &o, 0, U, nullptr))) return rc;
+        if ((rc = record(ev1, s))) return rc;
+        if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
+        if ((rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out))) return rc;
+    } else {
+        if ((rc = rg_mf_step_hot(s, tb, &batch, &w, hot_mark(st, cur_mark), &o, 0, R, &l))) return rc;
+        if ((rc = record(ev1, s))) return rc;
+    }
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
 void destroy(Stepper *st) {
     if (st->gen) hipStreamSynchronize(st->gen);
     if (st->prep) hipStreamSynchronize(st->prep);
+    hipDeviceSynchronize();
     for (int i = 0; i < kSlots; ++i) {
         if (st->gen_done[i]) hipEventDestroy(st->gen_done[i]);
         if (st->consumed[i]) hipEventDestroy(st->consumed[i]);
         if (st->words[i]) hipFree(st->words[i]);
         if (st->start_state[i]) hipFree(st->start_state[i]);
     }
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
         if (st->ready[i]) hipEventDestroy(st->ready[i]);
+        if (st->stamp[i]) hipFree(st->stamp[i]);
+    }
+    if (st->mark) hipEventDestroy(st->mark);
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
     rg::mt_jump_plan_destroy(st->jump);
@@ -241,12 +445,18 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     if (!st) { rg::set_error("rg_mf_stepper_create: out of memory"); return nullptr; }
     st->cfg = *cfg;
     st->set = cfg->current_set;
-    st->words_per_step = 2 * (int64_t)cfg->n_neg * cfg->global_cols;
+    st->W = 2 * (int64_t)cfg->n_neg * cfg->global_cols;
     if (st->cfg.neg_cols <= 0) st->cfg.neg_cols = cfg->global_cols;
-    st->release_late = env_flag("RG_RELEASE_LATE", false);
-    st->prep_after_pairs = env_flag("RG_PREP_AFTER_PAIRS", true);
-    // separate priorities keep the three streams on separate hardware queues: the
-    // walk is background work (lowest), the short prepare is on the step's path (highest)
+    {
+        const char *g = getenv("RG_MT_UNITS");
+        st->G = g ? atoi(g) : 4;
+        if (st->G < 1) st->G = 1;
+        if (st->G > 64) st->G = 64;
+    }
+    st->fused = env_flag("RG_FUSED", false);
+    st->hot_scan = env_flag("RG_HOT_SCAN", true);
+    // separate priorities keep the streams on separate hardware queues: the walk is
+    // background work (lowest), the short side prepare is on the step's path (highest)
     int least = 0, greatest = 0;
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     const int prio_mode = getenv("RG_STREAM_PRIO") ? atoi(getenv("RG_STREAM_PRIO")) : 1;
@@ -259,13 +469,15 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     const int ev_mode = getenv("RG_EVENT_MODE") ? atoi(getenv("RG_EVENT_MODE")) : 1;
     const unsigned evf = hipEventDisableTiming | (ev_mode == 1 ? hipEventDisableSystemFence
                                                  : ev_mode == 2 ? hipEventReleaseToDevice : 0u);
+    const size_t slot_words = (size_t)(st->G * st->W + RG_MT_PAD);
     for (int i = 0; e == hipSuccess && i < kSlots; ++i) {
         e = hipEventCreateWithFlags(&st->gen_done[i], evf);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&st->consumed[i], evf);
-        if (e == hipSuccess) e = hipMalloc(&st->words[i], (size_t)(st->words_per_step + RG_MT_PAD) * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc(&st->words[i], slot_words * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMalloc(&st->start_state[i], 625 * sizeof(uint32_t));
     }
     for (int i = 0; e == hipSuccess && i < 2; ++i) e = hipEventCreateWithFlags(&st->ready[i], evf);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&st->mark, evf);
     uint32_t pos = 624;
     if (e == hipSuccess) e = hipMemcpy(&pos, cfg->mt_state + 624, sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
@@ -274,7 +486,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         return nullptr;
     }
     st->cp_pos = (int32_t)pos;
-    if (env_flag("RG_MT_JUMP", false)) st->jump = rg::mt_jump_plan_create(st->words_per_step);
+    if (env_flag("RG_MT_JUMP", false)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
     return st;
 }
 
@@ -289,59 +501,20 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !cur) return rg::fail_arg("rg_mf_stepper_train: null handle/input");
     hipStream_t s = (hipStream_t)stream;
-    int64_t chunk;
-    int rc = acquire(*st, s, *cur, &chunk);
-    if (rc) return rc;
-    rg_mf_work_t w = st->cfg.work;
-    set_plan(w, *cur);
-    rg_mf_batch_t batch = make_batch(*st, *cur, chunk);
-    if ((rc = rg_mf_pairs(s, &st->cfg.tables[st->set], &batch, &w, 1))) return rc;
-    if (!st->release_late && (rc = release(*st, s))) return rc;
-    if ((rc = ensure_generated(*st, chunk + 1 + kAhead))) return rc;       // keep the walk ahead
-    if (next) {
-        const hipEvent_t after = (st->prep_after_pairs && !st->release_late) ? st->consumed[chunk % kSlots] : nullptr;
-        if ((rc = prepare(*st, chunk + 1, *next, after))) return rc;
-    }
-    st->cfg.step += 1;
-    const rg_opt_t o = opt_at(*st, st->cfg.step);
-    const rg_mf_loss_t l = loss_of(*st, cur->global_pos, loss_out);
-    hipError_t e;
-    const rg_mf_tables_t *tb = &st->cfg.tables[st->set];
-    const int64_t U = tb->num_users, R = tb->num_users + tb->num_items;
-    if (st->cfg.item_grad) {                     // user-sharded data parallel
-        if ((rc = rg_mf_grads(s, tb, &w, st->cfg.item_grad, U, R, &l))) return rc;
-        if (st->cfg.comm && (rc = rg::comm_begin(st->cfg.comm, s, st->cfg.item_grad,
-                                                 tb->num_items * (int64_t)(tb->dim + 1) + 1)))
-            return rc;
-    }
-    if (ev_apply_begin && (e = hipEventRecord((hipEvent_t)ev_apply_begin, s)) != hipSuccess)
-        return hip_fail("stepper: record event", e);
-    if (st->cfg.item_grad) {
-        if ((rc = rg_mf_apply(s, tb, &w, &o, 0, U, nullptr))) return rc;
-    } else {
-        if ((rc = rg_mf_apply(s, tb, &w, &o, 0, -1, &l))) return rc;
-    }
-    if (ev_apply_end && (e = hipEventRecord((hipEvent_t)ev_apply_end, s)) != hipSuccess)
-        return hip_fail("stepper: record event", e);
-    if (st->cfg.item_grad) {
-        if (st->cfg.comm && (rc = rg::comm_end(st->cfg.comm, s))) return rc;
-        if ((rc = rg_mf_apply_dense(s, tb, st->cfg.item_grad, &o, U, R, loss_out))) return rc;
-    }
-    if (st->release_late && (rc = release(*st, s))) return rc;
-    st->set = 1 - st->set;
-    return RG_OK;
+    if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
+        return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+    return train_split(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
 }
 
 extern "C" int rg_mf_stepper_acquire(void *h, void *stream, const rg_mf_step_in_t *cur, rg_mf_batch_t *batch_out,
                                      rg_mf_work_t *work_out) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !cur || !batch_out || !work_out) return rg::fail_arg("rg_mf_stepper_acquire: null argument");
-    int64_t chunk;
-    int rc = acquire(*st, (hipStream_t)stream, *cur, &chunk);
+    int64_t unit;
+    int rc = acquire(*st, (hipStream_t)stream, *cur, &unit);
     if (rc) return rc;
-    *batch_out = make_batch(*st, *cur, chunk);
-    *work_out = st->cfg.work;
-    set_plan(*work_out, *cur);
+    *batch_out = make_batch(*st, *cur, unit);
+    *work_out = work_for(*st, *cur);
     return RG_OK;
 }
 
@@ -379,23 +552,28 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
     if (!st || !host_state) return rg::fail_arg("rg_mf_stepper_sync_mt: null argument");
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return hip_fail("stepper: sync", e);
-    if (direction == 0) {   // device -> host: the state after the last CONSUMED chunk
-        const bool ahead = st->generated > st->taken;
-        const int slot = (int)(st->taken % kSlots);
+    if (direction == 0) {   // device -> host: the state after the last CONSUMED unit
+        const int64_t rel = st->taken - st->unit_base;
+        const int64_t slot_rel = rel / st->G, inside = rel % st->G;
+        const bool ahead = st->gen_slots > slot_rel;
+        const int slot = (int)(slot_rel % kSlots);
         const uint32_t *src = ahead ? st->start_state[slot] : st->cfg.mt_state;
         const bool window = ahead ? st->win_at[slot] : st->window_form;
         const int32_t pos = ahead ? st->pos_at[slot] : st->cp_pos;
         uint32_t dev[625];
         e = hipMemcpy(dev, src, 625 * sizeof(uint32_t), hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hip_fail("stepper: copy MT state", e);
-        if (!window) {
-            std::memcpy(host_state, dev, sizeof(dev));
-            return RG_OK;
-        }
-        return rg_mt_window_to_cpython(dev, pos, host_state);
+        int rc = RG_OK;
+        if (!window) std::memcpy(host_state, dev, sizeof(dev));
+        else rc = rg_mt_window_to_cpython(dev, pos, host_state);
+        if (rc == RG_OK && inside > 0) rc = rg_mt_advance_host(host_state, inside * st->W);
+        return rc;
     }
-    // host -> device: chunks generated ahead are dropped
-    st->generated = st->taken;
+    // host -> device: words generated ahead are dropped; unit numbering restarts here
+    st->unit_base = st->taken;
+    st->gen_slots = 0;
+    st->waited_slot = -1;
+    st->waited_stream = nullptr;
     st->prepared = false;
     st->window_form = false;
     st->cp_pos = (int32_t)host_state[624];

@@ -65,3 +65,22 @@ def test_window_to_cpython_rejects_bad_pos(lib):
     out = np.zeros(625, np.uint32)
     assert lib.rg_mt_window_to_cpython(_p(w), 0, _p(out)) != 0
     assert lib.rg_mt_window_to_cpython(_p(w), 625, _p(out)) != 0
+
+
+@pytest.mark.parametrize("pos,k", [(624, 0), (624, 1), (0, 624), (17, 607), (17, 608), (300, 81920 * 3 + 5),
+                                   (1, 5 * 624)])
+def test_advance_host_equals_getrandbits(lib, pos, k):
+    """rg_mt_advance_host (mid-slot export of the stepper's word ring): the state after
+    k raw words equals CPython's after k calls of getrandbits(32)."""
+    import random
+    from oracle import rng as orng2
+    st = orng2.py_seed_state(5)
+    st[624] = pos
+    r = random.Random()
+    r.setstate((3, tuple(int(v) for v in st), None))
+    for _ in range(k):
+        r.getrandbits(32)
+    ref = orng2.state_from_python(r.getstate())
+    got = st.copy()
+    assert lib.rg_mt_advance_host(_p(got), k) == 0
+    assert (got == ref).all()
