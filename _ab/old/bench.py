@@ -9,9 +9,6 @@ GPU (weak scaling), each with n = 5 negatives drawn bit-exactly from the CPython
 MT19937 stream, the BPR loss on the neg.view(n, B) pairing, backward, and a dense
 coupled-L2 Adam update of every row of the four BilinearNet tables (the
 reference's semantics: implicit.py:347-364, spotlight/optimizers.py:10-16).
-The native stepper runs it as two launches (rg_mf_step_front: pair pass | next
-step's prepare | update of the rows the batch does not touch; rg_mf_step_hot:
-update of the touched rows); RG_FUSED=0 selects the split pairs -> apply step.
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
 With N > 1 ranks (one process per GPU) the step is user-sharded
@@ -21,9 +18,9 @@ replicated and their gradient is all-reduced with RCCL inside the native step,
 overlapped with the user-shard update.
 
 Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
-max over ranks of the timed wall time.  `roofline` is for the step's two kernels
-(front + hot: every algorithmic byte of the step), timed with HIP events on the
-stream they are launched on; `cpu_baseline` times the CPU restatement (oracle/, the
+max over ranks of the timed wall time.  `roofline` is for the dominant kernel
+(rg_mf_apply, the dense optimizer pass), timed with HIP events on the stream it
+is launched on; `cpu_baseline` times the CPU restatement (oracle/, the
 reference's algorithm incl. its random.choices sampler) on a bounded sample.
 """
 import argparse
@@ -74,7 +71,7 @@ def parse():
     ap.add_argument("--gan-slate", type=int, default=5)
     ap.add_argument("--gan-emb", type=int, default=5)
     ap.add_argument("--events-every", type=int, default=8,
-                    help="record the dominant kernel's timing events on every k-th timed step")
+                    help="record the rg_mf_apply timing events on every k-th timed step")
     return ap.parse_args()
 
 
@@ -301,8 +298,6 @@ def main():
     if not os.path.exists(rg_build.LIB):
         rg_build.build()
     d, B, n = args.dim, args.batch, args.neg
-    # the stepper's overlapped step (rg_stepper.cpp train_fused) unless disabled
-    fused = os.environ.get("RG_FUSED", "0") == "1" and args.loss != "adaptive_hinge"
     data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
     U, I = data.num_users, data.num_items
     torch.manual_seed(0)                               # mf_spotlight.py:37
@@ -391,27 +386,16 @@ def main():
             from recommendation_gans_amd import _lib
             ms = [_lib.elapsed_ms(a, b) for a, b in (ev for ev in evs if ev is not None)]
             avg = float(np.mean(ms)) * 1e-3
-            if fused:
-                # the events bracket rg_mf_step_front (pairs | next prepare | cold-row update)
-                # and rg_mf_step_hot (touched-row update): the whole step's algorithmic bytes
-                # (DP: up to the user-shard update; the item update follows the exchange)
-                alg = gather + ids + user_adam
-                kname = "rg_mf_step_front + rg_mf_step_hot (mf_front_kernel, mf_hot_kernel)"
-            else:
-                # rg_mf_apply_prepare: the dense optimizer pass and the next step's prepare
-                # (ids in, prepared pairs out) in one launch
-                alg = user_adam + ids
-                kname = "rg_mf_apply_prepare (mf_back_kernel: dense update + next-step prepare)"
-            ach = alg / avg / 1e9
-            out["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": ach,
+            ach = user_adam / avg / 1e9
+            out["roofline"] = {"bound": "hbm", "kernel": "rg_mf_apply (mf_apply_kernel)", "achieved": ach,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                               "traffic": None, "algorithmic_bytes_per_launch": alg,
+                               "traffic": None, "algorithmic_bytes_per_launch": user_adam,
                                "avg_launch_us": avg * 1e6}
-            pmc = os.path.join(ROOT, "profiles", "pmc_step.json" if fused else "pmc_back.json")
+            pmc = os.path.join(ROOT, "profiles", "pmc_apply.json")
             if world == 1 and os.path.exists(pmc):
                 p = json.load(open(pmc))
                 if p.get("dim") == d and p.get("batch") == B:
-                    out["roofline"]["traffic"] = p.get("hbm_bytes_per_step" if fused else "hbm_bytes_per_launch")
+                    out["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
         out["final_loss"] = loss_last
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)

@@ -167,9 +167,6 @@ int rg_mt_window_host(const uint32_t *state_host, int64_t D, uint32_t *window_ou
 /* Window-form state x[P-624 .. P) -> CPython's getstate() layout for the same stream
  * position with position `pos` (1..624) inside its block.  Host memory only. */
 int rg_mt_window_to_cpython(const uint32_t *window_host, int32_t pos, uint32_t *state_out_host);
-/* Advance a CPython getstate() layout state (625 words, host memory) by k raw words
- * in place, as k calls of getrandbits(32) would. */
-int rg_mt_advance_host(uint32_t *state_host, int64_t k);
 
 /* Number of float loss partials rg_mf_pairs writes for `cols` columns. */
 int64_t rg_mf_partials_len(int64_t cols, int32_t dim);
@@ -182,42 +179,6 @@ int64_t rg_mf_plan_units_per_block(int32_t dim);
  * Fully parallel; depends only on the words, the pool, the plan and the ids, so it
  * can run ahead on another stream. */
 int rg_mf_prepare(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work);
-
-/* Row marks of one prepared step (the overlapped step below).  stamp: [U + I] int32
- * (caller-owned, zero-initialised), serial: nonzero, unique per marked prepare. */
-typedef struct rg_mf_mark {
-    int32_t *stamp;
-    int64_t num_users;
-    int32_t serial, pad_;
-} rg_mf_mark_t;
-
-/* rg_mf_prepare that also stamps every row the step's pairs touch with
- * mark->serial; the first pair to stamp a row gets the row's ownership flag (bit 31
- * of its prepared id; rg_mf_pairs and the NCF kernels ignore the flags). */
-int rg_mf_prepare_marked(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work,
-                         const rg_mf_mark_t *mark);
-
-/* The overlapped training step (implicit.py:347-364 as two launches):
- *   rg_mf_step_front: rg_mf_pairs(backward) of `cur` (prepared with cur_mark), the
- *     marked prepare of `next` (optional; its own stamp array and serial), and the
- *     optimizer update of every row in [cold_begin, cold_end) whose stamp is not
- *     cur_mark->serial (no data gradient: weight decay only), all in ONE grid;
- *   rg_mf_step_hot: the update of every touched row in [row_begin, row_end), pulling
- *     the lists / partials of the pair pass, plus the loss: rows found by a scan of
- *     the range for cur_mark's serial (mark non-null) or through the owner-flagged
- *     ids of cur's pairs (mark null).
- * Together they equal rg_mf_pairs + rg_mf_apply over the same rows, bit for bit.
- * Not for adaptive hinge (its backward needs the global max first). */
-int rg_mf_step_front(void *stream, const rg_mf_tables_t *tables, const rg_mf_batch_t *cur, rg_mf_work_t *work,
-                     const rg_mf_mark_t *cur_mark, const rg_opt_t *opt, int64_t cold_begin, int64_t cold_end,
-                     const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mf_mark_t *next_mark);
-/* The cold-row part of rg_mf_step_front as its own launch (rows in range whose
- * stamp is not mark->serial; weight decay only), for a two-stream schedule. */
-int rg_mf_step_cold(void *stream, const rg_mf_tables_t *tables, const rg_mf_mark_t *mark, const rg_opt_t *opt,
-                    int64_t row_begin, int64_t row_end);
-int rg_mf_step_hot(void *stream, const rg_mf_tables_t *tables, const rg_mf_batch_t *cur, rg_mf_work_t *work,
-                   const rg_mf_mark_t *mark, const rg_opt_t *opt, int64_t row_begin, int64_t row_end,
-                   const rg_mf_loss_t *loss);
 
 /* Forward of all pairs of the step, the loss terms, dL/dz, and the per-row
  * contribution lists (+ planned partials) consumed by rg_mf_apply / rg_mf_grads.
@@ -232,13 +193,6 @@ int rg_mf_pairs(void *stream, const rg_mf_tables_t *tables, const rg_mf_batch_t 
  * row in the range (coupled weight decay touches all rows).  loss: optional. */
 int rg_mf_apply(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
                 int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss);
-
-/* rg_mf_apply and the rg_mf_prepare of the NEXT step (optional: next null) in one
- * launch (the prepare runs in extra workgroups beside the HBM-bound update), so a
- * training step needs no side stream and no per-step cross-stream event. */
-int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
-                        int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss, const rg_mf_batch_t *next,
-                        const rg_mf_work_t *next_work);
 
 /* Pull the DATA gradient (no weight decay) of the rows in range into the flat
  * buffer grad_dev = [n*dim row grads | n bias grads | loss], n = row_end - row_begin

@@ -1,0 +1,271 @@
+"""oracle/mf.py -- TEST INFRASTRUCTURE ONLY.
+
+CPU restatement (torch-CPU fp32, explicit formulas, no autograd) of the
+reference's matrix-factorisation training step:
+
+  * BilinearNet.__init__ / forward      spotlight/factorization/representations.py:40-91
+      ScaledEmbedding N(0, 1/d) init     spotlight/layers.py:30-37
+      ZeroEmbedding bias init            spotlight/layers.py:49-56
+  * pointwise_loss (BCE, log>=-100)     spotlight/losses.py:20-56
+  * bpr_loss  1 - sigmoid(pos - neg)    spotlight/losses.py:59-96   (pairing neg.view(n,B))
+  * hinge_loss                          spotlight/losses.py:99-130  (pairing neg.view(n,B))
+  * adaptive_hinge_loss (global max)    spotlight/losses.py:133-172 (flat negatives, as implicit.py:199 runs it)
+  * autograd of the above + embedding_dense_backward (implicit.py:361)
+  * torch.optim Adam / SGD / RMSprop single-tensor CPU update, coupled L2
+      spotlight/optimizers.py:4-22, implicit.py:363
+  * run_train_iteration                 implicit.py:347-364 (negatives drawn with
+      random.choices over the pool, k = n * batch_size even for a partial batch)
+
+The gradient formulas mirror ATen's backward kernels (binary_cross_entropy_backward
+with EPSILON = 1e-12, sigmoid_backward, clamp_backward with x >= min passing,
+max(dim=0) backward scattering to the argmax).  It is pinned against golden
+vectors generated from the reference itself (tests/golden/make_golden.py).
+"""
+import math
+import random
+
+import numpy as np
+import torch
+
+from . import rng as orng
+
+LOSSES = ("pointwise", "bpr", "hinge", "adaptive_hinge")
+OPTIMIZERS = ("adam", "sgd", "rms")
+
+
+# ------------------------------------------------------------------ init
+def init_tables(num_users, num_items, dim):
+    """Draw the four BilinearNet tables exactly as the reference constructor does:
+    user table normal_(0, 1/d), item table normal_(0, 1/d) from the current torch
+    CPU generator (representations.py:50-57 -> layers.py:35), biases zero."""
+    U = torch.empty(num_users, dim).normal_(0, 1.0 / dim)
+    I = torch.empty(num_items, dim).normal_(0, 1.0 / dim)
+    ub = torch.zeros(num_users, 1)
+    ib = torch.zeros(num_items, 1)
+    return U, I, ub, ib
+
+
+# ------------------------------------------------------------------ forward
+def scores(U, I, ub, ib, u, i):
+    """representations.py:80-91: sigmoid(sum(U[u]*I[i]) + ub[u] + ib[i])."""
+    dot = (U[u] * I[i]).sum(1)
+    return torch.sigmoid(dot + ub[u, 0] + ib[i, 0])
+
+
+# ------------------------------------------------------------------ losses
+def loss_and_dp(kind, p_pos, p_neg, n, batch_size, den=None):
+    """Return (loss, dL/dp_pos, dL/dp_neg) for the loss selected by ``kind``.
+
+    p_pos: (Bp,) positive scores (Bp <= batch_size on the last partial batch).
+    p_neg: (n*batch_size,) negative scores, flat as drawn (implicit.py:352).
+    den:   None -> the reference's means over this batch.  (pos_den, neg_den) ->
+           sums divided by those counts instead: one rank's share of a loss whose
+           means run over the positives / negatives of every data-parallel rank.
+    """
+    Bp = p_pos.shape[0]
+    pos_den, neg_den = (Bp, p_neg.shape[0]) if den is None else den
+    if kind == "pointwise":
+        if den is None:
+            lp = -torch.clamp(torch.log(p_pos), min=-100.0).mean()
+            ln = -torch.clamp(torch.log(1.0 - p_neg), min=-100.0).mean()
+        else:
+            lp = -torch.clamp(torch.log(p_pos), min=-100.0).sum() / pos_den
+            ln = -torch.clamp(torch.log(1.0 - p_neg), min=-100.0).sum() / neg_den
+        eps = 1e-12
+        dpp = (1.0 / pos_den) * (p_pos - 1.0) / torch.clamp((1.0 - p_pos) * p_pos, min=eps)
+        dpn = (1.0 / neg_den) * (p_neg - 0.0) / torch.clamp((1.0 - p_neg) * p_neg, min=eps)
+        return lp + ln, dpp, dpn
+    if kind in ("bpr", "hinge"):
+        negm = p_neg.view(n, batch_size)[:, :Bp]
+        g = 1.0 / (n * pos_den)
+        dpn = torch.zeros(n, batch_size, dtype=p_pos.dtype)
+        if kind == "bpr":
+            s = torch.sigmoid(p_pos[None, :] - negm)
+            loss = (1.0 - s).mean() if den is None else (1.0 - s).sum() * g
+            dx = (-g) * (1.0 - s) * s          # d/dx of (1 - sigmoid(x)), x = pos - neg
+            dpp = dx.sum(0)
+            dpn[:, :Bp] = -dx
+        else:
+            x = negm - p_pos[None, :] + 1.0
+            loss = torch.clamp(x, min=0.0).mean() if den is None else torch.clamp(x, min=0.0).sum() * g
+            dx = g * (x >= 0).to(p_pos.dtype)
+            dpp = -dx.sum(0)
+            dpn[:, :Bp] = dx
+        return loss, dpp, dpn.reshape(-1)
+    if kind == "adaptive_hinge":
+        m, idx = torch.max(p_neg, 0)
+        x = m - p_pos + 1.0
+        loss = torch.clamp(x, min=0.0).mean() if den is None else torch.clamp(x, min=0.0).sum() / pos_den
+        dx = (1.0 / pos_den) * (x >= 0).to(p_pos.dtype)
+        dpn = torch.zeros_like(p_neg)
+        dpn[int(idx)] = dx.sum()
+        return loss, -dx, dpn
+    raise ValueError(kind)
+
+
+def dense_grads(U, I, ub, ib, u, i, dz):
+    """embedding_dense_backward for the four tables given dL/dz per pair."""
+    dU = torch.zeros_like(U)
+    dI = torch.zeros_like(I)
+    dub = torch.zeros_like(ub)
+    dib = torch.zeros_like(ib)
+    dU.index_add_(0, u, dz[:, None] * I[i])
+    dI.index_add_(0, i, dz[:, None] * U[u])
+    dub.index_add_(0, u, dz[:, None])
+    dib.index_add_(0, i, dz[:, None])
+    return dU, dI, dub, dib
+
+
+# ------------------------------------------------------------------ optimizers
+class Optim:
+    """torch.optim single-tensor CPU update (spotlight/optimizers.py:4-22)."""
+
+    def __init__(self, kind, params, lr, weight_decay, betas=(0.5, 0.999), eps=1e-8, alpha=0.99):
+        assert kind in OPTIMIZERS
+        self.kind, self.lr, self.wd = kind, lr, weight_decay
+        self.b1, self.b2 = betas
+        self.eps, self.alpha = eps, alpha
+        self.t = 0
+        self.state = [(torch.zeros_like(p), torch.zeros_like(p)) for p in params]
+
+    def step(self, params, grads):
+        self.t += 1
+        t = self.t
+        for k, (p, g) in enumerate(zip(params, grads)):
+            m, v = self.state[k]
+            if self.wd != 0:
+                g = g + self.wd * p
+            if self.kind == "sgd":
+                p.add_(g, alpha=-self.lr)
+            elif self.kind == "adam":
+                m.lerp_(g, 1 - self.b1)
+                v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+                bc1 = 1 - self.b1 ** t
+                bc2 = 1 - self.b2 ** t
+                denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+                p.addcdiv_(m, denom, value=-(self.lr / bc1))
+            else:  # rms
+                v.mul_(self.alpha).addcmul_(g, g, value=1 - self.alpha)
+                avg = v.sqrt().add_(self.eps)
+                p.addcdiv_(g, avg, value=-self.lr)
+
+
+# ------------------------------------------------------------------ the step
+class MFOracle:
+    """One ``run_train_iteration`` (implicit.py:347-364) per call to ``step``.
+
+    ``pool_u``/``pool_i``: the negative pool (get_negative_samples output).
+    ``mt_state``: np.uint32[625] CPython MT state; advanced in place (C restatement),
+    or, with ``python_sampler=True``, a ``random.Random`` drawing from a list of
+    tuples exactly like the reference (the timed CPU-baseline mode).
+    """
+
+    def __init__(self, U, I, ub, ib, pool_u, pool_i, mt_state, loss="pointwise",
+                 optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=5, batch_size=256,
+                 betas=(0.5, 0.999), python_sampler=False):
+        assert loss in LOSSES
+        self.params = [U, I, ub, ib]
+        self.loss_kind = loss
+        self.n = n_neg
+        self.batch_size = batch_size
+        self.opt = Optim(optimizer, self.params, lr, weight_decay, betas=betas)
+        self.pool_u = torch.as_tensor(np.asarray(pool_u, dtype=np.int64))
+        self.pool_i = torch.as_tensor(np.asarray(pool_i, dtype=np.int64))
+        self.state = mt_state
+        self.python_sampler = python_sampler
+        if python_sampler:
+            self.pool_list = list(zip(np.asarray(pool_u).tolist(), np.asarray(pool_i).tolist()))
+            self.rand = random.Random()
+            self.rand.setstate(orng.state_to_python(mt_state))
+
+    def draw(self, k):
+        if self.python_sampler:
+            nu, ni = zip(*self.rand.choices(self.pool_list, k=k))
+            return None, torch.from_numpy(np.array(nu)).long(), torch.from_numpy(np.array(ni)).long()
+        idx = orng.py_choices_indices(self.state, len(self.pool_u), k)
+        t = torch.from_numpy(idx)
+        return idx, self.pool_u[t], self.pool_i[t]
+
+    def step(self, pos_u, pos_i, return_all=False, den=None, exchange=None):
+        """``den``/``exchange``: the user-sharded data-parallel step (one rank's shard,
+        recommendation_gans_amd/sharding.py): loss means over every rank's positives
+        and negatives, and ``exchange(grads) -> grads`` (the item-gradient all-reduce)
+        between backward and the optimizer update."""
+        U, I, ub, ib = self.params
+        pos_u = torch.as_tensor(pos_u).long()
+        pos_i = torch.as_tensor(pos_i).long()
+        p_pos = scores(U, I, ub, ib, pos_u, pos_i)
+        idx, nu, ni = self.draw(self.n * self.batch_size)
+        p_neg = scores(U, I, ub, ib, nu, ni)
+        loss, dpp, dpn = loss_and_dp(self.loss_kind, p_pos, p_neg, self.n, self.batch_size, den=den)
+        dzp = dpp * (1.0 - p_pos) * p_pos
+        dzn = dpn * (1.0 - p_neg) * p_neg
+        u = torch.cat([pos_u, nu])
+        i = torch.cat([pos_i, ni])
+        grads = dense_grads(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
+        if exchange is not None:
+            grads = exchange(grads)
+        self.opt.step(self.params, grads)
+        if return_all:
+            return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx,
+                        neg_u=nu, neg_i=ni, grads=grads)
+        return float(loss)
+
+
+def val_loss(oracle, pos_u, pos_i):
+    """run_val_iteration (implicit.py:366-379): same draw, loss only, no update."""
+    U, I, ub, ib = oracle.params
+    p_pos = scores(U, I, ub, ib, torch.as_tensor(pos_u).long(), torch.as_tensor(pos_i).long())
+    _, nu, ni = oracle.draw(oracle.n * oracle.batch_size)
+    p_neg = scores(U, I, ub, ib, nu, ni)
+    loss, _, _ = loss_and_dp(oracle.loss_kind, p_pos, p_neg, oracle.n, oracle.batch_size)
+    return float(loss)
+
+
+def fit(oracle, train_u, train_i, valid_u, valid_i, np_state, n_iter):
+    """ImplicitFactorizationModel.fit (implicit.py:238-345) for the MF path.
+
+    ``np_state``: 625-word NumPy legacy state of the model's RandomState *after*
+    the constructor's set_seed draw (implicit.py:146).  Returns
+    (summary rows [(train_loss, validation_loss, epoch)], best params, best epoch).
+    """
+    perm = orng.np_shuffle_indices(np_state, len(train_u))          # implicit.py:262
+    tu, ti = np.asarray(train_u)[perm], np.asarray(train_i)[perm]
+    B = oracle.batch_size
+    rows, best, best_val, best_epoch = [], None, None, -1
+    for epoch in range(n_iter):
+        tl = [oracle.step(tu[s:s + B], ti[s:s + B]) for s in range(0, len(tu), B)]
+        if np.isnan(np.mean(tl)) or np.mean(tl) == 0.0:
+            raise ValueError("Degenerate epoch loss: {}".format(np.mean(tl)))
+        vl = [val_loss(oracle, valid_u[s:s + B], valid_i[s:s + B]) for s in range(0, len(valid_u), B)]
+        v = float(np.mean(vl))          # == valid_epoch_loss / nbatches
+        if best_val is None or v < best_val:
+            best = [p.clone() for p in oracle.params]
+            best_val, best_epoch = v, epoch
+        rows.append((float(np.mean(tl)), float(np.mean(vl)), epoch))
+    return rows, best, best_epoch
+
+
+def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0):
+    """Parity verdict used by the GPU tests and smoke() (returns (ok, message)).
+
+    Passes if ||got - ref32|| <= rtol * ||ref32|| (the north_star's 1e-5 relative,
+    as a tensor norm).  After an Adam/RMSprop step an element whose gradient sum
+    cancels to ~eps has its update g/(|g|+eps) set by the last bits of that sum, so a
+    small tensor (the biases) can exceed that while both fp32 results are equally
+    right; then, given the same computation in float64 (``ref64``), the GPU result
+    must be as close to it as the fp32 reference restatement is: ||got - ref64|| <=
+    band * ||ref32 - ref64|| + rtol/10 * ||ref64||."""
+    g = torch.as_tensor(got).double().reshape(-1).cpu()
+    r = torch.as_tensor(ref32).double().reshape(-1)
+    e32 = float((g - r).norm())
+    n32 = float(r.norm())
+    if e32 <= rtol * max(n32, 1e-30):
+        return True, f"rel {e32 / max(n32, 1e-30):.2e}"
+    if ref64 is None:
+        return False, f"rel {e32 / max(n32, 1e-30):.2e} > {rtol}"
+    r64 = torch.as_tensor(ref64).double().reshape(-1)
+    eg = float((g - r64).norm())
+    er = float((r - r64).norm())
+    ok = eg <= band * er + 0.1 * rtol * float(r64.norm())
+    return ok, (f"rel-to-fp32 {e32 / max(n32, 1e-30):.2e}; |gpu-fp64| {eg:.3e} vs |fp32-fp64| {er:.3e}")

@@ -1,0 +1,132 @@
+"""oracle/ncf.py -- TEST INFRASTRUCTURE ONLY.
+
+CPU restatement (torch-CPU fp32, explicit formulas, no autograd) of the
+reference's NCF training step:
+
+  * MLP.__init__ / forward             spotlight/dnn_models/mlp.py:5-46
+      layers [2E, E, ..., 8] -> 1      ncf_spotlight.py:53-56
+      Linear -> LeakyReLU(0.1) -> Dropout(0.5) per hidden layer, Linear -> Sigmoid
+  * losses on (N, 1) scores            spotlight/losses.py:20-172 (as oracle/mf.py)
+  * autograd of the above              implicit.py:361 (linear / leaky_relu /
+      dropout / sigmoid backward as ATen computes them, dense embedding grads)
+  * Adam over every parameter          spotlight/optimizers.py:10-16, implicit.py:363
+
+Dropout masks are inputs (the reference draws them from torch's CPU generator;
+tests/golden records them with forward hooks), scaled by 1 / (1 - 0.5) = 2.
+Pinned by tests/golden/mlp_*.npz (made by importing the reference).
+"""
+import torch
+
+from . import mf as omf
+from . import rng as orng
+
+LRELU = 0.1
+DROP_SCALE = 2.0
+
+
+def layer_sizes(E):
+    """ncf_spotlight.py:53-55: [2**x for x in reversed(range(3, log2(2E) + 1))]."""
+    import math
+    top = int(math.log2(E * 2))
+    return [2 ** x for x in reversed(range(3, top + 1))]
+
+
+class MLPParams:
+    """Parameters in the reference's named_parameters() order."""
+
+    NAMES_FMT = ("embedding_user.weight", "embedding_item.weight")
+
+    def __init__(self, tensors, names):
+        self.t = list(tensors)
+        self.names = list(names)
+
+    def emb(self):
+        return self.t[0], self.t[1]
+
+    def linears(self):
+        return [(self.t[k], self.t[k + 1]) for k in range(2, len(self.t), 2)]
+
+
+def forward(P, u, i, masks):
+    """Returns p (N,1) and the cache for backward.  ``masks``: per hidden layer (N, out) 0/1."""
+    Ue, Ie = P.emb()
+    x = torch.cat([Ue[u], Ie[i]], dim=-1)
+    lin = P.linears()
+    cache = {"x": x, "z": [], "a": [x]}
+    a = x
+    for k, (W, b) in enumerate(lin[:-1]):
+        z = a.mm(W.t()) + b
+        r = torch.where(z > 0, z, z * LRELU)
+        a = r * (masks[k].to(z.dtype) * DROP_SCALE)
+        cache["z"].append(z)
+        cache["a"].append(a)
+    W, b = lin[-1]
+    logit = a.mm(W.t()) + b
+    p = torch.sigmoid(logit)
+    cache["p"] = p
+    return p, cache
+
+
+def backward(P, u, i, masks, cache, dp):
+    """dp: dL/dp (N,1).  Returns dense grads in parameter order."""
+    p = cache["p"]
+    dz = dp * (1 - p) * p
+    lin = P.linears()
+    grads_lin = []
+    for k in range(len(lin) - 1, -1, -1):
+        W, b = lin[k]
+        a_prev = cache["a"][k]
+        dW = dz.t().mm(a_prev)
+        db = dz.sum(0)
+        grads_lin.append((dW, db))
+        da = dz.mm(W)
+        if k > 0:
+            z = cache["z"][k - 1]
+            da = da * (masks[k - 1].to(z.dtype) * DROP_SCALE)
+            dz = torch.where(z > 0, da, da * LRELU)
+        else:
+            dx = da
+    grads_lin.reverse()
+    Ue, Ie = P.emb()
+    E = Ue.shape[1]
+    dU = torch.zeros_like(Ue).index_add_(0, u, dx[:, :E])
+    dI = torch.zeros_like(Ie).index_add_(0, i, dx[:, E:])
+    out = [dU, dI]
+    for dW, db in grads_lin:
+        out += [dW, db]
+    return out
+
+
+class NCFOracle:
+    """One run_train_iteration (implicit.py:347-364) of the NCF MLP per ``step``."""
+
+    def __init__(self, tensors, names, pool_u, pool_i, mt_state, loss="pointwise", lr=1e-2, weight_decay=1e-5,
+                 n_neg=5, batch_size=256, betas=(0.5, 0.999)):
+        self.P = MLPParams(tensors, names)
+        self.loss_kind = loss
+        self.n, self.batch_size = n_neg, batch_size
+        self.opt = omf.Optim("adam", self.P.t, lr, weight_decay, betas=betas)
+        self.pool_u = torch.as_tensor(pool_u).long()
+        self.pool_i = torch.as_tensor(pool_i).long()
+        self.state = mt_state
+
+    def draw(self, k):
+        idx = orng.py_choices_indices(self.state, len(self.pool_u), k)
+        t = torch.from_numpy(idx)
+        return idx, self.pool_u[t], self.pool_i[t]
+
+    def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
+        u = torch.as_tensor(pos_u).long()
+        i = torch.as_tensor(pos_i).long()
+        p_pos, c_pos = forward(self.P, u, i, masks_pos)
+        idx, nu, ni = self.draw(self.n * self.batch_size)
+        p_neg, c_neg = forward(self.P, nu, ni, masks_neg)
+        kind = self.loss_kind
+        loss, dpp, dpn = omf.loss_and_dp(kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n, self.batch_size)
+        g1 = backward(self.P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1))
+        g2 = backward(self.P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1))
+        grads = [a + b for a, b in zip(g1, g2)]
+        self.opt.step(self.P.t, grads)
+        if return_all:
+            return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx, neg_u=nu, neg_i=ni, grads=grads)
+        return float(loss)

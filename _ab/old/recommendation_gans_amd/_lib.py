@@ -54,11 +54,6 @@ class MFWork(ctypes.Structure):
         "part_row", "part_bias")]
 
 
-class MFMark(ctypes.Structure):
-    _fields_ = [("stamp", ctypes.c_void_p), ("num_users", ctypes.c_int64), ("serial", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
-
-
 class MFLoss(ctypes.Structure):
     _fields_ = [("n_partials", ctypes.c_int64), ("inv_a", ctypes.c_double), ("inv_b", ctypes.c_double),
                 ("out", ctypes.c_void_p)]
@@ -170,7 +165,6 @@ SIGNATURES = [
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("rg_mt_window_to_cpython", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
-    ("rg_mt_advance_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("rg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("rg_comm_create", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
@@ -180,24 +174,10 @@ SIGNATURES = [
     ("rg_mf_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     ("rg_mf_plan_units_per_block", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_mf_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
-    ("rg_mf_prepare_marked", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
-                                            ctypes.POINTER(MFMark)]),
     ("rg_mf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
                                    ctypes.POINTER(MFWork), ctypes.c_int32]),
     ("rg_mf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
                                    ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
-    ("rg_mf_apply_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
-                                           ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss),
-                                           ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
-    ("rg_mf_step_front", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
-                                        ctypes.POINTER(MFWork), ctypes.POINTER(MFMark), ctypes.POINTER(Opt),
-                                        ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFBatch),
-                                        ctypes.POINTER(MFWork), ctypes.POINTER(MFMark)]),
-    ("rg_mf_step_cold", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFMark),
-                                       ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
-    ("rg_mf_step_hot", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
-                                      ctypes.POINTER(MFWork), ctypes.POINTER(MFMark), ctypes.POINTER(Opt),
-                                      ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
     ("rg_mf_grads", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
     ("rg_mf_apply_dense", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,

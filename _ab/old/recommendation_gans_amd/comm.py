@@ -1,0 +1,51 @@
+"""RCCL communicator of the librg_hip.so data-parallel step (include/rg_hip.h,
+rg_comm_*).  torch.distributed sets up the process group (one process per GPU,
+RANK / WORLD_SIZE / MASTER_ADDR from torchrun) and carries the 128-byte unique
+id; the per-step item-gradient all-reduce then runs inside rg_mf_stepper_train on
+the communicator's own stream, overlapped with the user-shard update."""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import RG_COMM_ID_BYTES, check, ptr
+
+
+class RcclComm:
+    def __init__(self, device, group=None):
+        import torch.distributed as dist
+        self.lib = _lib.load()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        uid = np.zeros(RG_COMM_ID_BYTES, dtype=np.uint8)
+        if self.rank == 0:
+            check(self.lib.rg_comm_unique_id(uid.ctypes.data_as(ctypes.c_void_p), RG_COMM_ID_BYTES),
+                  "rg_comm_unique_id")
+        box = [uid.tobytes()]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = np.frombuffer(box[0], dtype=np.uint8).copy()
+        index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.handle = self.lib.rg_comm_create(uid.ctypes.data_as(ctypes.c_void_p), self.world, self.rank, index)
+        if not self.handle:
+            raise RuntimeError("rg_comm_create: " + self.lib.rg_last_error().decode())
+
+    def allreduce_(self, t):
+        """In-place fp32 sum over ranks, ordered on the current stream."""
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
+            raise ValueError("allreduce_ takes a contiguous fp32 tensor on the communicator's device")
+        check(self.lib.rg_comm_allreduce_sum_f32(self.handle, _lib.stream_handle(), ptr(t), t.numel()),
+              "rg_comm_allreduce_sum_f32")
+        return t
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.rg_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,118 @@
+// RCCL communicator for the user-sharded data-parallel MF step (host code).
+//
+// One process per GPU.  The unique id is created by rank 0 (rg_comm_unique_id)
+// and broadcast by the caller (torch.distributed), then every rank builds its
+// communicator (rg_comm_create).  The collective runs on the communicator's own
+// stream, fenced by events against the caller's compute stream, so compute
+// enqueued between rg_comm_allreduce_begin and rg_comm_allreduce_end overlaps it.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "rg_common.h"
+
+namespace rg {
+
+struct Comm {
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    int world = 0, rank = 0;
+};
+
+static int nccl_fail(const char *what, ncclResult_t r) {
+    set_error(std::string(what) + ": " + ncclGetErrorString(r));
+    return RG_E_LAUNCH;
+}
+
+static int hip_fail(const char *what, hipError_t e) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return RG_E_LAUNCH;
+}
+
+int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c || !buf || n < 0) return fail_arg("rg_comm_allreduce_begin: bad argument");
+    hipError_t e = hipEventRecord(c->ev_in, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+    if (e != hipSuccess) return hip_fail("rg_comm_allreduce_begin", e);
+    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) return nccl_fail("ncclAllReduce", r);
+    return RG_OK;
+}
+
+int comm_end(void *h, hipStream_t stream) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c) return fail_arg("rg_comm_allreduce_end: null communicator");
+    hipError_t e = hipEventRecord(c->ev_out, c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, c->ev_out, 0);
+    if (e != hipSuccess) return hip_fail("rg_comm_allreduce_end", e);
+    return RG_OK;
+}
+
+}  // namespace rg
+
+extern "C" int rg_comm_unique_id(uint8_t *out, int64_t len) {
+    if (!out || len < RG_COMM_ID_BYTES) return rg::fail_arg("rg_comm_unique_id: buffer too small");
+    static_assert(sizeof(ncclUniqueId) == RG_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return rg::nccl_fail("ncclGetUniqueId", r);
+    std::memcpy(out, &id, sizeof(id));
+    return RG_OK;
+}
+
+extern "C" void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, int32_t device) {
+    if (!id || world < 1 || rank < 0 || rank >= world) {
+        rg::set_error("rg_comm_create: bad argument");
+        return nullptr;
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { rg::hip_fail("rg_comm_create: hipSetDevice", e); return nullptr; }
+    rg::Comm *c = new (std::nothrow) rg::Comm();
+    if (!c) { rg::set_error("rg_comm_create: out of memory"); return nullptr; }
+    c->world = world;
+    c->rank = rank;
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
+    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;   // same-device ordering only
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, evf);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, evf);
+    if (e != hipSuccess) {
+        rg::hip_fail("rg_comm_create", e);
+        delete c;
+        return nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        rg::nccl_fail("ncclCommInitRank", r);
+        hipStreamDestroy(c->stream);
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+extern "C" int rg_comm_destroy(void *h) {
+    rg::Comm *c = static_cast<rg::Comm *>(h);
+    if (!c) return RG_OK;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->ev_in) hipEventDestroy(c->ev_in);
+    if (c->ev_out) hipEventDestroy(c->ev_out);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return RG_OK;
+}
+
+extern "C" int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf, int64_t n) {
+    int rc = rg::comm_begin(comm, (hipStream_t)stream, buf, n);
+    if (rc) return rc;
+    return rg::comm_end(comm, (hipStream_t)stream);
+}

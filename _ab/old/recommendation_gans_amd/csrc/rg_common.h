@@ -1,0 +1,228 @@
+// Shared device helpers for librg_hip.so (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rg_hip.h"
+
+namespace rg {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string &msg);
+int fail_arg(const std::string &msg);
+int check_launch(const char *what);
+// rg_comm.cpp: all-reduce of buf on the communicator stream, fenced against `stream`
+int comm_begin(void *comm, hipStream_t stream, float *buf, int64_t n);
+int comm_end(void *comm, hipStream_t stream);
+
+// ---------------------------------------------------------------- MT jump-ahead
+// One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,
+// rg_sampler.hip).  Device buffers are owned by the plan.
+constexpr int kMtMaxTail = 8;
+struct MtTailSegs {
+    int64_t start[kMtMaxTail], len[kMtMaxTail];
+    int n;
+};
+struct MtJumpPlan {
+    int64_t words = 0, head = 0;   // words per step, head length
+    MtTailSegs segs{};
+    int chunks = 0;                // blocks per jump in mt_jump_kernel
+    int32_t *terms = nullptr;      // concatenated set bits of t^(D-1) mod chi, per slot
+    int32_t *term_off = nullptr;   // [segs.n + 2]
+    uint32_t *raw = nullptr;       // [(segs.n + 1) * 624] XOR accumulators
+};
+// nullptr if `words` is too short for the jump path (then use rg_mt_generate)
+MtJumpPlan *mt_jump_plan_create(int64_t words);
+void mt_jump_plan_destroy(MtJumpPlan *plan);
+// head -> jump -> tail on `stream`: out[0 .. words) and the next window-form state
+int mt_produce_jump(hipStream_t stream, const MtJumpPlan &plan, uint32_t *state, uint32_t *out,
+                    uint32_t *state_before);
+
+// ---------------------------------------------------------------- DPP
+// Cross-lane moves inside a 16-lane DPP row (no LDS traffic, all lanes valid).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned groups of G lanes (G a power of two <= 64); every lane of the
+// group ends with the bitwise-identical total (each step adds a value and its
+// partner's, which commute exactly).
+template <int G>
+__device__ __forceinline__ float group_sum(float x) {
+    if constexpr (G >= 2) x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x += dpp_mov<0x141>(x);   // row_half_mirror
+    if constexpr (G >= 16) x += dpp_mov<0x140>(x);  // row_mirror
+    if constexpr (G >= 32) x += __shfl_xor(x, 16);
+    if constexpr (G >= 64) x += __shfl_xor(x, 32);
+    return x;
+}
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations
+// (lgkmcnt) but leaves its global stores/atomics in flight.  __syncthreads() on
+// gfx9 also emits s_waitcnt vmcnt(0), draining every outstanding global store
+// before the barrier -- needless when no other thread of the block reads them.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---------------------------------------------------------------- MT19937
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680U;
+    y ^= (y << 15) & 0xefc60000U;
+    y ^= (y >> 18);
+    return y;
+}
+
+// CPython random.choices: pop[floor(random() * float(n))] with
+// random() = ((a>>5)*2^26 + (b>>6)) / 2^53 on two tempered words (pass the
+// raw state words: they are tempered here).  Every
+// operation is exact except the final product, which is a single IEEE
+// round-to-nearest multiply exactly as in CPython; no contraction is possible.
+__device__ __forceinline__ int64_t choice_index(uint32_t w0, uint32_t w1, int64_t n) {
+    w0 = mt_temper(w0);
+    w1 = mt_temper(w1);
+    const double r = ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+    return (int64_t)floor(r * (double)n);
+}
+
+__device__ __forceinline__ float sigmoidf_ref(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+// torch.optim single-tensor update of one element, in the rounding torch's CPU
+// kernels use (checked on the reference's AVX-512 build): add(alpha) and addcmul
+// fuse their final multiply-add (FMA), addcdiv rounds (value * t1) / t2 then adds,
+// lerp(w = 1 - beta1) takes ATen's two-branch form.  g is the data gradient.
+__device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gdata, float &m, float &v) {
+    const float g = fmaf(o.weight_decay, p, gdata);         // grad.add(param, alpha=wd)
+    if (o.kind == RG_OPT_ADAM) {
+        const float w = o.one_minus_beta1;                  // exp_avg.lerp_(grad, 1 - beta1)
+        m = (fabsf(w) < 0.5f) ? fmaf(w, g - m, m) : fmaf(w - 1.0f, g - m, g);
+        v = fmaf(o.one_minus_beta2 * g, g, v * o.beta2);   // mul_(beta2).addcmul_(g, g, 1 - beta2)
+        const float denom = sqrtf(v) / o.bias_correction2_sqrt + o.eps;
+        return p + ((-o.step_size) * m) / denom;           // addcdiv_(m, denom, -step_size)
+    }
+    if (o.kind == RG_OPT_SGD) return fmaf(-o.lr, g, p);     // add_(g, alpha=-lr)
+    v = fmaf(o.one_minus_alpha * g, g, v * o.alpha);        // RMSprop (centered = False)
+    return p + ((-o.lr) * g) / (sqrtf(v) + o.eps);
+}
+
+
+// ---------------------------------------------------------------- row layouts
+// A table row of D floats is spread over LPU lanes.  VEC: D == 4 * LPU and each
+// lane owns one contiguous float4 (rows are 16-B aligned when D % 4 == 0).
+// !VEC: LPU == 64, lane l owns elements l, l + 64, ... (runtime D <= 64 * EPL).
+template <int LPU_, int EPL_, bool VEC_>
+struct RowLayout {
+    static constexpr int LPU = LPU_;
+    static constexpr int EPL = EPL_;
+    static constexpr bool VEC = VEC_;
+    static constexpr int UPW = kWave / LPU;   // rows (units) per wave
+
+    __device__ static __forceinline__ int elem(int sub, int e) { return VEC ? sub * 4 + e : sub + 64 * e; }
+
+    __device__ static __forceinline__ void load(float (&v)[EPL], const float *__restrict__ base,
+                                                int64_t row, int D, int sub) {
+        if constexpr (VEC) {
+            const float4 t = *reinterpret_cast<const float4 *>(base + row * (int64_t)(4 * LPU) + sub * 4);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                v[e] = c < D ? base[row * (int64_t)D + c] : 0.0f;
+            }
+        }
+    }
+
+    // row of an array with an explicit row stride (floats; a multiple of 4 for VEC)
+    __device__ static __forceinline__ void load_strided(float (&v)[EPL], const float *__restrict__ base,
+                                                        int64_t row, int64_t stride, int D, int sub) {
+        if constexpr (VEC) {
+            const float4 t = *reinterpret_cast<const float4 *>(base + row * stride + sub * 4);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                v[e] = c < D ? base[row * stride + c] : 0.0f;
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void store(float *__restrict__ base, int64_t row, int D, int sub,
+                                                 const float (&v)[EPL]) {
+        if constexpr (VEC) {
+            *reinterpret_cast<float4 *>(base + row * (int64_t)(4 * LPU) + sub * 4) =
+                make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                if (c < D) base[row * (int64_t)D + c] = v[e];
+            }
+        }
+    }
+
+    // streaming (non-temporal) store: the line is not kept dirty in L2, so the
+    // end-of-kernel release has less to write back before the next kernel starts
+    __device__ static __forceinline__ void store_nt(float *__restrict__ base, int64_t row, int D, int sub,
+                                                    const float (&v)[EPL]) {
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f t = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(t, reinterpret_cast<v4f *>(base + row * (int64_t)(4 * LPU) + sub * 4));
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                if (c < D) __builtin_nontemporal_store(v[e], base + row * (int64_t)D + c);
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base,
+                                                   int64_t row, int D, int sub) {
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f t = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(base + row * (int64_t)(4 * LPU) + sub * 4));
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + 64 * e;
+                v[e] = c < D ? __builtin_nontemporal_load(base + row * (int64_t)D + c) : 0.0f;
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void zero(float (&v)[EPL]) {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) v[e] = 0.0f;
+    }
+};
+
+// Dispatch on dim: calls f.template operator()<Layout>() for the layout of `dim`.
+template <typename F>
+inline int dispatch_dim(int dim, F &&f) {
+    switch (dim) {
+        case 8: return f.template operator()<RowLayout<2, 4, true>>();
+        case 16: return f.template operator()<RowLayout<4, 4, true>>();
+        case 32: return f.template operator()<RowLayout<8, 4, true>>();
+        case 64: return f.template operator()<RowLayout<16, 4, true>>();
+        case 128: return f.template operator()<RowLayout<32, 4, true>>();
+        case 256: return f.template operator()<RowLayout<64, 4, true>>();
+        default: break;
+    }
+    if (dim >= 1 && dim <= 64) return f.template operator()<RowLayout<64, 1, false>>();
+    if (dim <= 128) return f.template operator()<RowLayout<64, 2, false>>();
+    if (dim <= 192) return f.template operator()<RowLayout<64, 3, false>>();
+    if (dim <= 256) return f.template operator()<RowLayout<64, 4, false>>();
+    return fail_arg("dim must be in [1, 256]");
+}
+
+}  // namespace rg

@@ -59,20 +59,12 @@ struct PairsArgs {
     const int32_t *pos_slot;   // plan: position -> partial slot of its positive's item side
     float *part_row, *part_bias;
     const int2 *pairs;         // prepared (user, item) per pair: [(1 + n) * cols], processing order
-    int32_t *stamp;            // prepare: per-row serial of the last stamping prepare (null: no stamps)
-    int32_t serial;
 };
 
-// Prepared ids carry ownership flags in bit 31 when the prepare pass stamped rows:
-// the first pair (any order) to stamp a row with this step's serial owns it, and
-// the hot-row apply (mf_hot_kernel) updates each touched row through its owner only.
-constexpr int32_t kOwnerBit = (int32_t)0x80000000;
-constexpr int32_t kIdMask = 0x7fffffff;
-
-// rg_mf_prepare: pairs[q * cols + s] for q = 0 (positive) and q = 1 + k (negative k).
-// With stamps, every row a pair touches (valid or not: extra rows are harmless, a
-// missed one would not be) is stamped with the serial, and the first stamper owns it.
-__device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict__ out, int64_t idx) {
+// rg_mf_prepare: pairs[q * cols + s] for q = 0 (positive) and q = 1 + k (negative k)
+__global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out, int prio) {
+    if (prio) __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
+    const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t total = (int64_t)(1 + a.n_neg) * a.cols;
     if (idx >= total) return;
     const int64_t q = idx / a.cols, s = idx - q * a.cols;
@@ -85,18 +77,7 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         const uint2 w = a.words[j];
         r = a.pool[choice_index(w.x, w.y, a.pool_len)];
     }
-    if (a.stamp != nullptr) {
-        const int32_t ou = atomicExch(a.stamp + r.x, a.serial);
-        const int32_t oi = atomicExch(a.stamp + a.num_users + r.y, a.serial);
-        if (ou != a.serial) r.x |= kOwnerBit;
-        if (oi != a.serial) r.y |= kOwnerBit;
-    }
     out[idx] = r;
-}
-
-__global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out, int prio) {
-    if (prio) __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
-    prepare_one(a, out, (int64_t)blockIdx.x * kBlock + threadIdx.x);
 }
 
 // atomically add a row-vector contribution (overflow path, rare)
@@ -134,8 +115,8 @@ constexpr int kLdsFloats = 1280;   // >= units per block * (dim + 1) for every l
 // rows) is instead reduced per block in LDS into one partial row per
 // (item, block): plain stores, no atomics, fixed order.
 template <class L, int PHASE, int NMAX>
-__device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk) {
-    constexpr int LPU = L::LPU, EPL = L::EPL, NP = NMAX + 1;
+__global__ __launch_bounds__(kBlock) void mf_pairs_kernel(PairsArgs a) {
+    constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW, NP = NMAX + 1;
     constexpr int UPB = kBlock / LPU;                  // units per block
     constexpr int TPL = (2 * NP + LPU - 1) / LPU;      // list tasks per lane
     constexpr bool kBackward = (PHASE == kFused) || (PHASE == kAdaptBwd);
@@ -148,7 +129,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     const int sub = lane & (LPU - 1);
     const int ubase = lane & ~(LPU - 1);
     const int ublk = threadIdx.x / LPU;               // unit within the block
-    const int64_t s = blk * UPB + ublk;                 // processing position
+    const int64_t s = (int64_t)blockIdx.x * UPB + ublk; // processing position
     const bool active = s < a.cols;
     const bool plan = a.pos_slot != nullptr;
     const bool has_pos = active && s < a.n_pos;        // a plan puts the positives first
@@ -166,11 +147,9 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const int2 pr = a.pairs[valid[q] || q == 0 ? (int64_t)q * a.cols + (active ? s : 0) : 0];
-        uid[q] = pr.x & kIdMask;     // drop the ownership flags
-        iid[q] = pr.y & kIdMask;
+        uid[q] = pr.x;
+        iid[q] = pr.y;
     }
-    // the positive's plan slot, loaded beside the ids (used after the dot products)
-    const int myslot = (kBackward && plan && has_pos) ? a.pos_slot[s] : -1;
 
     // ---- claim list slots early (their latency hides under the gathers) -------
     int slot[TPL];
@@ -332,6 +311,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         if (plan) {
             // block-level segmented sum of the positives' item-side rows, sorted by item
             const int stride = D + 1;
+            const int myslot = has_pos ? a.pos_slot[s] : -1;
             if (has_pos) {
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
@@ -373,15 +353,10 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
             float sa = 0.0f, sb = 0.0f;
 #pragma unroll
             for (int i = 0; i < kBlock / kWave; ++i) { sa += red[0][i]; sb += red[1][i]; }
-            a.partials[2 * blk] = sa;
-            a.partials[2 * blk + 1] = sb;
+            a.partials[2 * blockIdx.x] = sa;
+            a.partials[2 * blockIdx.x + 1] = sb;
         }
     }
-}
-
-template <class L, int PHASE, int NMAX>
-__global__ __launch_bounds__(kBlock) void mf_pairs_kernel(PairsArgs a) {
-    pairs_body<L, PHASE, NMAX>(a, blockIdx.x);
 }
 
 // adaptive hinge: the global-max negative receives sum_b 1/Bp over active b
@@ -448,31 +423,45 @@ struct ApplyArgs {
 // mf_apply modes: pull the gradient from the lists and update (single GPU);
 // pull into the flat dense gradient (before an all-reduce);
 // update from the (all-reduced) flat gradient.
-enum ApplyMode : int { kApplyPull = 0, kGradOnly = 1, kApplyDense = 2, kApplyCold = 3 /* arg checks only */ };
+enum ApplyMode : int { kApplyPull = 0, kGradOnly = 1, kApplyDense = 2 };
 
-// loss of the step from the pair kernel's per-block partials (one wave, fixed order)
-__device__ __forceinline__ float finalize_loss(const float *__restrict__ partials, int64_t np_, double inv_a,
-                                               double inv_b, int lane) {
-    double sa = 0.0, sb = 0.0;
-    for (int64_t i = lane; i < np_; i += kWave) {
-        sa += (double)partials[2 * i];
-        sb += (double)partials[2 * i + 1];
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        sa += __shfl_xor(sa, off);
-        sb += __shfl_xor(sb, off);
-    }
-    return (float)(sa * inv_a + sb * inv_b);
-}
-
-// Gradient + optimizer update of unified row r (users [0, U), items [U, U + I)).
-// COLD: a row no pair of the step touches -- its data gradient is exactly zero
-// (only the coupled weight decay acts), so nothing of the step's scratch is read.
-template <class L, int MODE, int NT, bool COLD, bool SPEC = false>
-__device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub) {
-    constexpr int EPL = L::EPL;
-    const int64_t rb = a.row_begin, nr = a.row_end - rb;
+// Streams every row of [row_begin, row_end) once (item rows first, so the few
+// long Zipf-hot item rows start early instead of trailing the grid).
+// NT: 1 = streaming stores of the updated p, m, v; 2 = also streaming loads of the
+// pre-step p, m, v (each touched once per step)
+template <class L, int MODE, int NT = 0>
+__global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
+    constexpr int LPU = L::LPU, EPL = L::EPL, UPW = L::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t k = wave * UPW + (lane / LPU);
+    const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
     const int D = a.dim;
+
+    if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
+        double sa = 0.0, sb = 0.0;
+        for (int64_t i = lane; i < a.n_partials; i += kWave) {
+            sa += (double)a.partials[2 * i];
+            sb += (double)a.partials[2 * i + 1];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            sa += __shfl_xor(sa, off);
+            sb += __shfl_xor(sb, off);
+        }
+        if (lane == 0) {
+            const float lv = (float)(sa * a.inv_a + sb * a.inv_b);
+            *a.loss_out = lv;
+            if (MODE == kGradOnly) a.grad[nr * (int64_t)(D + 1)] = lv;
+        }
+    }
+    if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+        *a.loss_out = a.grad[nr * (int64_t)(D + 1)];
+
+    if (k >= nr) return;
+    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item part [ia0, re)
+    const int64_t ni = re > ia0 ? re - ia0 : 0;
+    const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
     const int t = r < a.num_users ? 0 : 1;          // 0: user table, 1: item table
     const int64_t lr_ = t ? r - a.num_users : r;
     const int64_t gk = r - rb;                      // index in the flat gradient
@@ -503,29 +492,13 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     if (MODE == kApplyDense) {
         L::load(g, a.grad, gk, D, sub);
         if (sub == 0) gb = a.grad[nr * (int64_t)D + gk];
-    } else if (!COLD) {
+    } else {
         const int c = a.row_count[r];
-        // SPEC: the list and the item's partial-slot range are loaded beside the count
-        // (entries past the count are stale and never used), so a touched row's partner
-        // rows are its only dependent round trip
-        int2 spec[SPEC ? kCap : 1];
-        int s0 = 0, s1 = 0;
-        if (SPEC) {
-            const int4 *lst = reinterpret_cast<const int4 *>(a.row_list + r * kCap);
-#pragma unroll
-            for (int e = 0; e < kCap / 2; ++e) {
-                const int4 v = lst[e];
-                spec[2 * e] = make_int2(v.x, v.y);
-                spec[2 * e + 1] = make_int2(v.z, v.w);
-            }
-            if (t == 1 && a.item_slot_off != nullptr) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
-        }
         if (c > 0) {
             const int ne = c < kCap ? c : kCap;
             int2 ent[kCap];
 #pragma unroll
-            for (int e = 0; e < kCap; ++e)
-                ent[e] = e < ne ? (SPEC ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
+            for (int e = 0; e < kCap; ++e) ent[e] = e < ne ? a.row_list[r * kCap + e] : make_int2(0, 0);
             // MF: the partner row of the other table; NCF: the stored gradient half
             const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
             const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
@@ -558,7 +531,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             if (sub == 0) a.row_count[r] = 0;
         }
         if (t == 1 && a.item_slot_off != nullptr) {   // planned positive partials of this item
-            if (!SPEC) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
+            const int s0 = a.item_slot_off[lr_], s1 = a.item_slot_off[lr_ + 1];
             for (int sl = s0; sl < s1; sl += 4) {
                 float h[4][EPL];
                 float hb[4];
@@ -604,164 +577,6 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     }
 }
 
-// Streams every row of [row_begin, row_end) once (item rows first, so the few
-// long Zipf-hot item rows start early instead of trailing the grid).
-// NT: 1 = streaming stores of the updated p, m, v; 2 = also streaming loads of the
-// pre-step p, m, v (each touched once per step)
-template <class L, int MODE, int NT = 0, bool SPEC = false>
-__global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t k = wave * UPW + (lane / LPU);
-    const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
-    const int D = a.dim;
-
-    if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
-        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) {
-            *a.loss_out = lv;
-            if (MODE == kGradOnly) a.grad[nr * (int64_t)(D + 1)] = lv;
-        }
-    }
-    if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-        *a.loss_out = a.grad[nr * (int64_t)(D + 1)];
-
-    if (k >= nr) return;
-    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item part [ia0, re)
-    const int64_t ni = re > ia0 ? re - ia0 : 0;
-    const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
-    apply_row<L, MODE, NT, false, SPEC>(a, r, sub);
-}
-
-// the dense update of rows [row_begin, row_end) (blocks [0, apply_blocks), as
-// mf_apply_kernel) and the prepare pass of the NEXT step (the remaining blocks) in one
-// launch: the split step then needs no side stream and no per-step cross-stream event
-template <class L, int NT>
-__global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
-                                                        int64_t apply_blocks) {
-    const int64_t blk = blockIdx.x;
-    if (blk >= apply_blocks) {
-        prepare_one(prep, prep_out, (blk - apply_blocks) * kBlock + threadIdx.x);
-        return;
-    }
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    const int64_t wave = (blk * kBlock + threadIdx.x) >> 6;
-    const int64_t k = wave * UPW + (lane / LPU);
-    const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
-    if (a.loss_out != nullptr && blk == 0 && threadIdx.x < kWave) {
-        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) *a.loss_out = lv;
-    }
-    if (k >= nr) return;
-    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item rows first, as mf_apply_kernel
-    const int64_t ni = re > ia0 ? re - ia0 : 0;
-    const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
-    apply_row<L, kApplyPull, NT, false>(a, r, sub);
-}
-
-// ---------------------------------------------------------------------------- overlapped step
-// One training step as two launches instead of prepare / pairs / apply:
-//
-//   mf_front_kernel  blocks [0, P)        the pair pass of this step (pairs_body)
-//                    blocks [P, P + Q)    the prepare pass of the NEXT step (stamps
-//                                         the rows it will touch with its serial)
-//                    blocks [P + Q, ...)  the optimizer update of every COLD row of
-//                                         this step (stamp != this step's serial):
-//                                         zero data gradient, so it needs nothing
-//                                         from the pair pass and streams beside it
-//   mf_hot_kernel    the update of the touched rows, one per owner flag of the
-//                    prepared pairs, pulling the pair pass's lists / partials
-//
-// The latency-bound pair pass (gathers, atomics, LDS) thus hides under two thirds
-// of the HBM-bound dense optimizer pass instead of preceding all of it.
-struct FrontArgs {
-    int64_t pair_blocks, prep_blocks;
-    int2 *prep_out;                 // next step's pairs buffer (prep_blocks > 0)
-    const int32_t *cold_stamp;      // this step's stamps
-    int32_t cold_serial;
-};
-
-template <class L, int NMAX>
-__global__ __launch_bounds__(kBlock) void mf_front_kernel(PairsArgs pa, PairsArgs prep, ApplyArgs aa, FrontArgs f) {
-    const int64_t blk = blockIdx.x;
-    if (blk < f.pair_blocks) {
-        pairs_body<L, kFused, NMAX>(pa, blk);
-        return;
-    }
-    if (blk < f.pair_blocks + f.prep_blocks) {
-        prepare_one(prep, f.prep_out, (blk - f.pair_blocks) * kBlock + threadIdx.x);
-        return;
-    }
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    const int64_t wave = ((blk - f.pair_blocks - f.prep_blocks) * kBlock + threadIdx.x) >> 6;
-    const int64_t r = aa.row_begin + wave * UPW + (lane / LPU);
-    if (r >= aa.row_end) return;
-    if (f.cold_stamp[r] == f.cold_serial) return;           // touched: mf_hot_kernel
-    apply_row<L, kApplyPull, 0, true>(aa, r, sub);
-}
-
-// the cold-row update of the front grid as a launch of its own (two-stream schedule:
-// beside rg_mf_pairs on another stream, at its own register budget)
-template <class L>
-__global__ __launch_bounds__(kBlock) void mf_cold_kernel(ApplyArgs a, const int32_t *__restrict__ stamp,
-                                                        int32_t serial) {
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t r = a.row_begin + wave * UPW + (lane / LPU);
-    if (r >= a.row_end) return;
-    if (stamp[r] == serial) return;
-    apply_row<L, kApplyPull, 0, true>(a, r, sub);
-}
-
-// row-ordered variant: scan the rows, update those stamped with this step's serial
-// (sequential addresses with holes instead of the pairs' random order)
-template <class L>
-__global__ __launch_bounds__(kBlock) void mf_hot_scan_kernel(ApplyArgs a, const int32_t *__restrict__ stamp,
-                                                            int32_t serial) {
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    if (a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
-        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) *a.loss_out = lv;
-    }
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t r = a.row_begin + wave * UPW + (lane / LPU);
-    if (r >= a.row_end) return;
-    if (stamp[r] != serial) return;
-    apply_row<L, kApplyPull, 0, false>(a, r, sub);
-}
-
-// slot k = (pair k >> 1, side k & 1): the row the slot's pair touches on that side,
-// updated here iff the slot owns it (exactly one owner per touched row)
-template <class L>
-__global__ __launch_bounds__(kBlock) void mf_hot_kernel(ApplyArgs a, const int2 *__restrict__ pairs, int64_t n_slots) {
-    constexpr int LPU = L::LPU, UPW = L::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    if (a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
-        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) *a.loss_out = lv;
-    }
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t k = wave * UPW + (lane / LPU);
-    if (k >= n_slots) return;
-    const int2 pr = pairs[k >> 1];
-    const int32_t x = (k & 1) ? pr.y : pr.x;
-    if (x >= 0) return;                                     // owner flag (bit 31) not set
-    const int64_t r = (k & 1) ? a.num_users + (x & kIdMask) : (int64_t)(x & kIdMask);
-    if (r < a.row_begin || r >= a.row_end) return;
-    apply_row<L, kApplyPull, 0, false>(a, r, sub);
-}
-
 // ---------------------------------------------------------------------------- scores / loss
 template <class L>
 __global__ __launch_bounds__(kBlock) void mf_scores_kernel(const float *__restrict__ uw, const float *__restrict__ iw,
@@ -793,8 +608,16 @@ __global__ __launch_bounds__(kBlock) void mf_scores_kernel(const float *__restri
 
 __global__ __launch_bounds__(kWave) void loss_finalize_kernel(const float *__restrict__ partials, int64_t np_,
                                                               double inv_a, double inv_b, float *out) {
-    const float lv = finalize_loss(partials, np_, inv_a, inv_b, threadIdx.x);
-    if (threadIdx.x == 0) *out = lv;
+    double sa = 0.0, sb = 0.0;
+    for (int64_t i = threadIdx.x; i < np_; i += kWave) {
+        sa += (double)partials[2 * i];
+        sb += (double)partials[2 * i + 1];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sa += __shfl_xor(sa, off);
+        sb += __shfl_xor(sb, off);
+    }
+    if (threadIdx.x == 0) *out = (float)(sa * inv_a + sb * inv_b);
 }
 
 template <class L>
@@ -866,12 +689,7 @@ struct ApplyLaunchF {
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
-        static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 0; }();
-        if (mode == kApplyPull && spec && nt == 1)
-            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1, true>), dim3(nb), dim3(kBlock), 0, s, *a);
-        else if (mode == kApplyPull && spec)
-            hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 0, true>), dim3(nb), dim3(kBlock), 0, s, *a);
-        else if (mode == kApplyPull && nt == 1)
+        if (mode == kApplyPull && nt == 1)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kApplyPull && nt >= 2)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 2>), dim3(nb), dim3(kBlock), 0, s, *a);
@@ -926,8 +744,8 @@ static int check_tables(const rg_mf_tables_t *t) {
     return RG_OK;
 }
 
-static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_mf_work_t *w, int32_t backward,
-                      PairsArgs &a) {
+extern "C" int rg_mf_pairs(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *b, rg_mf_work_t *w,
+                           int32_t backward) {
     int rc = check_tables(t);
     if (rc) return rc;
     if (b == nullptr || w == nullptr) return fail_arg("rg_mf_pairs: null batch/work");
@@ -947,7 +765,7 @@ static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_
     if (w->plan_perm && (!w->plan_pos_slot || !w->part_row || !w->part_bias || !w->plan_item_slot_off))
         return fail_arg("rg_mf_pairs: incomplete plan");
 
-    a = PairsArgs{};
+    PairsArgs a{};
     a.user_w = t->user_w; a.item_w = t->item_w; a.user_b = t->user_b; a.item_b = t->item_b;
     a.num_users = t->num_users; a.dim = t->dim;
     a.pos_user = b->pos_user; a.pos_item = b->pos_item;
@@ -980,47 +798,24 @@ static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_
     a.perm = w->plan_perm;
     a.pos_slot = backward ? w->plan_pos_slot : nullptr;   // partials only in the backward pass
     a.part_row = w->part_row; a.part_bias = w->part_bias;
-    return RG_OK;
-}
-
-extern "C" int rg_mf_pairs(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *b, rg_mf_work_t *w,
-                           int32_t backward) {
-    PairsArgs a;
-    int rc = pairs_args(t, b, w, backward, a);
-    if (rc) return rc;
-    PairsLaunchF f{&a, (hipStream_t)stream, b->loss == RG_LOSS_ADAPTIVE_HINGE, backward != 0};
+    PairsLaunchF f{&a, (hipStream_t)stream, adaptive, backward != 0};
     return dispatch_dim(t->dim, f);
 }
 
-static int prepare_args(const rg_mf_batch_t *b, const rg_mf_work_t *w, const rg_mf_mark_t *mark, PairsArgs &a) {
+extern "C" int rg_mf_prepare(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w) {
     if (!b || !b->pairs) return fail_arg("rg_mf_prepare: null batch/pairs");
     if (b->n_neg < 1 || b->n_neg > kNMax) return fail_arg("rg_mf_prepare: n_neg must be in [1, 8]");
     if (b->cols <= 0 || b->n_pos < 0 || b->n_pos > b->cols) return fail_arg("rg_mf_prepare: bad n_pos/cols");
     if (b->col_offset < 0 || b->col_offset + b->cols > b->global_cols) return fail_arg("rg_mf_prepare: bad slice");
     if (b->pool_len <= 0 || !b->pool || !b->words) return fail_arg("rg_mf_prepare: empty pool / no words");
     if (b->n_pos > 0 && (!b->pos_user || !b->pos_item)) return fail_arg("rg_mf_prepare: null positives");
-    if (mark && (!mark->stamp || mark->serial == 0 || mark->num_users <= 0))
-        return fail_arg("rg_mf_prepare: bad row marks (stamp, serial != 0, num_users)");
-    a = PairsArgs{};
+    PairsArgs a{};
     a.pos_user = b->pos_user; a.pos_item = b->pos_item;
     a.n_pos = b->n_pos; a.cols = b->cols; a.col_offset = b->col_offset; a.global_cols = b->global_cols;
     a.words = reinterpret_cast<const uint2 *>(b->words);
     a.pool = reinterpret_cast<const int2 *>(b->pool);
     a.pool_len = b->pool_len; a.n_neg = b->n_neg;
     a.perm = w ? w->plan_perm : nullptr;
-    if (mark) {
-        a.stamp = mark->stamp;
-        a.serial = mark->serial;
-        a.num_users = mark->num_users;
-    }
-    return RG_OK;
-}
-
-extern "C" int rg_mf_prepare_marked(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w,
-                                    const rg_mf_mark_t *mark) {
-    PairsArgs a;
-    int rc = prepare_args(b, w, mark, a);
-    if (rc) return rc;
     const int64_t total = (int64_t)(1 + b->n_neg) * b->cols;
     static const int prio = [] { const char *e = getenv("RG_PREP_PRIO"); return e ? atoi(e) : 1; }();
     hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
@@ -1028,13 +823,9 @@ extern "C" int rg_mf_prepare_marked(void *stream, const rg_mf_batch_t *b, const 
     return check_launch("rg_mf_prepare");
 }
 
-extern "C" int rg_mf_prepare(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w) {
-    return rg_mf_prepare_marked(stream, b, w, nullptr);
-}
-
-static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const float *grad_in, float *grad_out,
-                      const rg_opt_t *opt, int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
-                      float *dense_loss_out, int mode, ApplyArgs &a) {
+static int apply_common(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const float *grad_in,
+                        float *grad_out, const rg_opt_t *opt, int64_t row_begin, int64_t row_end,
+                        const rg_mf_loss_t *loss, float *dense_loss_out, int mode) {
     int rc = check_tables(t);
     if (rc) return rc;
     const int64_t nrows = t->num_users + t->num_items;
@@ -1045,7 +836,7 @@ static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const floa
         if (!opt) return fail_arg("rg_mf_apply: null opt");
         if (!t->user_w_out || !t->item_w_out || !t->user_b_out || !t->item_b_out)
             return fail_arg("rg_mf_apply: null output tables");
-        if ((mode == kApplyPull || mode == kApplyCold) && (t->user_w_out == t->user_w || t->item_w_out == t->item_w ||
+        if (mode == kApplyPull && (t->user_w_out == t->user_w || t->item_w_out == t->item_w ||
                                    t->user_b_out == t->user_b || t->item_b_out == t->item_b))
             return fail_arg("rg_mf_apply: output tables must not alias the inputs (ping-pong)");
         if (opt->kind < RG_OPT_ADAM || opt->kind > RG_OPT_RMSPROP) return fail_arg("rg_mf_apply: bad optimizer");
@@ -1054,14 +845,13 @@ static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const floa
         if (opt->kind != RG_OPT_SGD && (!t->user_w_v || !t->item_w_v || !t->user_b_v || !t->item_b_v))
             return fail_arg("rg_mf_apply: optimizer needs v state");
     }
-    if (mode != kApplyDense && mode != kApplyCold) {
+    if (mode != kApplyDense) {
         if (!w || !w->row_count || !w->row_list || !w->hot_grad || !w->hot_bias_grad)
             return fail_arg("rg_mf_apply: null scratch");
         if (loss && loss->out && !w->loss_partials) return fail_arg("rg_mf_apply: loss needs partials");
     }
-    if (mode != kApplyPull && mode != kApplyCold && !(grad_in || grad_out))
-        return fail_arg("rg_mf_apply: null gradient buffer");
-    a = ApplyArgs{};
+    if (mode != kApplyPull && !(grad_in || grad_out)) return fail_arg("rg_mf_apply: null gradient buffer");
+    ApplyArgs a{};
     a.w_in[0] = t->user_w; a.w_in[1] = t->item_w; a.b_in[0] = t->user_b; a.b_in[1] = t->item_b;
     a.w_out[0] = t->user_w_out; a.w_out[1] = t->item_w_out; a.b_out[0] = t->user_b_out; a.b_out[1] = t->item_b_out;
     a.w_m[0] = t->user_w_m; a.w_m[1] = t->item_w_m; a.w_v[0] = t->user_w_v; a.w_v[1] = t->item_w_v;
@@ -1086,168 +876,7 @@ static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const floa
     }
     a.grad = grad_out ? grad_out : const_cast<float *>(grad_in);
     a.has_bias = true;
-    return RG_OK;
-}
-
-static int apply_common(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const float *grad_in,
-                        float *grad_out, const rg_opt_t *opt, int64_t row_begin, int64_t row_end,
-                        const rg_mf_loss_t *loss, float *dense_loss_out, int mode) {
-    ApplyArgs a;
-    int rc = apply_args(t, w, grad_in, grad_out, opt, row_begin, row_end, loss, dense_loss_out, mode, a);
-    if (rc) return rc;
     ApplyLaunchF f{&a, (hipStream_t)stream, mode};
-    return dispatch_dim(t->dim, f);
-}
-
-namespace {
-struct FrontLaunchF {
-    PairsArgs *pa, *prep;
-    ApplyArgs *aa;
-    FrontArgs f;
-    hipStream_t s;
-    template <class L>
-    int operator()() {
-        f.pair_blocks = pairs_blocks<L>(pa->cols);
-        const int64_t cold_rows = aa->row_end - aa->row_begin;
-        const int64_t cold_waves = (cold_rows + L::UPW - 1) / L::UPW;
-        const int64_t cold_blocks = (cold_waves + kBlock / kWave - 1) / (kBlock / kWave);
-        const dim3 grid((unsigned)(f.pair_blocks + f.prep_blocks + cold_blocks));
-        if (pa->n_neg <= 5)
-            hipLaunchKernelGGL((mf_front_kernel<L, 5>), grid, dim3(kBlock), 0, s, *pa, *prep, *aa, f);
-        else
-            hipLaunchKernelGGL((mf_front_kernel<L, kNMax>), grid, dim3(kBlock), 0, s, *pa, *prep, *aa, f);
-        return check_launch("rg_mf_step_front");
-    }
-};
-
-struct HotLaunchF {
-    ApplyArgs *a;
-    const int2 *pairs;
-    int64_t n_slots;
-    const rg_mf_mark_t *mark;
-    hipStream_t s;
-    template <class L>
-    int operator()() {
-        if (mark) {
-            const int64_t rows = a->row_end - a->row_begin;
-            const int64_t waves = (rows + L::UPW - 1) / L::UPW;
-            const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-            hipLaunchKernelGGL((mf_hot_scan_kernel<L>), dim3(nb < 1 ? 1 : nb), dim3(kBlock), 0, s, *a, mark->stamp,
-                               mark->serial);
-            return check_launch("rg_mf_step_hot");
-        }
-        const int64_t waves = (n_slots + L::UPW - 1) / L::UPW;
-        const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-        hipLaunchKernelGGL((mf_hot_kernel<L>), dim3(nb < 1 ? 1 : nb), dim3(kBlock), 0, s, *a, pairs, n_slots);
-        return check_launch("rg_mf_step_hot");
-    }
-};
-}  // namespace
-
-namespace {
-struct BackLaunchF {
-    ApplyArgs *a;
-    PairsArgs *prep;
-    int2 *prep_out;
-    int64_t prep_blocks;
-    hipStream_t s;
-    template <class L>
-    int operator()() {
-        const int64_t rows = a->row_end - a->row_begin;
-        const int64_t waves = (rows + L::UPW - 1) / L::UPW;
-        int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-        if (nb < 1) nb = 1;
-        const dim3 grid((unsigned)(nb + prep_blocks));
-        hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
-        return check_launch("rg_mf_apply_prepare");
-    }
-};
-}  // namespace
-
-extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
-                                   int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
-                                   const rg_mf_batch_t *next, const rg_mf_work_t *next_w) {
-    ApplyArgs a;
-    int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull, a);
-    if (rc) return rc;
-    PairsArgs prep{};
-    int64_t prep_blocks = 0;
-    int2 *prep_out = nullptr;
-    if (next) {
-        if ((rc = prepare_args(next, next_w, nullptr, prep))) return rc;
-        prep_out = reinterpret_cast<int2 *>(next->pairs);
-        prep_blocks = ((int64_t)(1 + next->n_neg) * next->cols + kBlock - 1) / kBlock;
-    }
-    BackLaunchF f{&a, &prep, prep_out, prep_blocks, (hipStream_t)stream};
-    return dispatch_dim(t->dim, f);
-}
-
-extern "C" int rg_mf_step_front(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *cur, rg_mf_work_t *w,
-                                const rg_mf_mark_t *cur_mark, const rg_opt_t *opt, int64_t cold_begin,
-                                int64_t cold_end, const rg_mf_batch_t *next, const rg_mf_work_t *next_w,
-                                const rg_mf_mark_t *next_mark) {
-    if (!cur_mark || !cur_mark->stamp || cur_mark->serial == 0)
-        return fail_arg("rg_mf_step_front: the current step's pairs must be prepared with row marks");
-    if (cur && cur->loss == RG_LOSS_ADAPTIVE_HINGE)
-        return fail_arg("rg_mf_step_front: adaptive hinge needs the global max first (use rg_mf_pairs)");
-    PairsArgs pa, prep{};
-    int rc = pairs_args(t, cur, w, 1, pa);
-    if (rc) return rc;
-    ApplyArgs aa;
-    if ((rc = apply_args(t, w, nullptr, nullptr, opt, cold_begin, cold_end, nullptr, nullptr, kApplyPull, aa)))
-        return rc;
-    FrontArgs f{};
-    f.cold_stamp = cur_mark->stamp;
-    f.cold_serial = cur_mark->serial;
-    if (next) {
-        if (!next_mark || next_mark->stamp == cur_mark->stamp || next_mark->serial == cur_mark->serial)
-            return fail_arg("rg_mf_step_front: the next step needs its own stamp array and serial");
-        if ((rc = prepare_args(next, next_w, next_mark, prep))) return rc;
-        if (next->pairs == cur->pairs) return fail_arg("rg_mf_step_front: next pairs buffer aliases the current");
-        f.prep_out = reinterpret_cast<int2 *>(next->pairs);
-        f.prep_blocks = ((int64_t)(1 + next->n_neg) * next->cols + kBlock - 1) / kBlock;
-    }
-    FrontLaunchF fl{&pa, &prep, &aa, f, (hipStream_t)stream};
-    return dispatch_dim(t->dim, fl);
-}
-
-namespace {
-struct ColdLaunchF {
-    ApplyArgs *a;
-    const rg_mf_mark_t *mark;
-    hipStream_t s;
-    template <class L>
-    int operator()() {
-        const int64_t rows = a->row_end - a->row_begin;
-        if (rows <= 0) return RG_OK;
-        const int64_t waves = (rows + L::UPW - 1) / L::UPW;
-        const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-        hipLaunchKernelGGL((mf_cold_kernel<L>), dim3(nb), dim3(kBlock), 0, s, *a, mark->stamp, mark->serial);
-        return check_launch("rg_mf_step_cold");
-    }
-};
-}  // namespace
-
-extern "C" int rg_mf_step_cold(void *stream, const rg_mf_tables_t *t, const rg_mf_mark_t *mark, const rg_opt_t *opt,
-                               int64_t row_begin, int64_t row_end) {
-    if (!mark || !mark->stamp || mark->serial == 0) return fail_arg("rg_mf_step_cold: bad mark");
-    ApplyArgs a;
-    int rc = apply_args(t, nullptr, nullptr, nullptr, opt, row_begin, row_end, nullptr, nullptr, kApplyCold, a);
-    if (rc) return rc;
-    ColdLaunchF f{&a, mark, (hipStream_t)stream};
-    return dispatch_dim(t->dim, f);
-}
-
-extern "C" int rg_mf_step_hot(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *cur, rg_mf_work_t *w,
-                              const rg_mf_mark_t *mark, const rg_opt_t *opt, int64_t row_begin, int64_t row_end,
-                              const rg_mf_loss_t *loss) {
-    if (!cur || !cur->pairs) return fail_arg("rg_mf_step_hot: null batch/pairs");
-    if (mark && (!mark->stamp || mark->serial == 0)) return fail_arg("rg_mf_step_hot: bad mark");
-    ApplyArgs a;
-    int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull, a);
-    if (rc) return rc;
-    HotLaunchF f{&a, reinterpret_cast<const int2 *>(cur->pairs), 2 * (int64_t)(1 + cur->n_neg) * cur->cols, mark,
-                 (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
 

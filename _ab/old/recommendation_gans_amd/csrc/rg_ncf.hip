@@ -1,0 +1,654 @@
+// NCF MLP training step on gfx950 (spotlight/dnn_models/mlp.py:5-46 trained by
+// implicit.py:347-364; layers [2E, E, ..., 8] -> 1 as ncf_spotlight.py:53-56).
+//
+// One workgroup (4 waves) walks tiles of kRows = 32 examples; a tile holds whole
+// columns (a positive and its n negatives, pairs prepared by rg_mf_prepare), so
+// pairwise losses are resolved inside the tile.  Everything of a tile lives in
+// LDS: the MLP parameters (loaded once per workgroup), the activations of every
+// layer, the per-unit backward multipliers and the workgroup's running weight
+// gradient.  Each layer's three products run on the fp32 MFMA (16x16x4):
+//     Z_k = A_k W_k^T,   dW_k += delta_k^T A_k,   dA_k = delta_k W_k.
+// LeakyReLU(0.1) then Dropout(0.5) fold into one exact multiplier per unit,
+// m in {0, 2, 0.2} (training) or {1, 0.1} (eval): A_{k+1} = Z_k * m and
+// delta = dA * m reproduce torch's rounding (power-of-two scalings commute).
+// Outputs: per-example input gradients dX (rows of 2E) for the embedding update
+// (rg_ncf_apply pulls them through the per-row lists), planned per-tile partial
+// rows for the positives' items, the workgroup's weight-gradient partial and
+// deterministic loss partials.
+#include <cstdlib>
+
+#include "rg_common.h"
+
+namespace rg {
+
+constexpr int kRows = 32;              // examples per tile (two 16-row MFMA tiles)
+constexpr int kNcfThreads = 256;
+constexpr int kNcfCap = RG_MF_LIST_CAP;
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// layer sizes H_k = 2E >> k, k = 0..NH (H_NH = 8); NH hidden Linear layers + output 8 -> 1
+template <int E>
+struct NcfShape {
+    static constexpr int NH = E == 8 ? 1 : E == 16 ? 2 : E == 32 ? 3 : 4;
+    static constexpr int H(int k) { return (2 * E) >> k; }
+    static constexpr int w_off(int k) {       // flat parameter offset of layer k (W then b)
+        int o = 0;
+        for (int j = 0; j < k; ++j) o += H(j + 1) * H(j) + H(j + 1);
+        return o;
+    }
+    static constexpr int P = w_off(NH) + 8 + 1;                  // + output W (1x8), b (1)
+    // LDS float offsets: padded weights, activations, multipliers, dW, misc
+    static constexpr int sw_off(int k) {
+        int o = 0;
+        for (int j = 0; j < k; ++j) o += H(j + 1) * (H(j) + 1) + H(j + 1);
+        return o;
+    }
+    static constexpr int SW = sw_off(NH) + 9;
+    static constexpr int sa_off(int k) {
+        int o = 0;
+        for (int j = 0; j < k; ++j) o += kRows * (H(j) + 1);
+        return o;
+    }
+    static constexpr int SA = sa_off(NH + 1);
+    static constexpr int mask_units() {
+        int u = 0;
+        for (int k = 1; k <= NH; ++k) u += H(k);
+        return u;
+    }
+    static constexpr int LDS = SW + SA + SA + P + 11 * kRows + 8;   // W, A, M(=A layout), dW, misc
+};
+
+struct NcfArgs {
+    const float *user_w, *item_w;
+    const float *mlp;                 // flat parameters (named_parameters order)
+    int64_t num_users, num_items;
+    const int2 *pairs;                // prepared, [q * cols + s]
+    int64_t n_pos, cols, global_cols, col_offset;
+    int n_neg, loss, tc;              // tc: columns per tile
+    int64_t tiles;
+    float n_a, n_b;                   // loss denominators (as rg_mf_pairs)
+    const int32_t *perm, *pos_slot;   // plan (optional)
+    int32_t *row_count;
+    int2 *row_list;
+    float *hot_grad;
+    float *part_row;
+    float *loss_partials;             // [tiles * 2]
+    float *contrib;                   // [tiles * kRows * 2E]
+    float *wpart;                     // [gridDim.x * P]
+    float *scores;                    // [tiles * kRows] (forward-only phase)
+    const float *dp_in;               // [tiles * kRows] (given-dp phase)
+    const uint8_t *mask_pos, *mask_neg;
+    uint64_t seed;
+    int training;
+};
+
+enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2, kNcfLossOnly = 3 };
+
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// murmur3 fmix32: the per-unit dropout bit from the row's key
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bU;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35U;
+    h ^= h >> 16;
+    return h;
+}
+
+// C tile (16x16 at i0, j0) of A.B on LDS operands, K a multiple of 4.
+// A(i, k) = A[i * ai + k * ak], B(k, j) = B[k * bk + j * bj]; rows >= imax / cols >= jmax read 0.
+__device__ __forceinline__ v4f mma16(const float *A, int ai, int ak, const float *B, int bk, int bj, int i0, int j0,
+                                     int K, int imax, int jmax, int lane) {
+    // called with compile-time shapes (the layer loops are unrolled): the k loop
+    // unrolls, LDS reads get immediate offsets and issue ahead of the MFMAs, and
+    // two accumulators alternate so the 40-cycle dependency does not serialise them
+    v4f acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int li = lane & 15, lk = lane >> 4;
+    const bool iv = i0 + li < imax, jv = j0 + li < jmax;
+    const float *pa = A + (iv ? (i0 + li) : 0) * ai + lk * ak;
+    const float *pb = B + lk * bk + (jv ? (j0 + li) : 0) * bj;
+#pragma unroll
+    for (int k = 0; k < K; k += 8) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[k * ak] : 0.0f, jv ? pb[k * bk] : 0.0f, acc0, 0, 0, 0);
+        if (k + 4 < K)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[(k + 4) * ak] : 0.0f, jv ? pb[(k + 4) * bk] : 0.0f,
+                                                        acc1, 0, 0, 0);
+    }
+    return acc0 + acc1;
+}
+
+template <int E, int PHASE>
+__global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
+    using S = NcfShape<E>;
+    constexpr int NH = S::NH, P = S::P, IN0 = 2 * E;
+    extern __shared__ float lds[];
+    float *sW = lds;                      // padded weights
+    float *sA = sW + S::SW;               // activations A_0 .. A_NH, [kRows][H_k + 1]
+    float *sM = sA + S::SA;               // multipliers / deltas, same layout as sA (k >= 1)
+    float *sG = sM + S::SA;               // weight-gradient accumulator (flat, P)
+    float *sP = sG + P;                   // p per row
+    float *sDz = sP + kRows;              // dL/dlogit per row
+    int *sU = reinterpret_cast<int *>(sDz + kRows);
+    int *sI = sU + kRows;
+    int *sR = sI + kRows;                 // per row: reference row of its mask (pos: column, neg: draw j)
+    uint32_t *sK = reinterpret_cast<uint32_t *>(sR + kRows);   // per row: dropout hash key
+    float *sLa = reinterpret_cast<float *>(sK + kRows);        // per column loss terms
+    float *sLb = sLa + kRows;
+    int *sLu = reinterpret_cast<int *>(sLb + kRows);          // per row: user list slot (-1: none)
+    int *sLi = sLu + kRows;                                   // per row: item list slot (-1: none / planned)
+    int *sPs = sLi + kRows;                                   // per row: plan slot of a positive (-1: none)
+    float *sX = sM + S::sa_off(0);                            // dX rows [kRows][IN0 + 1] (M_0 is unused)
+    constexpr int cl_base = 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
+    const int n = a.n_neg, NP = n + 1, tc = a.tc;
+
+    // ---- parameters into LDS (row stride H_k + 1), gradient accumulator zeroed ----
+    for (int k = 0; k < NH; ++k) {
+        const int in = S::H(k), out = S::H(k + 1);
+        const float *W = a.mlp + S::w_off(k);
+        float *dst = sW + S::sw_off(k);
+        for (int e = tid; e < out * in; e += kNcfThreads) dst[(e / in) * (in + 1) + e % in] = W[e];
+        for (int e = tid; e < out; e += kNcfThreads) dst[out * (in + 1) + e] = W[out * in + e];
+    }
+    for (int e = tid; e < 9; e += kNcfThreads) sW[S::sw_off(NH) + e] = a.mlp[S::w_off(NH) + e];
+    for (int e = tid; e < P; e += kNcfThreads) sG[e] = 0.0f;
+    __syncthreads();
+
+    for (int64_t tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
+        const int64_t c0 = tile * tc;
+        // ---- row ids: row r = q * tc + cl ----------------------------------------------
+        if (tid < kRows) {
+            const int r = tid, q = r / tc, cl = r % tc;
+            const int64_t s = c0 + cl;
+            const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
+            bool valid = q < NP && s < a.cols;
+            if (valid && q == 0) valid = s < a.n_pos;
+            if (valid && q > 0 && pairwise) valid = s < a.n_pos;
+            int u = -1, i = -1;
+            if (valid) {
+                const int2 pr = a.pairs[(int64_t)q * a.cols + s];
+                u = pr.x;
+                i = pr.y;
+            }
+            sU[r] = u;
+            sI[r] = i;
+            // the example's identity for dropout: recorded-mask row, or the hash key
+            const int64_t colid = a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
+            const int64_t gj = q == 0 ? colid : (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
+            sR[r] = (int)gj;
+            sK[r] = hash32(a.seed ^ ((uint64_t)(q == 0 ? 0 : 1) << 40) ^ ((uint64_t)gj * 0x9E3779B97F4A7C15ULL));
+            // list slots are claimed now (the entry does not depend on the gradient), so the
+            // atomics' round trip overlaps the gather; overflow rows add from LDS at the end
+            int lu = -1, li = -1, ps = -1;
+            if (kBackward && u >= 0) {
+                const int64_t ex = tile * kRows + r;
+                lu = atomicAdd(a.row_count + u, 1);
+                if (lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+                if (q == 0 && a.pos_slot != nullptr) {
+                    ps = a.pos_slot[s];
+                } else {
+                    const int64_t row = a.num_users + i;
+                    li = atomicAdd(a.row_count + row, 1);
+                    if (li < kNcfCap) a.row_list[row * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+                }
+            }
+            sLu[r] = lu;
+            sLi[r] = li;
+            sPs[r] = ps;
+        }
+        __syncthreads();
+        // ---- gather A_0 = [U[u] | I[i]] ------------------------------------------------
+        for (int e = tid; e < kRows * (IN0 / 4); e += kNcfThreads) {
+            const int r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (sU[r] >= 0)
+                v = c4 < E ? *reinterpret_cast<const float4 *>(a.user_w + (int64_t)sU[r] * E + c4)
+                           : *reinterpret_cast<const float4 *>(a.item_w + (int64_t)sI[r] * E + (c4 - E));
+            float *d = sA + r * (IN0 + 1) + c4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __syncthreads();
+        // ---- forward hidden layers ---------------------------------------------------------
+        int mask_base = 0;
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int in = S::H(k), out = S::H(k + 1);
+            const float *Ak = sA + S::sa_off(k);
+            float *An = sA + S::sa_off(k + 1);
+            float *Mn = sM + S::sa_off(k + 1);
+            const float *Wk = sW + S::sw_off(k);
+            const float *bk = Wk + out * (in + 1);
+            const int ct = out < 16 ? 1 : out / 16;
+            for (int t = wave; t < 2 * ct; t += 4) {
+                const int i0 = (t / ct) * 16, j0 = (t % ct) * 16;
+                const v4f z = mma16(Ak, in + 1, 1, Wk, 1, in + 1, i0, j0, in, kRows, out, lane);
+                const int col = j0 + (lane & 15);
+                if (col < out) {
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = i0 + (lane >> 4) * 4 + rr;
+                        const float zz = z[rr] + bk[col];
+                        float m = zz > 0.0f ? 1.0f : 0.1f;
+                        if (a.training) {
+                            bool keep;
+                            if (a.mask_pos) {
+                                const int units = S::mask_units();
+                                const uint8_t *mk = row < tc ? a.mask_pos : a.mask_neg;
+                                keep = sU[row] >= 0 && mk[(int64_t)sR[row] * units + mask_base + col] != 0;
+                            } else {
+                                keep = (mix32(sK[row] + (uint32_t)(mask_base + col) * 0x85EBCA6BU) >> 7) & 1U;
+                            }
+                            m = keep ? 2.0f * m : 0.0f;
+                        }
+                        An[row * (out + 1) + col] = zz * m;
+                        Mn[row * (out + 1) + col] = m;
+                    }
+                }
+            }
+            mask_base += out;
+            __syncthreads();
+        }
+        // ---- output layer, scores, loss ---------------------------------------------------
+        {
+            const float *wo = sW + S::sw_off(NH);
+            const float *AN = sA + S::sa_off(NH);
+            if (tid < kRows) {
+                float d = 0.0f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d = fmaf(AN[tid * 9 + j], wo[j], d);
+                const float p = sigmoidf_ref(d + wo[8]);
+                sP[tid] = p;
+                if (PHASE == kNcfScores) a.scores[tile * kRows + tid] = sU[tid] >= 0 ? p : 0.0f;
+            }
+        }
+        __syncthreads();
+        if (PHASE == kNcfScores) continue;
+        // dL/dlogit per row (columns: one thread each) and the tile's loss partials
+        if (tid < kRows) sDz[tid] = 0.0f;
+        __syncthreads();
+        if (tid < tc) {
+            float la = 0.0f, lb = 0.0f;
+            {
+                const int cl = tid;
+                float dp[RG_MF_MAX_NEG + 1];
+                for (int q = 0; q < NP; ++q) dp[q] = 0.0f;
+                const int r0 = cl;
+                const bool has_pos = sU[r0] >= 0;
+                if (PHASE == kNcfGivenDp) {
+                    for (int q = 0; q < NP; ++q)
+                        if (sU[q * tc + cl] >= 0) dp[q] = a.dp_in[tile * kRows + q * tc + cl];
+                } else if (a.loss == RG_LOSS_POINTWISE) {
+                    if (has_pos) {
+                        const float p = sP[r0];
+                        la += -fmaxf(logf(p), -100.0f);
+                        dp[0] = ((p - 1.0f) / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_a;
+                    }
+                    for (int q = 1; q < NP; ++q) {
+                        const int r = q * tc + cl;
+                        if (sU[r] >= 0) {
+                            const float p = sP[r];
+                            lb += -fmaxf(logf(1.0f - p), -100.0f);
+                            dp[q] = (p / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_b;
+                        }
+                    }
+                } else if (has_pos) {   // bpr / hinge on the neg.view(n, B) pairing
+                    const float g = 1.0f / a.n_a, pp = sP[r0];
+                    for (int q = 1; q < NP; ++q) {
+                        const int r = q * tc + cl;
+                        if (sU[r] < 0) continue;
+                        if (a.loss == RG_LOSS_BPR) {
+                            const float sg = sigmoidf_ref(pp - sP[r]);
+                            la += 1.0f - sg;
+                            const float dx = (-g) * (1.0f - sg) * sg;
+                            dp[0] += dx;
+                            dp[q] = -dx;
+                        } else {
+                            const float x = (sP[r] - pp) + 1.0f;
+                            la += fmaxf(x, 0.0f);
+                            const float dx = x >= 0.0f ? g : 0.0f;
+                            dp[0] -= dx;
+                            dp[q] = dx;
+                        }
+                    }
+                }
+                for (int q = 0; q < NP; ++q) {
+                    const int r = q * tc + cl;
+                    const float p = sP[r];
+                    sDz[r] = sU[r] >= 0 ? (dp[q] * (1.0f - p)) * p : 0.0f;
+                }
+            }
+            sLa[cl_base + tid] = la;
+            sLb[cl_base + tid] = lb;
+        }
+        __syncthreads();
+        if (tid == 0) {     // column order, as the one-thread loop summed them
+            float la = 0.0f, lb = 0.0f;
+            for (int cl = 0; cl < tc; ++cl) { la += sLa[cl]; lb += sLb[cl]; }
+            a.loss_partials[2 * tile] = la;
+            a.loss_partials[2 * tile + 1] = lb;
+        }
+        __syncthreads();
+        if (PHASE == kNcfLossOnly) continue;         // validation: loss only (run_val_iteration)
+        // ---- backward ------------------------------------------------------------------------
+        {
+            // output layer: dW_out += sum_r dz_r A_NH[r], db_out += sum_r dz_r; G_NH = dz w_out^T
+            const float *wo = sW + S::sw_off(NH);
+            const float *AN = sA + S::sa_off(NH);
+            float *MN = sM + S::sa_off(NH);
+            if (tid < 9) {
+                float acc = 0.0f;
+                for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], tid < 8 ? AN[r * 9 + tid] : 1.0f, acc);
+                sG[S::w_off(NH) + tid] += acc;
+            }
+            for (int e = tid; e < kRows * 8; e += kNcfThreads) {
+                const int r = e / 8, j = e % 8;
+                MN[r * 9 + j] = (sDz[r] * wo[j]) * MN[r * 9 + j];      // delta_{NH-1} = G * m
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = NH - 1; k >= 0; --k) {
+            const int in = S::H(k), out = S::H(k + 1);
+            const float *Ak = sA + S::sa_off(k);
+            const float *Dk = sM + S::sa_off(k + 1);     // delta_k: [kRows][out + 1]
+            const float *Wk = sW + S::sw_off(k);
+            float *gW = sG + S::w_off(k);
+            // dW_k (out x in) += delta^T A_k ; db_k += column sums of delta
+            const int ro = out < 16 ? 1 : out / 16, ci = in / 16;
+            for (int t = wave; t < ro * ci; t += 4) {
+                const int i0 = (t / ci) * 16, j0 = (t % ci) * 16;
+                const v4f c = mma16(Dk, 1, out + 1, Ak, in + 1, 1, i0, j0, kRows, out, in, lane);
+                const int col = j0 + (lane & 15);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int o = i0 + (lane >> 4) * 4 + rr;
+                    if (o < out) gW[o * in + col] += c[rr];
+                }
+            }
+            for (int o = tid; o < out; o += kNcfThreads) {
+                float acc = 0.0f;
+                for (int r = 0; r < kRows; ++r) acc += Dk[r * (out + 1) + o];
+                gW[out * in + o] += acc;
+            }
+            // dA_k = delta W_k (kRows x in): k > 0 -> delta_{k-1} = dA * m_k ; k == 0 -> dX
+            const int cj = in / 16;
+            for (int t = wave; t < 2 * cj; t += 4) {
+                const int i0 = (t / cj) * 16, j0 = (t % cj) * 16;
+                const v4f c = mma16(Dk, out + 1, 1, Wk, in + 1, 1, i0, j0, out, kRows, in, lane);
+                const int col = j0 + (lane & 15);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = i0 + (lane >> 4) * 4 + rr;
+                    if (k > 0) {
+                        float *Mk = sM + S::sa_off(k);
+                        Mk[row * (in + 1) + col] = c[rr] * Mk[row * (in + 1) + col];
+                    } else {
+                        a.contrib[(tile * kRows + row) * (int64_t)IN0 + col] = c[rr];
+                        sX[row * (IN0 + 1) + col] = c[rr];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // ---- embedding gradient: overflow rows (hot users/items), planned item partials -----------
+        for (int e = tid; e < 2 * kRows * E; e += kNcfThreads) {
+            const int r = e / (2 * E), half = (e / E) & 1, c = e % E;
+            const int sl = half ? sLi[r] : sLu[r];
+            if (sl >= kNcfCap) {
+                const int64_t row = half ? a.num_users + sI[r] : (int64_t)sU[r];
+                atomicAdd(a.hot_grad + row * E + c, sX[r * (IN0 + 1) + half * E + c]);
+            }
+        }
+        if (a.pos_slot != nullptr) {
+            // positives' item halves, same plan slot -> one partial row (fixed order, plain stores)
+            for (int e = tid; e < tc * E; e += kNcfThreads) {
+                const int cl = e / E, c = e % E;
+                const int slot = sPs[cl];
+                if (slot < 0 || (cl > 0 && sPs[cl - 1] == slot)) continue;   // not the segment head
+                float acc = 0.0f;
+                for (int cc = cl; cc < tc && sPs[cc] == slot; ++cc) acc += sX[cc * (IN0 + 1) + E + c];
+                a.part_row[(int64_t)slot * E + c] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- the workgroup's weight-gradient partial ------------------------------------------------
+    if (kBackward)
+        for (int e = tid; e < P; e += kNcfThreads) a.wpart[(int64_t)blockIdx.x * P + e] = sG[e];
+}
+
+// reduce the weight-gradient partials + optimizer update of the MLP parameters in
+// place: a block owns 64 parameters, its 4 waves sum fixed quarters of the
+// partials (coalesced 256-B loads) and combine in LDS in a fixed order
+// (deterministic); block 0 also finalises the loss
+__global__ __launch_bounds__(256) void ncf_update_kernel(float *mlp, float *m, float *v, const float *wpart,
+                                                        int nparts, int P, rg_opt_t opt, const float *loss_partials,
+                                                        int64_t n_partials, double inv_a, double inv_b,
+                                                        float *loss_out) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (loss_out && blockIdx.x == 0 && wave == 0) {
+        double sa = 0.0, sb = 0.0;
+        for (int64_t i = lane; i < n_partials; i += 64) {
+            sa += (double)loss_partials[2 * i];
+            sb += (double)loss_partials[2 * i + 1];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            sa += __shfl_xor(sa, off);
+            sb += __shfl_xor(sb, off);
+        }
+        if (lane == 0) *loss_out = (float)(sa * inv_a + sb * inv_b);
+    }
+    const int e = blockIdx.x * 64 + lane;
+    const int q = (nparts + 3) / 4, k0 = wave * q, k1 = min(nparts, k0 + q);
+    float g = 0.0f;
+    if (e < P)
+        for (int k = k0; k < k1; ++k) g += wpart[(int64_t)k * P + e];
+    red[wave][lane] = g;
+    __syncthreads();
+    if (wave != 0 || e >= P) return;
+    g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
+    const float p = opt_update(opt, mlp[e], g, mm, vv);
+    mlp[e] = p;
+    if (m) m[e] = mm;
+    if (v) v[e] = vv;
+}
+
+// adaptive hinge from forward-only scores: dp of every row (positives: hinge
+// against the max negative; the argmax negative: minus the sum over active positives)
+__global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, float *dp, int64_t rows, int tc,
+                                                          int NP, int64_t n_pos_cols, int64_t cols, float n_a,
+                                                          float *loss_partial) {
+    __shared__ float smax[256];
+    __shared__ int64_t sidx[256];
+    __shared__ float scnt[256], sloss[256];
+    const int tid = threadIdx.x;
+    float best = -1.0f;
+    int64_t bi = -1;
+    for (int64_t r = tid; r < rows; r += 256) {
+        const int64_t tile = r / kRows, rr = r % kRows;
+        const int q = (int)(rr / tc);
+        const int64_t s = tile * tc + rr % tc;
+        dp[r] = 0.0f;
+        if (q >= 1 && q < NP && s < cols && scores[r] > best) { best = scores[r]; bi = r; }
+    }
+    smax[tid] = best;
+    sidx[tid] = bi;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {     // max, first occurrence in draw order on ties
+        if (tid < w) {
+            const bool take = smax[tid + w] > smax[tid];
+            if (take) { smax[tid] = smax[tid + w]; sidx[tid] = sidx[tid + w]; }
+        }
+        __syncthreads();
+    }
+    const float mx = smax[0];
+    float cnt = 0.0f, ls = 0.0f;
+    for (int64_t r = tid; r < rows; r += 256) {
+        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t s = tile * tc + rr % tc;
+        if (rr / tc == 0 && rr < (int64_t)tc && s < n_pos_cols) {
+            const float x = (mx - scores[r]) + 1.0f;
+            ls += fmaxf(x, 0.0f);
+            if (x >= 0.0f) { dp[r] = -(1.0f / n_a); cnt += 1.0f; }
+        }
+    }
+    scnt[tid] = cnt;
+    sloss[tid] = ls;
+    __syncthreads();
+    if (tid == 0) {
+        float c = 0.0f, l = 0.0f;
+        for (int i = 0; i < 256; ++i) { c += scnt[i]; l += sloss[i]; }
+        if (sidx[0] >= 0) dp[sidx[0]] = c * (1.0f / n_a);
+        loss_partial[0] = l;
+        loss_partial[1] = 0.0f;
+    }
+}
+
+template <int PHASE>
+struct NcfLaunchF {
+    NcfArgs *a;
+    hipStream_t s;
+    int blocks;
+    template <int E>
+    int run() {
+        using S = NcfShape<E>;
+        const size_t lds = (size_t)S::LDS * sizeof(float);
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(ncf_pairs_kernel<E, PHASE>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)lds) == hipSuccess;
+        if (!attr) return fail_arg("ncf_pairs_kernel: cannot reserve LDS");
+        hipLaunchKernelGGL((ncf_pairs_kernel<E, PHASE>), dim3(blocks), dim3(kNcfThreads), lds, s, *a);
+        return check_launch("rg_ncf_pairs");
+    }
+    int operator()(int E) {
+        switch (E) {
+            case 8: return run<8>();
+            case 16: return run<16>();
+            case 32: return run<32>();
+            case 64: return run<64>();
+            default: return fail_arg("NCF embedding_dim must be 8, 16, 32 or 64");
+        }
+    }
+};
+
+int ncf_mlp_len(int E) {
+    switch (E) {
+        case 8: return NcfShape<8>::P;
+        case 16: return NcfShape<16>::P;
+        case 32: return NcfShape<32>::P;
+        case 64: return NcfShape<64>::P;
+        default: return -1;
+    }
+}
+
+int ncf_mask_units(int E) {
+    switch (E) {
+        case 8: return NcfShape<8>::mask_units();
+        case 16: return NcfShape<16>::mask_units();
+        case 32: return NcfShape<32>::mask_units();
+        case 64: return NcfShape<64>::mask_units();
+        default: return -1;
+    }
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+extern "C" int64_t rg_ncf_mlp_len(int32_t dim) { return ncf_mlp_len(dim); }
+extern "C" int64_t rg_ncf_mask_units(int32_t dim) { return ncf_mask_units(dim); }
+extern "C" int64_t rg_ncf_cols_per_tile(int32_t n_neg) { return n_neg < 0 || n_neg >= kRows ? -1 : kRows / (n_neg + 1); }
+extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg) {
+    const int64_t tc = rg_ncf_cols_per_tile(n_neg);
+    return tc <= 0 ? -1 : (cols + tc - 1) / tc;
+}
+extern "C" int64_t rg_ncf_rows_per_tile(void) { return kRows; }
+extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg) {
+    const int64_t t = rg_ncf_tiles(cols, n_neg);
+    return t <= 0 ? -1 : (t < 256 ? t : 256);      // one resident workgroup per CU (LDS-bound)
+}
+
+extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_batch_t *b, rg_mf_work_t *w,
+                            rg_ncf_work_t *nw, int32_t phase) {
+    if (!m || !b || !w || !nw) return fail_arg("rg_ncf_pairs: null argument");
+    if (ncf_mlp_len(m->dim) < 0) return fail_arg("rg_ncf_pairs: embedding_dim must be 8, 16, 32 or 64");
+    if (b->n_neg < 1 || b->n_neg > RG_MF_MAX_NEG) return fail_arg("rg_ncf_pairs: n_neg out of range");
+    if (!b->pairs || !m->user_w || !m->item_w || !m->mlp) return fail_arg("rg_ncf_pairs: null tables / pairs");
+    if (b->n_pos > b->cols) return fail_arg("rg_ncf_pairs: n_pos > cols");
+    if (phase != kNcfScores && phase != kNcfLossOnly && (!w->row_count || !w->row_list || !w->hot_grad ||
+                                                         !w->loss_partials || !nw->contrib || !nw->mlp_partials))
+        return fail_arg("rg_ncf_pairs: null scratch");
+    if (phase == kNcfLossOnly && !w->loss_partials) return fail_arg("rg_ncf_pairs: loss needs partials");
+    if (phase == kNcfScores && !nw->scores) return fail_arg("rg_ncf_pairs: scores buffer needed");
+    if (phase == kNcfGivenDp && !nw->dp) return fail_arg("rg_ncf_pairs: dp buffer needed");
+    if ((phase == kNcfFused || phase == kNcfLossOnly) && b->loss == RG_LOSS_ADAPTIVE_HINGE)
+        return fail_arg("rg_ncf_pairs: adaptive hinge runs as scores -> rg_ncf_adapt_dp -> given-dp");
+    if (nw->training && (nw->mask_pos == nullptr) != (nw->mask_neg == nullptr))
+        return fail_arg("rg_ncf_pairs: give both dropout mask arrays or neither");
+    if (w->plan_pos_slot && !w->part_row) return fail_arg("rg_ncf_pairs: plan needs part_row");
+    NcfArgs a{};
+    a.user_w = m->user_w; a.item_w = m->item_w; a.mlp = m->mlp;
+    a.num_users = m->num_users; a.num_items = m->num_items;
+    a.pairs = reinterpret_cast<const int2 *>(b->pairs);
+    a.n_pos = b->n_pos; a.cols = b->cols; a.global_cols = b->global_cols; a.col_offset = b->col_offset;
+    a.n_neg = b->n_neg; a.loss = b->loss;
+    a.tc = (int)rg_ncf_cols_per_tile(b->n_neg);
+    a.tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    const int64_t negc = b->neg_cols > 0 ? b->neg_cols : b->global_cols;
+    switch (b->loss) {
+        case RG_LOSS_POINTWISE: a.n_a = (float)b->global_pos; a.n_b = (float)((int64_t)b->n_neg * negc); break;
+        case RG_LOSS_BPR:
+        case RG_LOSS_HINGE: a.n_a = (float)((int64_t)b->n_neg * b->global_pos); a.n_b = 1.0f; break;
+        default: a.n_a = (float)b->global_pos; a.n_b = 1.0f;
+    }
+    a.perm = w->plan_perm; a.pos_slot = w->plan_pos_slot;
+    a.row_count = w->row_count; a.row_list = reinterpret_cast<int2 *>(w->row_list);
+    a.hot_grad = w->hot_grad; a.part_row = w->part_row;
+    a.loss_partials = w->loss_partials;
+    a.contrib = nw->contrib; a.wpart = nw->mlp_partials; a.scores = nw->scores; a.dp_in = nw->dp;
+    a.mask_pos = nw->mask_pos; a.mask_neg = nw->mask_neg; a.seed = nw->seed; a.training = nw->training;
+    const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg);
+    if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
+    if (phase == kNcfScores) { NcfLaunchF<kNcfScores> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
+    if (phase == kNcfGivenDp) { NcfLaunchF<kNcfGivenDp> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
+    if (phase == kNcfLossOnly) { NcfLaunchF<kNcfLossOnly> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
+    return fail_arg("rg_ncf_pairs: bad phase");
+}
+
+extern "C" int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, float *loss_partials) {
+    if (!b || !nw || !nw->scores || !nw->dp || !loss_partials) return fail_arg("rg_ncf_adapt_dp: null argument");
+    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    hipLaunchKernelGGL(ncf_adapt_dp_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, nw->dp,
+                       tiles * kRows, (int)rg_ncf_cols_per_tile(b->n_neg), b->n_neg + 1, b->n_pos, b->cols,
+                       (float)b->global_pos, loss_partials);
+    return check_launch("rg_ncf_adapt_dp");
+}
+
+extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf_work_t *nw, int64_t nparts,
+                             const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss) {
+    if (!m || !nw || !opt || !nw->mlp_partials || !m->mlp) return fail_arg("rg_ncf_update: null argument");
+    if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_update: Adam needs m state");
+    if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_update: optimizer needs v state");
+    if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_update: loss needs partials");
+    const int P = ncf_mlp_len(m->dim);
+    if (P < 0) return fail_arg("rg_ncf_update: bad dim");
+    const bool with_loss = loss && loss->out;
+    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(256), 0, (hipStream_t)stream, m->mlp,
+                       opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,
+                       nw->mlp_partials, (int)nparts, P, *opt, with_loss ? loss_partials : nullptr,
+                       with_loss ? loss->n_partials : 0, with_loss ? loss->inv_a : 0.0,
+                       with_loss ? loss->inv_b : 0.0, with_loss ? loss->out : nullptr);
+    return check_launch("rg_ncf_update");
+}

@@ -1,0 +1,285 @@
+"""ImplicitFactorizationModel -- drop-in for the reference's implicit.py:31-471.
+
+Same constructor arguments, attributes, ``fit(train_set, valid_set, verbose)``,
+``run_train_iteration`` / ``run_val_iteration``, ``predict``, ``test`` and output
+files (``experiments_results/<name>/result_outputs/{configuration.json,
+summary.csv, test_summary.json}``, ``saved_models/best_model`` =
+``torch.save({'network': state_dict})``).  Training of a BilinearNet runs
+through the fused MI355X step (``mf_engine.MFEngine`` over librg_hip.so); there
+is no CPU training path.
+
+Semantics kept from the reference:
+* ``loss``: 'pointwise' -> pointwise, 'hinge' -> hinge, anything else of the
+  allowed names ('bpr', 'adaptive_hinge') -> adaptive hinge (implicit.py:194-199);
+  the build's pairwise BPR is the additive name 'pairwise_bpr';
+* negatives: ``random.choices(neg_examples, k=num_negative_samples * batch_size)``
+  from the module-level ``random`` stream (implicit.py:352), shared by training and
+  validation; the device stream starts at ``random.getstate()`` and is written
+  back with ``random.setstate`` after ``fit``;
+* one shuffle with the model's RandomState before the epochs (implicit.py:262),
+  ``set_seed(random_state.randint(-1e8, 1e8))`` at construction (:146);
+* the optimizer is what ``optimizer_func(params, weight_decay=l2, lr=lr)`` builds
+  (Adam when None), applied densely to every row every step;
+* best-by-validation-loss model, degenerate-loss ValueError, id-range ValueErrors.
+"""
+import copy
+import json
+import logging
+import os
+import random
+
+import numpy as np
+import torch
+
+from . import _mtstate
+from .mf_engine import MFEngine, build_plan
+from .ncf_engine import NCFEngine
+from .spotlight.factorization.representations import BilinearNet
+from .spotlight.optimizers import describe
+from .spotlight.sampling import NegativePool
+from .spotlight.torch_utils import set_seed, shuffle
+from .spotlight import evaluation
+from .utils.storage_utils import save_statistics
+
+logging.basicConfig(format="%(message)s", level=logging.INFO)
+
+_LOSS_MAP = {"pointwise": "pointwise", "hinge": "hinge", "bpr": "adaptive_hinge",
+             "adaptive_hinge": "adaptive_hinge", "pairwise_bpr": "bpr"}
+
+
+class ImplicitFactorizationModel:
+    def __init__(self, loss="pointwise", embedding_dim=32, n_iter=10, batch_size=256, l2=0.0,
+                 experiment_name="Implicit_Feedback", learning_rate=1e-2, optimizer_func=None, use_cuda=False,
+                 representation=None, sparse=False, model_name="mf", random_state=None, neg_examples=None,
+                 num_negative_samples=3):
+        self.exeriment_name = experiment_name
+        self.experiment_folder = os.path.abspath("experiments_results/" + experiment_name)
+        self.experiment_logs = os.path.join(self.experiment_folder, "result_outputs")
+        self.experiment_saved_models = os.path.join(self.experiment_folder, "saved_models")
+        self.starting_epoch = 0
+        for d in (self.experiment_logs, self.experiment_saved_models):
+            os.makedirs(d, exist_ok=True)
+        assert loss in _LOSS_MAP, loss
+        self._loss = loss
+        self._embedding_dim = embedding_dim
+        self._n_iter = n_iter
+        self._learning_rate = learning_rate
+        self._batch_size = batch_size
+        self._l2 = l2
+        self._use_cuda = use_cuda
+        self._representation = representation
+        self._sparse = sparse
+        self._optimizer_func = optimizer_func
+        self._random_state = random_state or np.random.RandomState()
+        self._num_negative_samples = num_negative_samples
+        self.neg_examples = neg_examples
+        self._num_users = None
+        self._num_items = None
+        self._net = None
+        self._engine = None
+        self.best_model = None
+        self.best_validation = None
+        self.model_name = model_name
+        self.best_epoch = -1
+        set_seed(self._random_state.randint(-10 ** 8, 10 ** 8), cuda=self._use_cuda)
+
+    def __repr__(self):
+        return "<ImplicitFactorizationModel: {}>".format(
+            "uninitialised" if self._net is None else f"{self._num_users} users x {self._num_items} items, "
+                                                      f"d={self._embedding_dim}, loss={self._loss}")
+
+    @property
+    def _initialized(self):
+        return self._net is not None
+
+    # ------------------------------------------------------------------ setup
+    def _device(self):
+        if not self._use_cuda:
+            raise RuntimeError("this implementation trains on the GPU only (librg_hip.so): pass use_cuda=True")
+        return torch.device("cuda", torch.cuda.current_device())
+
+    def _initialize(self, interactions):
+        self._num_users, self._num_items = interactions.num_users, interactions.num_items
+        dev = self._device()
+        net = self._representation
+        if net is None:
+            net = BilinearNet(self._num_users, self._num_items, self._embedding_dim, sparse=self._sparse)
+        self._net = net.to(dev)
+        self._opt = describe(self._optimizer_func, self._learning_rate, self._l2)
+        if not self.neg_examples:
+            raise NotImplementedError("training without a negative pool (neg_examples) is not supported")
+        self._pool = NegativePool.from_pairs(self.neg_examples)
+        o = self._opt
+        common = dict(loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
+                      betas=o.get("betas", (0.9, 0.999)), eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
+                      n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
+        if hasattr(net, "embedding_user") and hasattr(net, "layers"):          # NCF MLP (mlp.py:5-46)
+            self._kind = "ncf"
+            self._params = [net.embedding_user.weight, net.embedding_item.weight]
+            for lin in [m_ for m_ in net.layers if isinstance(m_, torch.nn.Linear)]:
+                self._params += [lin.weight, lin.bias]
+            self._embedding_dim = net.embedding_user.weight.shape[1]
+            self._engine = NCFEngine(self._params[0].detach(), self._params[1].detach(),
+                                     [p.detach() for p in self._params[2:]], self._pool.user_ids,
+                                     self._pool.item_ids, _mtstate.current(),
+                                     seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), **common)
+        elif hasattr(net, "user_embeddings") and hasattr(net, "item_biases"):   # BilinearNet
+            self._kind = "mf"
+            self._params = [net.user_embeddings.weight, net.item_embeddings.weight, net.user_biases.weight,
+                            net.item_biases.weight]
+            self._embedding_dim = net.user_embeddings.weight.shape[1]
+            w = [p.detach() for p in self._params]
+            self._engine = MFEngine(w[0], w[1], w[2].reshape(-1), w[3].reshape(-1), self._pool.user_ids,
+                                    self._pool.item_ids, _mtstate.current(), **common)
+        else:
+            raise NotImplementedError("the fused steps train BilinearNet and the NCF MLP representations")
+        self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
+                              "weight_decay": self._l2, "lr": self._learning_rate,
+                              "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
+                              "epochs": self._n_iter}
+        with open(os.path.join(self.experiment_logs, "configuration.json"), "w") as fp:
+            json.dump(self.configuration, fp)
+
+    def _check_input(self, user_ids, item_ids, allow_items_none=False):
+        user_id_max = user_ids if isinstance(user_ids, int) else user_ids.max()
+        if user_id_max >= self._num_users:
+            raise ValueError("Maximum user id greater than number of users in model.")
+        if allow_items_none and item_ids is None:
+            return
+        item_id_max = item_ids if isinstance(item_ids, int) else item_ids.max()
+        if item_id_max >= self._num_items:
+            raise ValueError("Maximum item id greater than number of items in model.")
+
+    # ------------------------------------------------------------------ training
+    def fit(self, train_set, valid_set, verbose=False):
+        self.train_set = train_set
+        users, items = shuffle(train_set.user_ids, train_set.item_ids, random_state=self._random_state)
+        if not self._initialized:
+            self._initialize(train_set)
+        self._check_input(train_set.user_ids, train_set.item_ids)
+        e, B, dev = self._engine, self._batch_size, self._engine.device
+        e.set_mt_state(_mtstate.current())
+        tu = torch.from_numpy(np.ascontiguousarray(users, dtype=np.int64)).to(dev)
+        ti = torch.from_numpy(np.ascontiguousarray(items, dtype=np.int64)).to(dev)
+        vu = torch.from_numpy(np.ascontiguousarray(valid_set.user_ids, dtype=np.int64)).to(dev)
+        vi = torch.from_numpy(np.ascontiguousarray(valid_set.item_ids, dtype=np.int64)).to(dev)
+        nb = (len(tu) + B - 1) // B
+        losses = torch.zeros(nb, dtype=torch.float32, device=dev)
+        total = {"train_loss": [], "validation_loss": [], "curr_epoch": []}
+        # the batches repeat every epoch (one shuffle): plans (and MF step inputs) are built once
+        if self._kind == "mf":
+            plans = [build_plan(ti[s * B:(s + 1) * B], B, e.units_per_block, e.I) for s in range(nb)]
+            inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
+        else:
+            plans = [e.make_plan(ti[s * B:(s + 1) * B]) for s in range(nb)]
+        for epoch in range(self._n_iter):
+            for s in range(nb):
+                if self._kind == "mf":
+                    e.train_step_in(inputs[s], inputs[s + 1] if s + 1 < nb else None, loss_out=losses[s:s + 1])
+                else:
+                    e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s],
+                                 loss_out=losses[s:s + 1])
+            tl = [float(x) for x in losses.cpu().numpy()]          # loss.item() per batch
+            train_epoch_loss = sum(tl) / nb
+            if np.isnan(train_epoch_loss) or train_epoch_loss == 0.0:
+                raise ValueError("Degenerate epoch loss: {}".format(train_epoch_loss))
+            vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B])[0]) for s in range(0, len(vu), B)]
+            valid_epoch_loss = sum(vl) / len(vl)
+            if self.best_validation is None or valid_epoch_loss < self.best_validation:
+                self.best_model = [t.detach().clone() for t in e.params()]
+                self.best_validation = valid_epoch_loss
+                self.best_epoch = epoch
+            if verbose:
+                logging.info("Epoch {}: training_loss {:10.5f}".format(epoch, train_epoch_loss))
+                logging.info("Epoch {}: validation_loss {:10.5f}".format(epoch, valid_epoch_loss))
+            total["train_loss"].append(np.mean(tl))
+            total["validation_loss"].append(np.mean(vl))
+            total["curr_epoch"].append(epoch)
+            save_statistics(experiment_log_dir=self.experiment_logs, filename="summary.csv", stats_dict=total,
+                            current_epoch=epoch, continue_from_mode=(self.starting_epoch != 0 or epoch > 0))
+        _mtstate.restore(e.mt_state())                 # the Python stream continues after fit
+        self._load_into_net(self.best_model)
+        if self._kind == "mf":
+            e.set_params(*self.best_model)
+        else:
+            e.set_params(self.best_model)
+        self.save_readable_model(self.experiment_saved_models, self._net.state_dict())
+        logging.info("Model chosen from epoch %d", self.best_epoch)
+
+    def _load_into_net(self, tables):
+        with torch.no_grad():
+            for p, t in zip(self._params, tables):
+                p.copy_(t.reshape(p.shape))
+
+    def run_train_iteration(self, batch_user, batch_item):
+        """One fused step on this batch (implicit.py:347-364); returns the loss (device, shape (1,))."""
+        e = self._engine
+        return e.train_step(batch_user.to(e.device, torch.int64).contiguous(),
+                            batch_item.to(e.device, torch.int64).contiguous())
+
+    def run_val_iteration(self, batch_user, batch_item):
+        e = self._engine
+        return e.val_loss(batch_user.to(e.device, torch.int64).contiguous(),
+                          batch_item.to(e.device, torch.int64).contiguous())
+
+    # ------------------------------------------------------------------ inference
+    def predict(self, user_ids, item_ids=None):
+        self._check_input(user_ids, item_ids, allow_items_none=True)
+        if item_ids is None:
+            item_ids = np.arange(self._num_items, dtype=np.int64)
+        if np.isscalar(user_ids):
+            user_ids = np.array(user_ids, dtype=np.int64)
+        u = torch.from_numpy(np.asarray(user_ids, dtype=np.int64).reshape(-1))
+        i = torch.from_numpy(np.asarray(item_ids, dtype=np.int64).reshape(-1))
+        if u.numel() != i.numel():
+            u = u.expand(i.numel())
+        return self._engine.scores(u, i).detach().cpu().numpy().flatten()
+
+    def score_users(self, users):
+        """Scores of every item for a block of users, (len(users), num_items) float32 on
+        the host (evaluation helper): one GEMM of the tables (MF), or the eval-mode MLP
+        over the block x items pairs (NCF)."""
+        u = torch.as_tensor(np.asarray(users, dtype=np.int64), device=self._engine.device)
+        if self._kind == "mf":
+            U, I, ub, ib = self._engine.params()
+            z = U[u] @ I.T + ub[u][:, None] + ib[None, :]
+            return torch.sigmoid(z).cpu().numpy()
+        items = torch.arange(self._num_items, device=u.device)
+        s = self._engine.scores(u.repeat_interleave(self._num_items), items.repeat(len(u)))
+        return s.reshape(len(u), self._num_items).detach().cpu().numpy()
+
+    def test(self, test_set, item_popularity, k=5, rmse_flag=False, precision_recall=False, map_recall=True):
+        test_results = {"k": k}
+        if rmse_flag:
+            dev = self._engine.device
+            tu = torch.from_numpy(np.asarray(test_set.user_ids, dtype=np.int64))
+            ti = torch.from_numpy(np.asarray(test_set.item_ids, dtype=np.int64))
+            total = 0.0
+            for s in range(0, len(tu), self._batch_size):
+                total += evaluation.rmse_score(self._net, tu[s:s + self._batch_size].to(dev),
+                                               ti[s:s + self._batch_size].to(dev))
+            total /= len(test_set)
+            logging.info("BCE: {}".format(np.sqrt(total)))
+            test_results["bce"] = float(np.sqrt(total))
+        if precision_recall:
+            pop_p, pop_r = evaluation.evaluate_popItems(item_popularity, test_set, k=k)
+            rand_p, rand_r = evaluation.evaluate_random(item_popularity, test_set, k=k)
+            p, r = evaluation.precision_recall_score(self, test=test_set, k=k)
+            logging.info(self.model_name + " precision@{} {} recall@{} {}".format(k, p, k, r))
+            logging.info("Random: precision@{} {} recall@{} {}".format(k, rand_p, k, rand_r))
+            logging.info("PopItem Algorithm: precision@{} {} recall@{} {}".format(k, pop_p, k, pop_r))
+            test_results.update(precision=float(p), recall=float(r), rand_prec=float(rand_p),
+                                rand_rec=float(rand_r), pop_prec=float(pop_p), pop_rec=float(pop_r), at_k=k)
+        if map_recall:
+            map_k = evaluation.map_at_k(self, test=test_set, k=k)
+            _, r = evaluation.precision_recall_score(self, test=test_set, k=k)
+            logging.info(self.model_name + " map@{} {} recall@{} {}".format(k, map_k, k, r))
+            test_results["map"] = float(map_k)
+        with open(os.path.join(self.experiment_logs, "test_summary.json"), "w") as fp:
+            json.dump(test_results, fp)
+        return test_results
+
+    def save_readable_model(self, model_save_dir, state_dict):
+        fname = os.path.join(model_save_dir, "best_model")
+        logging.info("Saving state in {}".format(fname))
+        torch.save({"network": {k: v.detach().cpu() for k, v in state_dict.items()}}, f=fname)

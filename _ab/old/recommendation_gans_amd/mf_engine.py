@@ -1,0 +1,503 @@
+"""Device-resident MF training engine: the fused replacement of
+``ImplicitFactorizationModel.run_train_iteration`` (implicit.py:347-364).
+
+Everything of the step lives in HBM and is only touched by librg_hip.so:
+
+    tables   user_w (U,d) item_w (I,d) user_b (U,) item_b (I,)   x2 (ping-pong)
+    optim    m, v of the same shapes (Adam), v only (RMSprop), none (SGD)
+    pool     negative pool as int32 (user, item) pairs, 8 B per entry
+    sampler  CPython MT19937 state (624 words + position) and two word buffers
+    scratch  per-row contribution counters/lists, overflow accumulators, loss partials
+
+Per step: rg_mf_pairs (forward, loss, dL/dz, contribution lists) then
+rg_mf_apply (pull gradients + optimizer over every row).  The native stepper
+(rg_stepper.cpp) generates the MT19937 words two steps ahead on a stream of its
+own and prepares the next step's pairs on another, so the sequential sampler is
+off the critical path.
+"""
+import ctypes
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import LOSS_KINDS, OPT_KINDS, RG_MF_LIST_CAP, RG_MF_MAX_NEG, RG_MT_PAD, check, ptr
+
+
+def _as_u32_tensor(words, device):
+    a = np.ascontiguousarray(np.asarray(words, dtype=np.uint32))
+    return torch.from_numpy(a.view(np.int32)).to(device)
+
+
+class DeviceSampler:
+    """CPython ``random`` stream on the GPU, bit-exact with ``random.choices``.
+
+    ``acquire(nwords)`` returns an int32 tensor holding the next ``nwords``
+    raw MT state words (bit pattern of uint32; tempered by the consumer) whose producer the current stream
+    has waited for; ``release()`` must follow the launch of the consumer and
+    starts generating the following ``nwords`` words on the side stream.
+    """
+
+    def __init__(self, mt_state, device, prefetch=True):
+        self.device = torch.device(device)
+        self.state = _as_u32_tensor(mt_state, self.device)
+        self.state_before = torch.empty(625, dtype=torch.int32, device=self.device)
+        self.prefetch = prefetch
+        self.side = torch.cuda.Stream(device=self.device)
+        self.bufs = [None, None]
+        self.ready = [torch.cuda.Event(), torch.cuda.Event()]
+        self.consumed = [None, None]
+        self.pending = None      # (buffer index, nwords)
+        self.cur = None
+
+    def _gen(self, b, nwords):
+        if self.bufs[b] is None or self.bufs[b].numel() < nwords:
+            with torch.cuda.stream(self.side):
+                self.bufs[b] = torch.empty(nwords + RG_MT_PAD, dtype=torch.int32, device=self.device)
+        with torch.cuda.stream(self.side):
+            if self.consumed[b] is not None:
+                self.side.wait_event(self.consumed[b])
+            check(_lib.load().rg_mt_generate(_lib.stream_handle(self.side), ptr(self.state), ptr(self.bufs[b]),
+                                             nwords, ptr(self.state_before)), "rg_mt_generate")
+            self.ready[b].record(self.side)
+
+    def _discard_pending(self):
+        if self.pending is None:
+            return
+        with torch.cuda.stream(self.side):
+            self.state.copy_(self.state_before)   # ordered after the prefetch on the side stream
+        self.pending = None
+
+    def acquire(self, nwords):
+        cur = torch.cuda.current_stream(self.device)
+        if self.pending is not None and self.pending[1] == nwords:
+            b = self.pending[0]
+            self.pending = None
+        else:
+            self._discard_pending()
+            b = 0 if self.cur is None else 1 - self.cur
+            self._gen(b, nwords)
+        cur.wait_event(self.ready[b])
+        self.cur = b
+        self._nwords = nwords
+        return self.bufs[b]
+
+    def release(self):
+        b = self.cur
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.consumed[b] = ev
+        if self.prefetch:
+            nb = 1 - b
+            self._gen(nb, self._nwords)
+            self.pending = (nb, self._nwords)
+
+    def export_state(self):
+        """625-word state after the last CONSUMED word (prefetched words are not drawn)."""
+        self.side.synchronize()
+        torch.cuda.current_stream(self.device).synchronize()
+        src = self.state_before if self.pending is not None else self.state
+        return src.cpu().numpy().view(np.uint32).copy()
+
+    def import_state(self, mt_state):
+        self.side.synchronize()
+        self.pending = None
+        self.state.copy_(_as_u32_tensor(mt_state, self.device))
+
+
+MFPlan = namedtuple("MFPlan", "perm pos_slot item_slot_off")
+
+
+def build_plan(pos_i, cols, units_per_block, num_items):
+    """Per-batch plan (include/rg_hip.h, rg_mf_work_t): process positives in
+    item-sorted column order; one partial slot per (item, pair-kernel block).
+
+    The reference shuffles the training set once per fit (implicit.py:262), so
+    every epoch revisits the same batches: plans are loop-invariant and are
+    built once per fit (``build_epoch_plans``)."""
+    dev = pos_i.device
+    n_pos = pos_i.numel()
+    items_sorted, order = torch.sort(pos_i, stable=True)
+    perm = torch.cat([order, torch.arange(n_pos, cols, device=dev)]).to(torch.int32)
+    blk = torch.arange(n_pos, device=dev) // units_per_block
+    new = torch.ones(n_pos, dtype=torch.bool, device=dev)
+    if n_pos > 1:
+        new[1:] = (items_sorted[1:] != items_sorted[:-1]) | (blk[1:] != blk[:-1])
+    slot = torch.cumsum(new.to(torch.int32), 0) - 1
+    pos_slot = torch.full((cols,), -1, dtype=torch.int32, device=dev)
+    pos_slot[:n_pos] = slot.to(torch.int32)
+    seg_items = items_sorted[new]
+    off = torch.searchsorted(seg_items, torch.arange(num_items + 1, device=dev)).to(torch.int32)
+    return MFPlan(perm.contiguous(), pos_slot.contiguous(), off.contiguous())
+
+
+def build_epoch_plans(items, batch_size, units_per_block, num_items, offset=0, stride=None):
+    """Plans of every batch of an epoch: batch k covers positives
+    [offset + k*stride, offset + k*stride + batch_size) of ``items`` (device int64)."""
+    stride = stride or batch_size
+    plans = []
+    n = items.numel()
+    k = 0
+    while offset + k * stride < n:
+        lo = offset + k * stride
+        plans.append(build_plan(items[lo:min(lo + batch_size, n)], batch_size, units_per_block, num_items))
+        k += 1
+    return plans
+
+
+class MFEngine:
+    """Owns the device state of one BilinearNet training run on one GPU (one rank) and
+    the native step runtime (rg_mf_stepper_*) that enqueues each step."""
+
+    def __init__(self, user_w, item_w, user_b, item_b, pool_u, pool_i, mt_state, *, loss="pointwise",
+                 optimizer="adam", lr=1e-3, weight_decay=0.0, betas=(0.5, 0.999), eps=1e-8, alpha=0.99,
+                 n_neg=5, batch_size=256, device="cuda", rank=0, world_size=1, prefetch=True,
+                 dp=None, comm=None):
+        """``dp``: data-parallel layout when world_size > 1 --
+        "user_shard" (default): the tables passed are this rank's user shard plus every
+            item (sharding.py); own MT stream, local draw layout, the item gradient is
+            the only exchange (``comm``: an RcclComm, else ``train_step_sharded``);
+        "global_stream": replicated tables, every rank draws its slice of one global
+            stream (rank r takes columns [r*B, (r+1)*B) of the global batch's draw),
+            the full flat gradient is exchanged (``train_step_dp``)."""
+        _lib.require_gpu()
+        if loss not in LOSS_KINDS:
+            raise ValueError(f"unknown loss {loss!r}")
+        if optimizer not in OPT_KINDS:
+            raise ValueError(f"unknown optimizer {optimizer!r}")
+        if not 1 <= n_neg <= RG_MF_MAX_NEG:
+            raise ValueError(f"num_negative_samples must be in [1, {RG_MF_MAX_NEG}] for the fused kernel")
+        dp = dp or ("user_shard" if world_size > 1 or comm is not None else None)
+        if dp not in (None, "user_shard", "global_stream"):
+            raise ValueError(f"unknown data-parallel layout {dp!r}")
+        if loss == "adaptive_hinge" and world_size != 1:
+            raise NotImplementedError("adaptive_hinge is implemented for world_size 1")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        dev = self.device
+        self.U, self.I = int(user_w.shape[0]), int(item_w.shape[0])
+        self.dim = int(user_w.shape[1])
+        if not 1 <= self.dim <= 256:
+            raise ValueError("embedding_dim must be in [1, 256]")
+        if self.U + self.I >= 2 ** 31:
+            raise ValueError("num_users + num_items must be < 2^31")
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        def put(t, shape):
+            return torch.as_tensor(t, dtype=torch.float32).reshape(shape).to(dev).contiguous()
+
+        self.tabs = [[put(user_w, (self.U, self.dim)), put(item_w, (self.I, self.dim)),
+                      put(user_b, (self.U,)), put(item_b, (self.I,))]]
+        self.tabs.append([torch.empty_like(t) for t in self.tabs[0]])
+        self.opt_kind = optimizer
+        self.m = [torch.zeros_like(t) for t in self.tabs[0]] if optimizer == "adam" else [None] * 4
+        self.v = [torch.zeros_like(t) for t in self.tabs[0]] if optimizer != "sgd" else [None] * 4
+        self.lr, self.wd, self.betas, self.eps, self.alpha = lr, weight_decay, betas, eps, alpha
+        pu = np.asarray(pool_u, dtype=np.int64)
+        pi = np.asarray(pool_i, dtype=np.int64)
+        if len(pu) == 0 or len(pu) != len(pi):
+            raise ValueError("negative pool must be non-empty with matching user/item arrays")
+        if pu.min() < 0 or pu.max() >= self.U or pi.min() < 0 or pi.max() >= self.I:
+            raise ValueError("negative pool contains ids outside the model's tables")
+        self.pool = torch.from_numpy(np.stack([pu, pi], 1).astype(np.int32)).to(dev).contiguous()
+        self.pool_len = len(pu)
+        self.loss = loss
+        self.n_neg = int(n_neg)
+        self.batch_size = int(batch_size)
+        self.rank, self.world = int(rank), int(world_size)
+        self.dp = dp
+        self.comm = comm
+        if dp == "global_stream":
+            self.col_offset, self.global_cols = self.rank * self.batch_size, self.batch_size * self.world
+        else:
+            self.col_offset, self.global_cols = 0, self.batch_size
+        self.neg_cols = self.batch_size * self.world
+        self.words_per_step = 2 * self.n_neg * self.global_cols
+        self.prefetch = prefetch
+        rows = self.U + self.I
+        self.row_count = torch.zeros(rows, dtype=torch.int32, device=dev)
+        self.row_list = torch.empty(rows * RG_MF_LIST_CAP * 2, dtype=torch.int32, device=dev)
+        self.hot_grad = torch.zeros(rows * self.dim, **f32)
+        self.hot_bias = torch.zeros(rows, **f32)
+        self.n_partials = self.lib.rg_mf_partials_len(self.batch_size, self.dim) // 2
+        self.partials = torch.zeros(2 * self.n_partials, **f32)
+        self.scores_buf = torch.empty(self.batch_size, **f32) if loss == "adaptive_hinge" else None
+        self.max_key = torch.zeros(1, dtype=torch.int64, device=dev) if loss == "adaptive_hinge" else None
+        self.active_count = torch.zeros(1, dtype=torch.int32, device=dev) if loss == "adaptive_hinge" else None
+        self.loss_out = torch.zeros(1, **f32)
+        self.part_row = torch.zeros(self.batch_size * self.dim, **f32)
+        self.part_bias = torch.zeros(self.batch_size, **f32)
+        self.units_per_block = int(self.lib.rg_mf_plan_units_per_block(self.dim))
+        self.grad_buf = None
+        self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
+        self.mt_buf = _as_u32_tensor(mt_state, dev)
+        self.pairs = [torch.zeros((1 + self.n_neg) * self.batch_size * 2, dtype=torch.int32, device=dev)
+                      for _ in range(2)]
+        self._work = _lib.MFWork(ptr(self.row_count), ptr(self.row_list), ptr(self.hot_grad), ptr(self.hot_bias),
+                                 ptr(self.partials), ptr(self.scores_buf), ptr(self.max_key),
+                                 ptr(self.active_count), None, None, None, ptr(self.part_row),
+                                 ptr(self.part_bias))
+        self._tables = [self._make_tables(0), self._make_tables(1)]
+        cfg = _lib.MFStepperConfig()
+        cfg.tables[0], cfg.tables[1] = self._tables[0], self._tables[1]
+        cfg.work = self._work
+        cfg.mt_state = ptr(self.mt_buf)
+        cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
+        cfg.pool, cfg.pool_len = ptr(self.pool), self.pool_len
+        cfg.n_neg, cfg.loss = self.n_neg, LOSS_KINDS[loss]
+        cfg.cols, cfg.col_offset, cfg.global_cols = self.batch_size, self.col_offset, self.global_cols
+        cfg.neg_cols = self.neg_cols
+        cfg.item_grad = ptr(self.item_grad)
+        cfg.comm = comm.handle if comm is not None else None
+        cfg.opt = self._opt_base()
+        cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
+        cfg.step, cfg.n_partials, cfg.current_set = 0, self.n_partials, 0
+        self._stepper = self.lib.rg_mf_stepper_create(ctypes.byref(cfg))
+        if not self._stepper:
+            raise RuntimeError("rg_mf_stepper_create: " + self.lib.rg_last_error().decode())
+        self._cfg = cfg   # keep alive
+
+    def __del__(self):
+        st = getattr(self, "_stepper", None)
+        if st:
+            try:
+                self.lib.rg_mf_stepper_destroy(st)
+            except Exception:
+                pass
+            self._stepper = None
+
+    # ------------------------------------------------------------------ plumbing
+    def _make_tables(self, cur):
+        a, b = self.tabs[cur], self.tabs[1 - cur]
+        m, v = self.m, self.v
+        return _lib.MFTables(ptr(a[0]), ptr(a[1]), ptr(a[2]), ptr(a[3]),
+                             ptr(b[0]), ptr(b[1]), ptr(b[2]), ptr(b[3]),
+                             ptr(m[0]), ptr(v[0]), ptr(m[1]), ptr(v[1]),
+                             ptr(m[2]), ptr(v[2]), ptr(m[3]), ptr(v[3]),
+                             self.U, self.I, self.dim, 0)
+
+    def _opt_base(self):
+        o = _lib.Opt()
+        o.kind = OPT_KINDS[self.opt_kind]
+        o.lr, o.beta1, o.beta2 = self.lr, self.betas[0], self.betas[1]
+        o.eps, o.weight_decay, o.alpha = self.eps, self.wd, self.alpha
+        o.one_minus_beta1 = 1 - self.betas[0]
+        o.one_minus_beta2 = 1 - self.betas[1]
+        o.one_minus_alpha = 1 - self.alpha
+        return o
+
+    def _state(self):
+        cs = ctypes.c_int32()
+        st = ctypes.c_int64()
+        check(self.lib.rg_mf_stepper_state(self._stepper, ctypes.byref(cs), ctypes.byref(st)), "stepper_state")
+        return cs.value, st.value
+
+    @property
+    def cur(self):
+        return self._state()[0]
+
+    @property
+    def t(self):
+        return self._state()[1]
+
+    def params(self):
+        """Current (user_w, item_w, user_b, item_b) device tensors."""
+        return self.tabs[self.cur]
+
+    def loss_scales(self, global_pos):
+        n, gc = self.n_neg, self.neg_cols
+        if self.loss == "pointwise":
+            return 1.0 / global_pos, 1.0 / (n * gc)
+        if self.loss in ("bpr", "hinge"):
+            return 1.0 / (n * global_pos), 0.0
+        return 1.0 / global_pos, 0.0
+
+    def make_plan(self, pos_i):
+        return build_plan(pos_i, self.batch_size, self.units_per_block, self.I)
+
+    def _loss(self, global_pos, out):
+        ia, ib = self.loss_scales(global_pos)
+        return _lib.MFLoss(self.n_partials, ia, ib, ptr(out))
+
+    def _check_ids(self, pos_u, pos_i):
+        for t in (pos_u, pos_i):
+            if t.dtype != torch.int64 or t.device != self.device or not t.is_contiguous():
+                raise ValueError("positive ids must be contiguous int64 tensors on the engine's device")
+        if pos_u.numel() != pos_i.numel() or pos_u.numel() > self.batch_size:
+            raise ValueError("positive id batch larger than batch_size or mismatched")
+
+    def step_input(self, pos_u, pos_i, global_pos=None, plan=None):
+        self._check_ids(pos_u, pos_i)
+        n_pos = int(pos_u.numel())
+        global_pos = n_pos * self.world if global_pos is None else int(global_pos)
+        x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos, global_pos,
+                          None, None, None)
+        if plan is not None:
+            x.plan_perm, x.plan_pos_slot, x.plan_item_slot_off = ptr(plan.perm), ptr(plan.pos_slot), \
+                ptr(plan.item_slot_off)
+        x._keep = (pos_u, pos_i, plan)
+        return x
+
+    # ------------------------------------------------------------------ step
+    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, apply_events=None, next_input=None):
+        """One training step on this rank's positives; returns the device loss tensor (1,).
+        ``plan``: optional MFPlan for this batch (see build_plan).  ``next_input``: the
+        following step's ``step_input(...)`` -- its words and pairs are then produced
+        ahead on the side stream.  ``apply_events``: optional (start, end) torch.cuda.Event
+        pair recorded around the rg_mf_apply launch (kernel timing for the roofline)."""
+        cur = self.step_input(pos_u, pos_i, global_pos, plan)
+        return self.train_step_in(cur, next_input if self.prefetch else None, apply_events)
+
+    def train_step_in(self, cur, next_input=None, apply_events=None, loss_out=None):
+        """One native step for a prebuilt ``step_input``; the loss goes to ``loss_out``
+        (a float32 device tensor of >= 1 element) or to the engine's own slot."""
+        if self.dp == "user_shard" and self.world > 1 and self.comm is None:
+            raise RuntimeError("user-sharded step over several ranks needs an RcclComm (or train_step_sharded)")
+        if self.dp == "global_stream" and self.world > 1:
+            raise RuntimeError("dp='global_stream' steps go through train_step_dp")
+        ev0 = ev1 = None
+        if apply_events is not None:
+            ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
+        out = self.loss_out if loss_out is None else loss_out
+        if out.dtype != torch.float32 or out.device != self.device:
+            raise ValueError("loss_out must be a float32 tensor on the engine's device")
+        check(self.lib.rg_mf_stepper_train(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
+                                           ctypes.byref(next_input) if next_input is not None else None,
+                                           ptr(out), ev0, ev1), "rg_mf_stepper_train")
+        return out
+
+    def _acquire(self, cur):
+        batch, work = _lib.MFBatch(), _lib.MFWork()
+        check(self.lib.rg_mf_stepper_acquire(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
+                                             ctypes.byref(batch), ctypes.byref(work)), "rg_mf_stepper_acquire")
+        return batch, work
+
+    def _release(self):
+        check(self.lib.rg_mf_stepper_release(self._stepper, _lib.stream_handle()), "rg_mf_stepper_release")
+
+    def _flat_grad(self, nrows):
+        n = nrows * (self.dim + 1) + 1
+        if self.grad_buf is None or self.grad_buf.numel() < n:
+            self.grad_buf = torch.zeros(n, dtype=torch.float32, device=self.device)
+        return self.grad_buf[:n]
+
+    def pairs_and_lists(self, pos_u, pos_i, global_pos=None, plan=None):
+        """rg_mf_pairs with backward on this step's draw; the lists are then consumed by
+        ``grads`` / ``apply_rows``."""
+        cur = self.step_input(pos_u, pos_i, global_pos, plan)
+        batch, work = self._acquire(cur)
+        check(self.lib.rg_mf_pairs(_lib.stream_handle(), self._tables[self.cur], ctypes.byref(batch),
+                                   ctypes.byref(work), 1), "rg_mf_pairs")
+        self._release()
+        self._work_step = work
+        self._global_pos = cur.global_pos
+        return cur
+
+    def grads(self, pos_u, pos_i, global_pos=None, plan=None, row_begin=0, row_end=-1):
+        """pairs + gradient pull of rows [row_begin, row_end) into the flat buffer
+        [n*d | n | loss]; no update.  Returns the (device) flat buffer."""
+        self.pairs_and_lists(pos_u, pos_i, global_pos, plan)
+        return self.pull_grads(row_begin, row_end)
+
+    def pull_grads(self, row_begin=0, row_end=-1):
+        re = self.U + self.I if row_end < 0 else row_end
+        g = self._flat_grad(re - row_begin)
+        check(self.lib.rg_mf_grads(_lib.stream_handle(), self._tables[self.cur], ctypes.byref(self._work_step),
+                                   ptr(g), row_begin, re, self._loss(self._global_pos, self.loss_out)),
+              "rg_mf_grads")
+        return g
+
+    def _opt_step(self, t):
+        o = _lib.Opt()
+        check(self.lib.rg_mf_stepper_opt(self._stepper, t, ctypes.byref(o)), "rg_mf_stepper_opt")
+        return o
+
+    def apply_rows(self, row_begin, row_end, loss=True):
+        """Pull + optimizer update of rows [row_begin, row_end) from the current lists
+        (does not flip the table sets; see ``finish_step``)."""
+        o = self._opt_step(self.t + 1)
+        check(self.lib.rg_mf_apply(_lib.stream_handle(), self._tables[self.cur], ctypes.byref(self._work_step),
+                                   ctypes.byref(o), row_begin, row_end,
+                                   self._loss(self._global_pos, self.loss_out) if loss else None), "rg_mf_apply")
+
+    def apply_dense_rows(self, grad, row_begin, row_end):
+        o = self._opt_step(self.t + 1)
+        check(self.lib.rg_mf_apply_dense(_lib.stream_handle(), self._tables[self.cur], ptr(grad), ctypes.byref(o),
+                                         row_begin, row_end, ptr(self.loss_out)), "rg_mf_apply_dense")
+
+    def finish_step(self):
+        """After a split step updated every row: flip the ping-pong sets, count the step."""
+        check(self.lib.rg_mf_stepper_advance(self._stepper, 1, 1), "rg_mf_stepper_advance")
+
+    def apply_dense(self, grad):
+        """Optimizer update of every row from a (summed) flat gradient buffer."""
+        self.apply_dense_rows(grad, 0, self.U + self.I)
+        self.finish_step()
+        return self.loss_out
+
+    def train_step_dp(self, pos_u, pos_i, global_pos, allreduce, plan=None):
+        """Data-parallel step with replicated tables: local pairs -> local flat gradient ->
+        ``allreduce`` (in-place sum across ranks, e.g. torch.distributed.all_reduce over
+        RCCL) -> replicated update."""
+        g = self.grads(pos_u, pos_i, global_pos, plan=plan)
+        allreduce(g)
+        return self.apply_dense(g)
+
+    def train_step_sharded(self, pos_u, pos_i, global_pos, allreduce, plan=None):
+        """The user-sharded step with the item-gradient exchange done by ``allreduce``
+        (in-place sum, e.g. torch.distributed over gloo in tests): what
+        rg_mf_stepper_train does natively with an RCCL communicator."""
+        if self.dp != "user_shard":
+            raise RuntimeError("train_step_sharded needs dp='user_shard'")
+        self.pairs_and_lists(pos_u, pos_i, global_pos, plan)
+        g = self.pull_grads(self.U, self.U + self.I)
+        allreduce(g)
+        self.apply_rows(0, self.U, loss=False)
+        self.apply_dense_rows(g, self.U, self.U + self.I)
+        self.finish_step()
+        return self.loss_out
+
+    def val_loss(self, pos_u, pos_i, global_pos=None):
+        """run_val_iteration (implicit.py:366): forward + loss on the same draw stream, no update."""
+        cur = self.step_input(pos_u, pos_i, global_pos, None)
+        batch, work = self._acquire(cur)
+        stream = _lib.stream_handle()
+        check(self.lib.rg_mf_pairs(stream, self._tables[self.cur], ctypes.byref(batch), ctypes.byref(work), 0),
+              "rg_mf_pairs")
+        self._release()
+        ia, ib = self.loss_scales(cur.global_pos)
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        check(self.lib.rg_loss_finalize(stream, ptr(self.partials), self.n_partials, ia, ib, ptr(out)),
+              "rg_loss_finalize")
+        return out
+
+    def scores(self, users, items):
+        """BilinearNet.forward (representations.py:62-91) for eval/predict."""
+        users = users.to(self.device, torch.int64).contiguous()
+        items = items.to(self.device, torch.int64).contiguous()
+        out = torch.empty(users.numel(), dtype=torch.float32, device=self.device)
+        U, I, ub, ib = self.params()
+        check(self.lib.rg_mf_scores(_lib.stream_handle(), ptr(U), ptr(I), ptr(ub), ptr(ib), self.dim,
+                                    ptr(users), ptr(items), users.numel(), ptr(out)), "rg_mf_scores")
+        return out
+
+    def set_params(self, user_w, item_w, user_b, item_b):
+        """Overwrite the current tables (teacher forcing in tests, checkpoint load)."""
+        for dst, src in zip(self.tabs[self.cur], (user_w, item_w, user_b, item_b)):
+            dst.copy_(torch.as_tensor(src, dtype=torch.float32).reshape(dst.shape))
+
+    def mt_state(self):
+        """CPython random state (624 words + position) after the last consumed draw."""
+        host = np.zeros(625, dtype=np.uint32)
+        check(self.lib.rg_mf_stepper_sync_mt(self._stepper, host.ctypes.data_as(ctypes.c_void_p), 0),
+              "rg_mf_stepper_sync_mt")
+        return host
+
+    def set_mt_state(self, st):
+        host = np.ascontiguousarray(np.asarray(st, dtype=np.uint32))
+        check(self.lib.rg_mf_stepper_sync_mt(self._stepper, host.ctypes.data_as(ctypes.c_void_p), 1),
+              "rg_mf_stepper_sync_mt")
+
+    def optimizer_state(self):
+        return {"step": self.t, "m": self.m, "v": self.v}

@@ -1,0 +1,265 @@
+"""Device-resident NCF MLP training engine: the fused replacement of
+run_train_iteration (implicit.py:347-364) for the reference's MLP representation
+(spotlight/dnn_models/mlp.py:5-46; layers as ncf_spotlight.py:53-56).
+
+Per step: the native stepper provides the step's CPython-exact negatives
+(rg_mt_generate + rg_mf_prepare, shared with the MF path), then
+rg_ncf_pairs (fused MLP forward / loss / backward on MFMA) -> rg_ncf_update
+(MLP weight-gradient reduce + optimizer) -> rg_ncf_apply (embedding pull +
+optimizer over every row).  Adaptive hinge runs scores -> rg_ncf_adapt_dp ->
+given-dp.  Dropout: recorded masks (parity with the reference's CPU generator)
+or a per-(step, example, unit) hash (the documented device RNG)."""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import LOSS_KINDS, OPT_KINDS, RG_MF_LIST_CAP, RG_MF_MAX_NEG, check, ptr
+from .mf_engine import build_plan
+
+
+class NCFEngine:
+    def __init__(self, user_w, item_w, mlp_params, pool_u, pool_i, mt_state, *, loss="pointwise", optimizer="adam",
+                 lr=1e-3, weight_decay=0.0, betas=(0.5, 0.999), eps=1e-8, alpha=0.99, n_neg=5, batch_size=256,
+                 device="cuda", seed=0):
+        _lib.require_gpu()
+        if loss not in LOSS_KINDS:
+            raise ValueError(f"unknown loss {loss!r}")
+        if optimizer not in OPT_KINDS:
+            raise ValueError(f"unknown optimizer {optimizer!r}")
+        if not 1 <= n_neg <= RG_MF_MAX_NEG:
+            raise ValueError(f"num_negative_samples must be in [1, {RG_MF_MAX_NEG}]")
+        self.lib = lib = _lib.load()
+        self.device = dev = torch.device(device)
+        self.U, self.I = int(user_w.shape[0]), int(item_w.shape[0])
+        self.E = E = int(user_w.shape[1])
+        self.P = int(lib.rg_ncf_mlp_len(E))
+        if self.P < 0:
+            raise ValueError("NCF embedding_dim must be 8, 16, 32 or 64")
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.user_w = torch.as_tensor(user_w, dtype=torch.float32).to(dev).contiguous()
+        self.item_w = torch.as_tensor(item_w, dtype=torch.float32).to(dev).contiguous()
+        flat = torch.cat([torch.as_tensor(p, dtype=torch.float32).reshape(-1) for p in mlp_params])
+        if flat.numel() != self.P:
+            raise ValueError(f"MLP parameters have {flat.numel()} values, the E={E} layout has {self.P}")
+        self.mlp_shapes = [tuple(torch.as_tensor(p).shape) for p in mlp_params]
+        self.mlp = flat.to(dev).contiguous()
+        self.opt_kind = optimizer
+        st = lambda t: torch.zeros_like(t)
+        self.m = [st(self.user_w), st(self.item_w), st(self.mlp)] if optimizer == "adam" else [None] * 3
+        self.v = [st(self.user_w), st(self.item_w), st(self.mlp)] if optimizer != "sgd" else [None] * 3
+        self.lr, self.wd, self.betas, self.eps, self.alpha = lr, weight_decay, betas, eps, alpha
+        pu = np.asarray(pool_u, dtype=np.int64)
+        pi = np.asarray(pool_i, dtype=np.int64)
+        if len(pu) == 0 or len(pu) != len(pi) or pu.min() < 0 or pu.max() >= self.U or pi.min() < 0 \
+                or pi.max() >= self.I:
+            raise ValueError("negative pool empty or outside the tables")
+        self.pool = torch.from_numpy(np.stack([pu, pi], 1).astype(np.int32)).to(dev).contiguous()
+        self.loss, self.n_neg, self.batch_size = loss, int(n_neg), int(batch_size)
+        B, n = self.batch_size, self.n_neg
+        self.tc = int(lib.rg_ncf_cols_per_tile(n))
+        self.tiles = int(lib.rg_ncf_tiles(B, n))
+        self.rows = self.tiles * int(lib.rg_ncf_rows_per_tile())
+        self.blocks = int(lib.rg_ncf_blocks(B, n))
+        self.units = int(lib.rg_ncf_mask_units(E))
+        rows = self.U + self.I
+        self.row_count = torch.zeros(rows, dtype=torch.int32, device=dev)
+        self.row_list = torch.empty(rows * RG_MF_LIST_CAP * 2, dtype=torch.int32, device=dev)
+        self.hot_grad = torch.zeros(rows * E, **f32)
+        self.hot_bias = torch.zeros(rows, **f32)
+        self.partials = torch.zeros(2 * max(self.tiles, 1), **f32)
+        self.adapt_partials = torch.zeros(2, **f32)
+        self.part_row = torch.zeros(B * E, **f32)
+        self.contrib = torch.zeros(self.rows * 2 * E, **f32)
+        self.mlp_partials = torch.zeros(self.blocks * self.P, **f32)
+        self.scores_buf = torch.zeros(self.rows, **f32)
+        self.dp_buf = torch.zeros(self.rows, **f32)
+        self.loss_out = torch.zeros(1, **f32)
+        self.pairs = [torch.zeros((1 + n) * B * 2, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.mt_buf = torch.from_numpy(np.ascontiguousarray(np.asarray(mt_state, np.uint32)).view(np.int32)).to(dev)
+        self.seed = int(seed)
+        self.t = 0
+        self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
+        self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
+                                    ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
+                                    self.U, self.I, E, 0)
+        # the sampler / prepare part of the native stepper (its MF tables are unused here)
+        tabs = _lib.MFTables(ptr(self.user_w), ptr(self.item_w), None, None, None, None, None, None,
+                             None, None, None, None, None, None, None, None, self.U, self.I, E, 0)
+        cfg = _lib.MFStepperConfig()
+        cfg.tables[0], cfg.tables[1] = tabs, tabs
+        cfg.work = _lib.MFWork(ptr(self.row_count), ptr(self.row_list), ptr(self.hot_grad), ptr(self.hot_bias),
+                               ptr(self.partials), None, None, None, None, None, None, ptr(self.part_row), None)
+        cfg.mt_state = ptr(self.mt_buf)
+        cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
+        cfg.pool, cfg.pool_len = ptr(self.pool), len(pu)
+        cfg.n_neg, cfg.loss = n, LOSS_KINDS[loss]
+        cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, 0, B, B
+        cfg.opt = self._opt_base()
+        cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
+        self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
+        if not self._stepper:
+            raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())
+        self._cfg = cfg
+
+    def __del__(self):
+        st = getattr(self, "_stepper", None)
+        if st:
+            try:
+                self.lib.rg_mf_stepper_destroy(st)
+            except Exception:
+                pass
+            self._stepper = None
+
+    def _opt_base(self):
+        o = _lib.Opt()
+        o.kind = OPT_KINDS[self.opt_kind]
+        o.lr, o.beta1, o.beta2 = self.lr, self.betas[0], self.betas[1]
+        o.eps, o.weight_decay, o.alpha = self.eps, self.wd, self.alpha
+        o.one_minus_beta1, o.one_minus_beta2, o.one_minus_alpha = 1 - self.betas[0], 1 - self.betas[1], 1 - self.alpha
+        return o
+
+    def _opt(self, t):
+        o = _lib.Opt()
+        check(self.lib.rg_mf_stepper_opt(self._stepper, t, ctypes.byref(o)), "rg_mf_stepper_opt")
+        return o
+
+    def make_plan(self, pos_i):
+        return build_plan(pos_i, self.batch_size, self.tc, self.I)
+
+    def mlp_params(self):
+        """The MLP parameters as tensors of their reference shapes (views of the flat buffer)."""
+        out, o = [], 0
+        for shp in self.mlp_shapes:
+            k = int(np.prod(shp))
+            out.append(self.mlp[o:o + k].view(shp))
+            o += k
+        return out
+
+    def _work(self, masks, training):
+        nw = _lib.NCFWork(ptr(self.contrib), ptr(self.mlp_partials), ptr(self.scores_buf), ptr(self.dp_buf),
+                          None, None, 0, 1 if training else 0, 0)
+        if masks is not None:
+            mp, mn = masks
+            nw.mask_pos, nw.mask_neg = ptr(mp), ptr(mn)
+        nw.seed = (self.seed * 0x9E3779B97F4A7C15 + self.t) & 0xFFFFFFFFFFFFFFFF
+        return nw
+
+    def _loss(self, global_pos, out):
+        n = self.n_neg
+        if self.loss == "pointwise":
+            ia, ib = 1.0 / global_pos, 1.0 / (n * self.batch_size)
+        elif self.loss in ("bpr", "hinge"):
+            ia, ib = 1.0 / (n * global_pos), 0.0
+        else:
+            ia, ib = 1.0 / global_pos, 0.0
+        np_ = 1 if self.loss == "adaptive_hinge" else self.tiles
+        return _lib.MFLoss(np_, ia, ib, ptr(out))
+
+    def _forward_backward(self, batch, work, nw, stream):
+        if self.loss == "adaptive_hinge":
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 1), "rg_ncf_pairs(scores)")
+            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
+                  "rg_ncf_adapt_dp")
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 2), "rg_ncf_pairs(given dp)")
+        else:
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 0), "rg_ncf_pairs")
+
+    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None):
+        """One step; ``masks`` = (mask_pos [B, units] uint8, mask_neg [n*B, units] uint8) device
+        tensors recorded from the reference, or None for the device dropout RNG.  The loss
+        goes to ``loss_out`` (float32 device tensor) or the engine's own slot."""
+        n_pos = int(pos_u.numel())
+        global_pos = n_pos if global_pos is None else int(global_pos)
+        x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos, global_pos,
+                          None, None, None)
+        if plan is not None:
+            x.plan_perm, x.plan_pos_slot, x.plan_item_slot_off = ptr(plan.perm), ptr(plan.pos_slot), \
+                ptr(plan.item_slot_off)
+        stream = _lib.stream_handle()
+        batch, work = _lib.MFBatch(), _lib.MFWork()
+        check(self.lib.rg_mf_stepper_acquire(self._stepper, stream, ctypes.byref(x), ctypes.byref(batch),
+                                             ctypes.byref(work)), "rg_mf_stepper_acquire")
+        self.t += 1
+        nw = self._work(masks, True)
+        if self.kernel_events is not None:
+            self.kernel_events[0].record()
+        self._forward_backward(batch, work, nw, stream)
+        if self.kernel_events is not None:
+            self.kernel_events[1].record()
+        check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
+        o = self._opt(self.t)
+        parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials
+        out = self.loss_out if loss_out is None else loss_out
+        check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
+                                     ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
+              "rg_ncf_update")
+        check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
+                                    ctypes.byref(o), 0, -1), "rg_ncf_apply")
+        check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
+        return out
+
+    def _step_in(self, pos_u, pos_i, global_pos):
+        n_pos = int(pos_u.numel())
+        return _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos,
+                             n_pos if global_pos is None else int(global_pos), None, None, None)
+
+    def val_loss(self, pos_u, pos_i, global_pos=None):
+        """run_val_iteration (implicit.py:366-379): eval-mode forward (no dropout) and the
+        loss on the same negative stream; no update."""
+        x = self._step_in(pos_u, pos_i, global_pos)
+        stream = _lib.stream_handle()
+        batch, work = _lib.MFBatch(), _lib.MFWork()
+        check(self.lib.rg_mf_stepper_acquire(self._stepper, stream, ctypes.byref(x), ctypes.byref(batch),
+                                             ctypes.byref(work)), "rg_mf_stepper_acquire")
+        nw = self._work(None, False)
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        l = self._loss(x.global_pos, out)
+        if self.loss == "adaptive_hinge":
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 1), "rg_ncf_pairs(scores)")
+            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
+                  "rg_ncf_adapt_dp")
+            parts = self.adapt_partials
+        else:
+            check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
+                                        ctypes.byref(nw), 3), "rg_ncf_pairs(loss)")
+            parts = self.partials
+        check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
+        check(self.lib.rg_loss_finalize(stream, ptr(parts), l.n_partials, l.inv_a, l.inv_b, ptr(out)),
+              "rg_loss_finalize")
+        return out
+
+    def params(self):
+        """[user table, item table, MLP parameters...] (device tensors of the reference's shapes)."""
+        return [self.user_w, self.item_w] + self.mlp_params()
+
+    def set_params(self, tensors):
+        for dst, src in zip(self.params(), tensors):
+            dst.copy_(torch.as_tensor(src, dtype=torch.float32).reshape(dst.shape))
+
+    def scores(self, users, items):
+        """Eval-mode scores (no dropout) for (user, item) pairs, on the device."""
+        users = torch.as_tensor(users).to(self.device, torch.int64).reshape(-1)
+        items = torch.as_tensor(items).to(self.device, torch.int64).reshape(-1)
+        x = torch.cat([self.user_w[users], self.item_w[items]], 1)
+        ps = self.mlp_params()
+        for k in range(0, len(ps) - 2, 2):
+            z = x @ ps[k].T + ps[k + 1]
+            x = torch.where(z > 0, z, z * 0.1)
+        return torch.sigmoid(x @ ps[-2].T + ps[-1]).reshape(-1)
+
+    def mt_state(self):
+        host = np.zeros(625, dtype=np.uint32)
+        check(self.lib.rg_mf_stepper_sync_mt(self._stepper, host.ctypes.data_as(ctypes.c_void_p), 0),
+              "rg_mf_stepper_sync_mt")
+        return host
+
+    def set_mt_state(self, st):
+        host = np.ascontiguousarray(np.asarray(st, dtype=np.uint32))
+        check(self.lib.rg_mf_stepper_sync_mt(self._stepper, host.ctypes.data_as(ctypes.c_void_p), 1),
+              "rg_mf_stepper_sync_mt")

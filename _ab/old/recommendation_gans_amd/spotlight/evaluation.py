@@ -1,0 +1,143 @@
+"""Ranking metrics of spotlight/evaluation.py (reference :115-353).
+
+Same definitions as the reference: per test user with at least one test item,
+rank all items by -score (``argsort``), precision/recall@k over the top k,
+average precision@k, hit ratio; popularity and random baselines.  The scores of a
+block of users against every item come from one GEMM on the device
+(``model.score_users``) instead of one ``predict`` call per user."""
+import numpy as np
+
+FLOAT_MAX = np.finfo(np.float32).max
+
+
+def _get_precision_recall(predictions, targets, k):
+    predictions = predictions[:k]
+    num_hit = len(set(predictions).intersection(set(targets)))
+    return float(num_hit) / k, float(num_hit) / len(targets)
+
+
+def _ranked(model, test_csr, train_csr=None, block=4096):
+    """Yields (user, row indices, item ranking) for every test user with items."""
+    users = np.flatnonzero(np.diff(test_csr.indptr) > 0)
+    for s in range(0, len(users), block):
+        ub = users[s:s + block]
+        scores = -model.score_users(ub)                      # (len(ub), I) float32, host
+        for r, u in enumerate(ub):
+            pred = scores[r]
+            if train_csr is not None:
+                pred[train_csr[u].indices] = FLOAT_MAX
+            yield u, test_csr[u].indices, pred.argsort(axis=0)
+
+
+def precision_recall_score(model, test, train=None, k=10):
+    test_csr = test.tocsr()
+    train_csr = train.tocsr() if train is not None else None
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    precision, recall = [], []
+    cold = 0
+    for u, targets, ranking in _ranked(model, test_csr, train_csr):
+        if train_csr is not None and not len(train_csr[u].indices):
+            cold += 1
+        p, r = zip(*[_get_precision_recall(ranking, targets, x) for x in ks])
+        precision.append(p)
+        recall.append(r)
+    print("Cold start users: ", cold)
+    return np.mean(np.array(precision).squeeze()), np.mean(np.array(recall).squeeze())
+
+
+def rmse_score(net, user_ids, item_ids):
+    predictions = net(user_ids, item_ids)
+    array = 1 - predictions.cpu().detach().numpy()
+    return np.sum(array ** 2)
+
+
+def hit_ratio(model, test, k=10):
+    hits = users = 0
+    for _, target, ranking in _ranked(model, test.tocsr()):
+        users += 1
+        if target in ranking[:k]:
+            hits += 1
+    return hits / users
+
+
+def apk(actual, predicted, k=10):
+    if len(predicted) > k:
+        predicted = predicted[:k]
+    score, num_hits = 0.0, 0.0
+    for i, p in enumerate(predicted):
+        if p in actual and p not in predicted[:i]:
+            num_hits += 1.0
+            score += num_hits / (i + 1.0)
+    if not actual.any():
+        return 0.0
+    return score / min(len(actual), k)
+
+
+def mapk(actual, predicted, k=10):
+    return np.mean([apk(a, p, k) for a, p in zip(actual, predicted)])
+
+
+def map_at_k(model, test, k=5):
+    vals = [apk(targets, ranking, k=k) for _, targets, ranking in _ranked(model, test.tocsr())]
+    return np.mean(np.array(vals).squeeze())
+
+
+def evaluate_popItems(item_popularity, test, k=10):
+    test = test.tocsr()
+    pop = np.asarray(getattr(item_popularity, "values", item_popularity))
+    pop_top = pop.argsort()[::-1][:k]
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    precision, recall = [], []
+    for row in test:
+        if not len(row.indices):
+            continue
+        p, r = zip(*[_get_precision_recall(pop_top, row.indices, x) for x in ks])
+        precision.append(p)
+        recall.append(r)
+    return np.mean(precision), np.mean(recall),
+
+
+def evaluate_random(item_popularity, test, k=10):
+    all_items = test.num_items
+    test = test.tocsr()
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    precision, recall = [], []
+    for row in test:
+        if not len(row.indices):
+            continue
+        predictions = np.random.choice(all_items, len(row.indices))
+        p, r = zip(*[_get_precision_recall(predictions, row.indices, x) for x in ks])
+        precision.append(p)
+        recall.append(r)
+    return np.mean(np.array(precision).squeeze()), np.mean(np.array(recall).squeeze())
+
+
+def precision_recall_score_slates(slates, test, k=3):
+    """spotlight/evaluation.py:355-382: precision / recall@k of each test user's
+    generated slate (row u of ``slates`` belongs to row u of the CSR ``test``)."""
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    test = test.tocsr()
+    precision, recall = [], []
+    for user_id in range(test.shape[0]):
+        targets = test.indices[test.indptr[user_id]:test.indptr[user_id + 1]]
+        if not len(targets):
+            continue
+        pred = slates[user_id].numpy() if hasattr(slates[user_id], "numpy") else np.asarray(slates[user_id])
+        p, r = zip(*[_get_precision_recall(pred, targets, x) for x in ks])
+        precision.append(p[0])
+        recall.append(r[0])
+    return precision, recall
+
+
+def precision_recall_slates_atk(fake_slates, real_slates, k=3):
+    """spotlight/evaluation.py:394-412, the generator's training precision / recall.
+    The reference intersects sets of 0-d torch tensors (rows of the two slate
+    tensors), which hash by identity, so every user scores 0; the same operations on
+    the same tensor types are kept here so summary.csv matches the reference."""
+    ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    precision, recall = [], []
+    for user_id in range(fake_slates.shape[0]):
+        p, r = zip(*[_get_precision_recall(fake_slates[user_id, :], real_slates[user_id, :], x) for x in ks])
+        precision.append(p[0])
+        recall.append(r[0])
+    return precision, recall

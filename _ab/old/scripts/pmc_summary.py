@@ -3,9 +3,8 @@
 bytes/launch = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE, averaged over launches:
 FETCH_SIZE/WRITE_SIZE are in KiB, and on gfx950 FETCH_SIZE counts exactly half of
 the bytes of wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md, HBM).
-Writes profiles/pmc_step.json (overlapped step: front + hot kernels) or
-profiles/pmc_apply.json (split step: rg_mf_apply) when --write is given; bench.py
-reads it as roofline.traffic."""
+Writes profiles/pmc_apply.json when --write is given (bench.py reads it as
+roofline.traffic for rg_mf_apply)."""
 import csv
 import glob
 import json
@@ -27,8 +26,7 @@ def per_kernel(path):
 
 
 def short(name):
-    for key in ("mf_apply_kernel", "mf_pairs_kernel", "mt_generate_kernel", "mf_prepare_kernel", "mf_front_kernel",
-                "mf_hot_kernel", "mt_head_kernel", "mt_jump_kernel", "mt_tail_kernel", "mf_back_kernel"):
+    for key in ("mf_apply_kernel", "mf_pairs_kernel", "mt_generate_kernel", "mf_prepare_kernel"):
         if key in name:
             return key
     return None
@@ -52,20 +50,12 @@ def main():
     res = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --steps 20",
            "dim": cfg.get("config", {}).get("embedding_dim"), "batch": cfg.get("config", {}).get("global_batch"),
            "kernels": out}
-    name = "pmc_apply.json"
     if "mf_apply_kernel" in out:
         res["hbm_bytes_per_launch"] = out["mf_apply_kernel"]["hbm_bytes_per_launch"]
-    if "mf_back_kernel" in out:       # split step: rg_mf_apply_prepare
-        res["hbm_bytes_per_launch"] = out["mf_back_kernel"]["hbm_bytes_per_launch"]
-        name = "pmc_back.json"
-    if "mf_front_kernel" in out and "mf_hot_kernel" in out:     # overlapped step: one of each per step
-        res["hbm_bytes_per_step"] = (out["mf_front_kernel"]["hbm_bytes_per_launch"] +
-                                     out["mf_hot_kernel"]["hbm_bytes_per_launch"])
-        name = "pmc_step.json"
     print(json.dumps(res, indent=1))
     if "--write" in sys.argv:
         json.dump(res, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
-                                         name), "w"), indent=1)
+                                         "pmc_apply.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

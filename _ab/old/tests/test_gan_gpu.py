@@ -1,0 +1,228 @@
+"""cGAN on the GPU (rg_gemm.hip, rg_gan.hip through the C-ABI).
+
+* the fp32 MFMA GEMM against a float64 product of the same fp32 operands, every
+  operand layout, split-K, ragged edges and the tanh epilogue (tolerance: 2e-6 of
+  sum |a b| per element, the f32 fma-chain bound at these K);
+* the discriminator / generator iterations against the reference's own steps
+  (tests/golden/gan_*.npz, recorded z and dropout masks fed in): D outputs, G(z),
+  losses, BatchNorm running stats, inference slates, and every parameter after
+  every step with the criterion of tests/test_gan_oracle.param_ok (1e-5 relative,
+  elements whose float64 gradient cancels to noise excepted);
+* generation through the fused argmax epilogue (heads wider than a column tile)
+  against the eval-mode forward of the float64 restatement;
+* the device dropout / noise path trains and is reproducible."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gan as og
+from tests.test_gan_oracle import key, load, param_ok
+
+pytestmark = pytest.mark.gpu
+
+
+def gemm(A, B, a_km, b_km, M, N, K, post=0, splits=1, bias=None, ldc=None):
+    from recommendation_gans_amd import _lib
+    from recommendation_gans_amd.gan_engine import ptr
+    import ctypes
+    L = _lib.load()
+    ldc = ldc or N
+    C = torch.zeros(M, ldc, device="cuda")
+    work = torch.zeros(max(1, splits) * M * N, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = L.rg_gemm_f32(st, ptr(A), A.shape[1], int(a_km), ptr(B), B.shape[1], int(b_km), M, N, K, ptr(C), ldc,
+                       ptr(bias), post, splits, ptr(work))
+    _lib.check(rc, "rg_gemm_f32")
+    torch.cuda.synchronize()
+    return C[:, :N].cpu()
+
+
+@pytest.mark.parametrize("a_km,b_km", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,splits", [(256, 512, 1000, 1), (250, 130, 64, 1), (64, 256, 2048, 7),
+                                          (300, 40, 36, 3)])
+def test_gemm_matches_float64(a_km, b_km, M, N, K, splits):
+    if (a_km or b_km) and K % 4:
+        pytest.skip("K-major operands need K % 4 == 0")
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(N, K, generator=g)
+    m4, n4 = (M + 3) // 4 * 4, (N + 3) // 4 * 4
+    A = (a if a_km else torch.cat([a.t(), torch.zeros(K, m4 - M)], 1)).contiguous().cuda()
+    B = (b if b_km else torch.cat([b.t(), torch.zeros(K, n4 - N)], 1)).contiguous().cuda()
+    got = gemm(A, B, a_km, b_km, M, N, K, splits=splits)
+    ref = a.double() @ b.double().t()
+    bound = 2e-6 * (a.double().abs() @ b.double().abs().t()) + 1e-30
+    assert ((got.double() - ref).abs() <= bound).all()
+
+
+def test_gemm_bias_tanh():
+    g = torch.Generator().manual_seed(3)
+    a, b, bias = torch.randn(200, 64, generator=g) * 0.2, torch.randn(300, 64, generator=g) * 0.2, torch.randn(300)
+    got = gemm(a.cuda(), b.cuda(), True, True, 200, 300, 64, post=1, bias=bias.cuda(), ldc=304)
+    ref = torch.tanh(a.double() @ b.double().t() + bias.double())
+    assert (got.double() - ref).abs().max() < 2e-6
+
+
+CASES = ["gan_rms_n50", "gan_adam_n50", "gan_sgd_n64"]
+
+
+def make_engine(z, gp, gb, dn, g_init, d_init, dims, opt, lr):
+    from recommendation_gans_amd.gan_engine import GANEngine
+    N, S, H, E, B, L, Z, nb, dsteps = dims
+    g_sd = {k: torch.from_numpy(np.asarray(v).copy()) for k, v in g_init.items()}
+    d_sd = {k: torch.from_numpy(np.asarray(v).copy()) for k, v in d_init.items()}
+    return GANEngine(g_sd, d_sd, N, S, H, E, Z, batch_max=B, optimizer=opt, lr=lr)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_gan_steps_match_reference(golden_dir, case):
+    from recommendation_gans_amd.gan_engine import GANBatch
+    z, dims, gp, gb, dn, g_init, d_init = load(golden_dir, case)
+    N, S, H, E, B, L, Z, nb, dsteps = dims
+    lr, opt = float(z["lr"][0]), case.split("_")[1]
+    eng = make_engine(z, gp, gb, dn, g_init, d_init, dims, opt, lr)
+    o = og.GANOracle(g_init, d_init, N, S, H, E, Z, opt=opt, lr=lr)
+    scales = tuple(float(x) for x in z["drop_scale"])
+    gat = int(z["g_step_at"][0])
+    ill = {}
+    for k in range(dsteps):
+        b = int(z[f"d{k}_batch"][0])
+        hist, sl = z["hist"][b * B:(b + 1) * B], z["slates"][b * B:(b + 1) * B]
+        batch = GANBatch(hist, sl, N, S, "cuda")
+        masks = [z[f"d{k}_mask{j}"] for j in range(8)]
+        out = eng.d_step(batch, z=torch.from_numpy(z[f"d{k}_z"]), masks=masks).cpu().numpy()
+        o.d_step(hist, sl, z[f"d{k}_z"].astype(np.float64), [m.astype(np.float64) for m in masks], scales)
+        dval = eng.last_d_out(2 * B).cpu().numpy()
+        np.testing.assert_allclose(dval[:B], z[f"d{k}_d_real"].ravel(), rtol=1e-5, err_msg=f"{case} D{k} real")
+        np.testing.assert_allclose(dval[B:], z[f"d{k}_d_fake"].ravel(), rtol=1e-5, err_msg=f"{case} D{k} fake")
+        np.testing.assert_allclose(eng.last_fake(B).cpu().numpy(), z[f"d{k}_fake"], rtol=1e-4, atol=1e-5)
+        assert abs(out[0] - z[f"d{k}_loss"][0]) <= 1e-5 * abs(z[f"d{k}_d_real"]).mean()
+        dsd = eng.d_state_dict()
+        for n in dn:
+            ok, msg = param_ok(dsd[n].numpy(), z[key(f"d{k}_after_D_", n)], o.last_grads[n], lr,
+                               prior=ill.setdefault("D" + n, np.zeros(o.D[n].shape, bool)))
+            assert ok, f"{case} D{k} {n}: {msg}"
+        gsd = eng.g_state_dict()
+        for n in gb:
+            np.testing.assert_allclose(gsd[n].numpy(), z[key(f"d{k}_after_G_", n)], rtol=1e-5, atol=1e-7,
+                                       err_msg=f"{case} D{k} {n}")
+        if k == gat:
+            masks = [z[f"g{k}_mask{j}"] for j in range(5)]
+            gl, slates = eng.g_step(batch, z=torch.from_numpy(z[f"g{k}_z"]), masks=masks)
+            o.g_step(hist, z[f"g{k}_z"].astype(np.float64), [m.astype(np.float64) for m in masks], scales)
+            np.testing.assert_allclose(float(gl[0]), z[f"g{k}_loss"][0], rtol=1e-5)
+            np.testing.assert_allclose(eng.last_d_out(B).cpu().numpy(), z[f"g{k}_d_fake"].ravel(), rtol=1e-5)
+            assert (slates.cpu().numpy() == z[f"g{k}_slates_after"]).all()
+            gsd = eng.g_state_dict()
+            for n in gp:
+                ok, msg = param_ok(gsd[n].numpy(), z[key(f"g{k}_after_G_", n)], o.last_grads[n], lr,
+                                   exempt=n in o.pre_bn_biases(),
+                                   prior=ill.setdefault("G" + n, np.zeros(o.G[n].shape, bool)))
+                assert ok, f"{case} G{k} {n}: {msg}"
+            for n in gb:
+                np.testing.assert_allclose(gsd[n].numpy(), z[key(f"g{k}_after_G_", n)], rtol=1e-5, atol=1e-7)
+
+
+def test_gan_reference_init_clamp(golden_dir):
+    """The reference's own D init (clamp-bound): step-0 forward values and that the
+    step started from the clamped weights."""
+    from recommendation_gans_amd.gan_engine import GANBatch
+    z, dims, gp, gb, dn, g_init, d_init = load(golden_dir, "gan_rms_refinit")
+    N, S, H, E, B, L, Z, nb, dsteps = dims
+    lr = float(z["lr"][0])
+    eng = make_engine(z, gp, gb, dn, g_init, d_init, dims, "rms", lr)
+    batch = GANBatch(z["hist"][:B], z["slates"][:B], N, S, "cuda")
+    eng.d_step(batch, z=torch.from_numpy(z["d0_z"]), masks=[z[f"d0_mask{j}"] for j in range(8)])
+    dval = eng.last_d_out(2 * B).cpu().numpy()
+    np.testing.assert_allclose(dval[:B], z["d0_d_real"].ravel(), rtol=1e-5)
+    np.testing.assert_allclose(dval[B:], z["d0_d_fake"].ravel(), rtol=1e-5)
+    dsd = eng.d_state_dict()
+    for n in dn:
+        before = np.clip(d_init[n], -og.CLAMP, og.CLAMP)
+        assert np.abs(dsd[n].numpy() - before).max() <= 10 * lr * (1 + 1e-5), n
+
+
+def random_gan(N, S, H, E, Z, seed):
+    """Reference-shaped G / D state dicts (cGAN_models.py init: xavier weights, bias 0.01,
+    N(0,1) embeddings with a zero padding row, BatchNorm gamma 1 / beta 0)."""
+    g = torch.Generator().manual_seed(seed)
+    H1 = H // 2
+
+    def lin(o, i):
+        b = (6.0 / (i + o)) ** 0.5
+        return (torch.rand(o, i, generator=g) * 2 - 1) * b, torch.full((o,), 0.01)
+
+    def emb():
+        e = torch.randn(N + 1, E, generator=g)
+        e[N] = 0
+        return e
+
+    gs = {"embedding_layer.weight": emb()}
+    for pre, (o, i) in (("layers.0", (H1, Z + E)), ("layers.4", (H, H1))):
+        gs[pre + ".weight"], gs[pre + ".bias"] = lin(o, i)
+    for pre, w in (("layers.1", H1), ("layers.5", H)):
+        gs.update({pre + ".weight": torch.ones(w), pre + ".bias": torch.zeros(w), pre + ".running_mean": torch.zeros(w),
+                   pre + ".running_var": torch.ones(w), pre + ".num_batches_tracked": torch.tensor(0)})
+    for s in range(S):
+        gs[f"mult_heads.head_{s}.weight"], gs[f"mult_heads.head_{s}.bias"] = lin(N, H)
+    ds = {"embedding_layer.weight": emb()}
+    for pre, (o, i) in (("layers.0", (2 * H, S * N + E)), ("layers.3", (H, 2 * H)), ("layers.6", (H1, H)),
+                        ("layers.9", (1, H1))):
+        ds[pre + ".weight"], ds[pre + ".bias"] = lin(o, i)
+    return gs, ds
+
+
+def hist_and_slates(rs, rows, N, S, L):
+    hist = np.full((rows, L), N, np.int64)
+    for r in range(rows):
+        ln = rs.randint(0, L + 1)
+        hist[r, :ln] = rs.choice(N, ln, replace=False)
+    slates = np.stack([rs.choice(N, S, replace=False) for _ in range(rows)])
+    return hist, slates
+
+
+def test_gan_generate_fused_argmax():
+    """Heads of N = 300 > one column tile: the fused argmax epilogue (tiles straddling two
+    heads) against the float64 eval-mode forward; a near-tie may pick either item, so the
+    chosen item's tanh must be the maximum to 1e-5."""
+    from recommendation_gans_amd.gan_engine import GANBatch, GANEngine
+    N, S, H, E, Z, B, L = 300, 5, 32, 5, 100, 64, 12
+    gs, ds = random_gan(N, S, H, E, Z, 5)
+    gs["layers.1.running_mean"].uniform_(-0.1, 0.1)
+    gs["layers.5.running_var"].uniform_(0.5, 2.0)
+    eng = GANEngine(gs, ds, N, S, H, E, Z, batch_max=B)
+    rs = np.random.RandomState(1)
+    hist, _ = hist_and_slates(rs, B, N, S, L)
+    zz = torch.rand(B, Z, generator=torch.Generator().manual_seed(2))
+    got = eng.generate(GANBatch(hist, None, N, S, "cuda"), z=zz).cpu().numpy().astype(np.int64)
+    o = og.GANOracle({k: v.numpy() for k, v in gs.items()}, {k: v.numpy() for k, v in ds.items()}, N, S, H, E, Z)
+    heads, _ = o.g_forward(zz.double().numpy(), hist.astype(np.float64), train=False)
+    for s in range(S):
+        t = heads[s]
+        chosen = t[np.arange(B), got[:, s]]
+        assert (chosen >= t.max(1) - 1e-5).all()
+
+
+def test_gan_device_noise_trains():
+    """torch.rand z and the hash dropout: finite losses, reproducible for a seed, and the
+    generator's loss responds to training."""
+    from recommendation_gans_amd.gan_engine import GANBatch, GANEngine
+    N, S, H, E, Z, B, L = 200, 5, 64, 5, 100, 128, 20
+    gs, ds = random_gan(N, S, H, E, Z, 9)
+    rs = np.random.RandomState(4)
+    hist, slates = hist_and_slates(rs, B, N, S, L)
+    runs = []
+    for rep in range(2):
+        eng = GANEngine(gs, ds, N, S, H, E, Z, batch_max=B, seed=3)
+        batch = GANBatch(hist, slates, N, S, "cuda")
+        torch.manual_seed(11)
+        losses = []
+        for k in range(10):
+            losses.append(eng.d_step(batch).cpu().numpy())
+            if (k + 1) % 5 == 0:
+                losses.append(eng.g_step(batch)[0].cpu().numpy())
+        runs.append(np.concatenate(losses))
+        assert np.isfinite(runs[-1]).all()
+    np.testing.assert_array_equal(runs[0], runs[1])

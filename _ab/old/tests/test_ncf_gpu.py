@@ -1,0 +1,88 @@
+"""NCF MLP step on the GPU (rg_ncf.hip through the C-ABI) against the reference's
+own NCF steps (tests/golden/mlp_*.npz, dropout masks recorded from the reference
+and fed to the kernel): loss, MT stream, and every parameter after each Adam
+step (tensor parity vs the fp32 reference; small tensors vs the fp64 restatement
+as in oracle.mf.tensor_parity)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mf as omf
+from oracle import ncf as oncf
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["mlp_pointwise_e16", "mlp_pointwise_e64", "mlp_adaptive_hinge_e16", "mlp_bpr_e16"]
+
+
+def masks_for(z, s, nl, B, n, dev):
+    def cat(kind, rows):
+        m = np.concatenate([z[f"s{s}_mask_{kind}{k}"] for k in range(nl)], axis=1)
+        out = np.zeros((rows, m.shape[1]), np.uint8)
+        out[:m.shape[0]] = m
+        return torch.from_numpy(out).to(dev).contiguous()
+    return cat("pos", B), cat("neg", n * B)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_ncf_steps_match_reference(golden_dir, case):
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    dev = torch.device("cuda:0")
+    z = np.load(os.path.join(golden_dir, case + ".npz"))
+    names = [str(x) for x in z["param_names"]]
+    init = [torch.from_numpy(z["init_" + nm.replace(".", "_")].copy()) for nm in names]
+    U, I, E, B, n = (int(x) for x in z["meta"])
+    loss = case.split("_e")[0][len("mlp_"):]
+    nl = len(z["layers"]) - 1
+    e = NCFEngine(init[0], init[1], init[2:], z["pool_u"], z["pool_i"], z["s0_mt_state"].copy(), loss=loss,
+                  optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev)
+    o64 = oncf.NCFOracle([t.double() for t in init], names, z["pool_u"], z["pool_i"], z["s0_mt_state"].copy(),
+                         loss=loss, lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B)
+    for s in range(3):
+        pu = torch.from_numpy(z[f"s{s}_pos_u"]).to(dev)
+        pi = torch.from_numpy(z[f"s{s}_pos_i"]).to(dev)
+        masks = masks_for(z, s, nl, B, n, dev)
+        got = e.train_step(pu, pi, masks=masks)
+        mp = [torch.from_numpy(z[f"s{s}_mask_pos{k}"]) for k in range(nl)]
+        mn = [torch.from_numpy(z[f"s{s}_mask_neg{k}"]) for k in range(nl)]
+        o64.step(z[f"s{s}_pos_u"], z[f"s{s}_pos_i"], mp, mn)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(float(got[0]), float(z[f"s{s}_loss"][0]), rtol=1e-5, err_msg=f"{case} loss {s}")
+        assert (e.mt_state() == (z[f"s{s + 1}_mt_state"] if s < 2 else z["end_mt_state"])).all(), f"{case} MT {s}"
+        params = [e.user_w, e.item_w] + e.mlp_params()
+        for nm, p, r64 in zip(names, params, o64.P.t):
+            ref = torch.from_numpy(z[f"s{s}_after_" + nm.replace(".", "_")])
+            ok, msg = omf.tensor_parity(p.reshape(ref.shape), ref, r64.reshape(ref.shape))
+            assert ok, f"{case} step {s} {nm}: {msg}"
+    assert int(e.row_count.abs().sum()) == 0 and float(e.hot_grad.abs().sum()) == 0.0
+
+
+def test_ncf_device_dropout_trains():
+    """Device dropout RNG: reproducible for a seed (to float-atomic order: these tiny tables
+    overflow the per-row lists, whose overflow path adds with atomics), and a fixed
+    batch's loss falls."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from oracle import rng as orng
+    dev = torch.device("cuda:0")
+    U, I, E, B, n = 400, 300, 64, 512, 5
+    torch.manual_seed(0)
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E), torch.randn(I, E)]
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+        w = torch.empty(b_, a_)
+        torch.nn.init.xavier_uniform_(w)
+        params += [w, torch.full((b_,), 0.01)]
+    rs = np.random.RandomState(0)
+    pool_u, pool_i = rs.randint(0, U, 5000), rs.randint(0, I, 5000)
+    pu, pi = torch.from_numpy(rs.randint(0, U, B)).to(dev), torch.from_numpy(rs.randint(0, I, B)).to(dev)
+    losses = []
+    for rep in range(2):
+        e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, orng.py_seed_state(0), loss="pointwise",
+                      lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=7)
+        ls = [float(e.train_step(pu, pi, plan=e.make_plan(pi))[0]) for _ in range(6)]
+        losses.append(ls)
+        assert all(np.isfinite(ls))
+    np.testing.assert_allclose(losses[0], losses[1], rtol=1e-6)
+    assert losses[0][-1] < losses[0][0]

@@ -15,17 +15,18 @@
 // consumed units is the start state of their slot advanced by the units consumed
 // inside it (rg_mf_stepper_sync_mt).
 //
-// Overlapped step (default; pointwise / bpr / hinge):
+// Overlapped step (RG_FUSED=1; pointwise / bpr / hinge; measured slower):
 //   main  rg_mf_step_front(pairs of t | marked prepare of t+1 | cold-row update of t)
 //         -> rg_mf_step_hot(touched rows of t, loss)
 // Two launches per step on one stream and no per-step event: the prepare of the
 // next step rides in the front grid, so the only cross-stream dependency left is
 // one wait per ring slot for the generated words.
 //
-// Split step (adaptive hinge, RG_FUSED=0, and the external consumers that go
-// through acquire / release: validation, NCF, the Python split DP steps):
-//   prep  rg_mf_prepare of the next unit (after the current pairs kernel)
-//   main  rg_mf_pairs -> rg_mf_apply (-> exchange)
+// Split step (the default; adaptive hinge always):
+//   main  rg_mf_pairs -> rg_mf_apply_prepare (dense update + the NEXT step's prepare in
+//         one launch) (-> exchange): no side stream, no per-step event
+// External consumers (validation, NCF, the Python split DP steps) go through
+// acquire / release, which prepare on a side stream ordered after the caller's work.
 //
 // Device memory: the caller (PyTorch) owns tables, scratch, pool and pairs; the
 // stepper owns its word ring, the per-slot start states, the row stamps of the
@@ -71,7 +72,7 @@ struct Stepper {
     int32_t serial = 0;                   // last mark serial issued
     int32_t *stamp[2] = {nullptr, nullptr};   // [U + I] each, lazily allocated
     int set = 0;                          // ping-pong set holding the current tables
-    bool fused = true;
+    bool fused = false;
     bool hot_scan = true;
     // MT jump-ahead path: the device state is in window form after a jump slot;
     // cp_pos tracks CPython's position-in-block of the same stream point
@@ -299,15 +300,44 @@ int record(void *ev, hipStream_t s) {
     return e == hipSuccess ? RG_OK : hip_fail("stepper: record event", e);
 }
 
-// the update half of a step after the pair pass: user-sharded DP exchange or loss
-int finish_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, rg_mf_work_t &w, float *loss_out,
-                 void *ev0, void *ev1) {
+// Split step: [marked-free prepare if not prefetched] -> rg_mf_pairs -> rg_mf_apply_prepare
+// (the dense update plus the NEXT step's prepare in one launch), all on the caller's
+// stream: no side stream, no per-step event; the words of a ring slot are waited for
+// once per slot.  User-sharded DP: item gradient -> all-reduce (communicator stream)
+// beside the user-shard update (+ next prepare) -> item update.
+int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+                float *loss_out, void *ev0, void *ev1) {
+    const int64_t unit = st.taken;
+    int rc = keep_ahead(st, unit);
+    if (rc) return rc;
+    rg_mf_work_t w = work_for(st, cur);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if ((rc = wait_side(st, s, (int)(unit % 2)))) return rc;      // a side prepare (acquire path) of this buffer
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
+        if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+        st.prepared = true;
+        st.prep_unit = unit;
+        st.prep_in = cur;
+        st.prep_serial = 0;
+    }
+    if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = wait_words(st, s, unit))) return rc;   // adapt-max reads them
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) return rc;
+    if ((rc = release(st, s))) return rc;
+    rg_mf_batch_t nbatch{};
+    rg_mf_work_t nw{};
+    if (next) {
+        if ((rc = keep_ahead(st, unit + 1))) return rc;
+        if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        nbatch = make_batch(st, *next, unit + 1);
+        nw = work_for(st, *next);
+    }
     st.cfg.step += 1;
     const rg_opt_t o = opt_at(st, st.cfg.step);
     const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
-    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     const int64_t U = tb->num_users, R = tb->num_users + tb->num_items;
-    int rc;
     if (st.cfg.item_grad) {                     // user-sharded data parallel
         if ((rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l))) return rc;
         if (st.cfg.comm && (rc = rg::comm_begin(st.cfg.comm, s, st.cfg.item_grad,
@@ -315,27 +345,20 @@ int finish_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, rg_mf_w
             return rc;
     }
     if ((rc = record(ev0, s))) return rc;
-    if ((rc = st.cfg.item_grad ? rg_mf_apply(s, tb, &w, &o, 0, U, nullptr) : rg_mf_apply(s, tb, &w, &o, 0, -1, &l)))
+    if ((rc = rg_mf_apply_prepare(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
+                                  next ? &nbatch : nullptr, next ? &nw : nullptr)))
         return rc;
     if ((rc = record(ev1, s))) return rc;
     if (st.cfg.item_grad) {
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
         if ((rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out))) return rc;
     }
-    return RG_OK;
-}
-
-int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
-                float *loss_out, void *ev0, void *ev1) {
-    int64_t unit;
-    int rc = acquire(st, s, cur, &unit);
-    if (rc) return rc;
-    rg_mf_work_t w = work_for(st, cur);
-    const rg_mf_batch_t batch = make_batch(st, cur, unit);
-    if ((rc = rg_mf_pairs(s, &st.cfg.tables[st.set], &batch, &w, 1))) return rc;
-    if ((rc = release(st, s))) return rc;
-    if (next && (rc = prepare_side(st, s, unit + 1, *next))) return rc;
-    if ((rc = finish_split(st, s, cur, w, loss_out, ev0, ev1))) return rc;
+    if (next) {
+        st.prepared = true;
+        st.prep_unit = unit + 1;
+        st.prep_in = *next;
+        st.prep_serial = 0;
+    }
     st.set = 1 - st.set;
     return RG_OK;
 }
@@ -449,7 +472,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     if (st->cfg.neg_cols <= 0) st->cfg.neg_cols = cfg->global_cols;
     {
         const char *g = getenv("RG_MT_UNITS");
-        st->G = g ? atoi(g) : 4;
+        st->G = g ? atoi(g) : 8;
         if (st->G < 1) st->G = 1;
         if (st->G > 64) st->G = 64;
     }
