@@ -9,9 +9,9 @@ GPU (weak scaling), each with n = 5 negatives drawn bit-exactly from the CPython
 MT19937 stream, the BPR loss on the neg.view(n, B) pairing, backward, and a dense
 coupled-L2 Adam update of every row of the four BilinearNet tables (the
 reference's semantics: implicit.py:347-364, spotlight/optimizers.py:10-16).
-The native stepper runs it as two launches (rg_mf_step_front: pair pass | next
-step's prepare | update of the rows the batch does not touch; rg_mf_step_hot:
-update of the touched rows); RG_FUSED=0 selects the split pairs -> apply step.
+The native stepper runs it as rg_mf_pairs -> rg_mf_apply_prepare (the dense
+update and the next step's prepare in one launch); RG_FUSED=1 selects the
+overlapped two-launch step (rg_mf_step_front + rg_mf_step_hot, measured slower).
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
 With N > 1 ranks (one process per GPU) the step is user-sharded
@@ -21,9 +21,9 @@ replicated and their gradient is all-reduced with RCCL inside the native step,
 overlapped with the user-shard update.
 
 Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
-max over ranks of the timed wall time.  `roofline` is for the step's two kernels
-(front + hot: every algorithmic byte of the step), timed with HIP events on the
-stream they are launched on; `cpu_baseline` times the CPU restatement (oracle/, the
+max over ranks of the timed wall time.  `roofline` is for the dominant kernel
+(rg_mf_apply_prepare: the dense optimizer pass + the next step's prepare), timed
+with HIP events on the stream it is launched on; `cpu_baseline` times the CPU restatement (oracle/, the
 reference's algorithm incl. its random.choices sampler) on a bounded sample.
 """
 import argparse

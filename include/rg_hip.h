@@ -82,8 +82,9 @@ typedef struct rg_mf_tables {
  * and negative slot j / global_cols (the reference's flat draw order viewed as
  * (n, B) -- SURVEY §0.1); this rank owns columns [col_offset, col_offset + cols).
  * rg_mf_prepare fills `pairs` with the (user, item) ids of every pair in
- * processing order (position s = column, or plan_perm[s] with a plan): row 0 the
- * positives, row 1 + k negative slot k.  rg_mf_pairs reads only `pairs` (plus
+ * processing order (position s = column, or plan_perm[s] with a plan), one record
+ * per position (rg_mf_pairs_len): entry 0 the positive, 1 + k negative slot k,
+ * n_neg + 1 the positive's plan slot.  rg_mf_pairs reads only `pairs` (plus
  * words/pool for the adaptive hinge's max). */
 typedef struct rg_mf_batch {
     const int64_t *pos_user, *pos_item;  /* [n_pos] this rank's positives (column order) */
@@ -98,7 +99,7 @@ typedef struct rg_mf_batch {
     int64_t pool_len;
     int32_t n_neg;          /* negatives per positive, 1..RG_MF_MAX_NEG */
     int32_t loss;           /* enum rg_loss_kind */
-    int32_t *pairs;         /* [(1 + n_neg) * cols * 2] int32 (user, item), see above */
+    int32_t *pairs;         /* [rg_mf_pairs_len(cols, n_neg)] int32, see above */
 } rg_mf_batch_t;
 
 /* Caller-owned scratch.  row_count, hot_grad and hot_bias_grad must be zero
@@ -170,6 +171,11 @@ int rg_mt_window_to_cpython(const uint32_t *window_host, int32_t pos, uint32_t *
 /* Advance a CPython getstate() layout state (625 words, host memory) by k raw words
  * in place, as k calls of getrandbits(32) would. */
 int rg_mt_advance_host(uint32_t *state_host, int64_t k);
+
+/* int32 elements of a prepared-pairs buffer: one record of S int2 per column (S = 8
+ * for n_neg <= 6, else 16): [q] = (user, item) of pair q (0 = the positive, 1 + k =
+ * negative k), [n_neg + 1] = (the positive's plan slot or -1, 0), zero padding. */
+int64_t rg_mf_pairs_len(int64_t cols, int32_t n_neg);
 
 /* Number of float loss partials rg_mf_pairs writes for `cols` columns. */
 int64_t rg_mf_partials_len(int64_t cols, int32_t dim);

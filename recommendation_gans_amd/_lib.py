@@ -179,6 +179,7 @@ SIGNATURES = [
                                       ctypes.c_void_p]),
     ("rg_mf_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     ("rg_mf_plan_units_per_block", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_mf_pairs_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     ("rg_mf_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
     ("rg_mf_prepare_marked", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
                                             ctypes.POINTER(MFMark)]),

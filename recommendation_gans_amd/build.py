@@ -44,14 +44,20 @@ def up_to_date():
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build(force=False, verbose=False, jobs=8):
-    if not force and up_to_date():
+DIAG_LIB = os.path.join(PKG, "librg_hip_diag.so")
+
+
+def build(force=False, verbose=False, jobs=8, diag=False):
+    """diag=True: librg_hip_diag.so with the RG_DIAG_STAMPS phase stamps (scripts only;
+    the product never loads it)."""
+    lib = DIAG_LIB if diag else LIB
+    if not force and not diag and up_to_date():
         return LIB
     hipcc = _hipcc()
-    objdir = os.path.join(PKG, "_obj")
+    objdir = os.path.join(PKG, "_obj_diag" if diag else "_obj")
     os.makedirs(objdir, exist_ok=True)
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
-              "-Wall", "-Wno-unused-function", "-ffp-contract=fast"]
+              "-Wall", "-Wno-unused-function", "-ffp-contract=fast"] + (["-DRG_DIAG_STAMPS"] if diag else [])
     procs, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -71,15 +77,15 @@ def build(force=False, verbose=False, jobs=8):
             print(out)
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(f"--- {s}\n{o}" for s, o in failed))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     # librccl.so.1 by SONAME: inside a process that imported torch it binds to the
     # RCCL torch already loaded (same library torch.distributed's "nccl" backend uses)
     cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + \
         ["-L/opt/rocm/lib", "-lrccl"]
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, diag="--diag" in sys.argv))

@@ -41,6 +41,13 @@ void mt_jump_plan_destroy(MtJumpPlan *plan);
 int mt_produce_jump(hipStream_t stream, const MtJumpPlan &plan, uint32_t *state, uint32_t *out,
                     uint32_t *state_before);
 
+// ---------------------------------------------------------------- prepared pairs
+// rg_mf_prepare's output: one record per batch column s (processing order) of
+// kPairStride(n) int2 -- [q] = (user, item) of pair q (0: the positive, 1 + k: negative
+// k), [n + 1] = (plan slot of the positive's item side, 0) when a plan is given, the rest
+// zero -- so a column's ids and slot are one 64-B (n <= 6) or 128-B line.
+__host__ __device__ constexpr int pair_stride(int n_neg) { return n_neg + 2 <= 8 ? 8 : 16; }
+
 // ---------------------------------------------------------------- DPP
 // Cross-lane moves inside a 16-lane DPP row (no LDS traffic, all lanes valid).
 template <int CTRL>

@@ -69,13 +69,42 @@ struct PairsArgs {
 constexpr int32_t kOwnerBit = (int32_t)0x80000000;
 constexpr int32_t kIdMask = 0x7fffffff;
 
-// rg_mf_prepare: pairs[q * cols + s] for q = 0 (positive) and q = 1 + k (negative k).
+// Diagnostic build only (RG_DIAG_STAMPS, librg_hip_diag.so; scripts/mf_pairs_stamps.py):
+// per-wave s_memrealtime stamps at the pair pass's phase boundaries, each after a full
+// vmcnt drain so it marks when that phase's data had landed.  The product library has
+// no stamp code.
+#ifdef RG_DIAG_STAMPS
+__device__ unsigned long long *g_diag_stamps;
+#define RG_STAMP(k)                                                                                   \
+    do {                                                                                              \
+        if (g_diag_stamps) {                                                                          \
+            unsigned long long t_;                                                                    \
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+            if ((threadIdx.x & 63) == 0) g_diag_stamps[(blk * (kBlock / 64) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+        }                                                                                             \
+    } while (0)
+#else
+#define RG_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
+// rg_mf_prepare: record s of the prepared pairs (rg_common.h pair_stride): [q] for
+// q = 0 (positive) and q = 1 + k (negative k), [n + 1] the positive's plan slot; one
+// thread per entry, column-major so the record is written contiguously.
 // With stamps, every row a pair touches (valid or not: extra rows are harmless, a
 // missed one would not be) is stamped with the serial, and the first stamper owns it.
 __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict__ out, int64_t idx) {
-    const int64_t total = (int64_t)(1 + a.n_neg) * a.cols;
+    const int NP = 1 + a.n_neg, E = NP + 1;              // entries written per column
+    const int64_t total = (int64_t)E * a.cols;
     if (idx >= total) return;
-    const int64_t q = idx / a.cols, s = idx - q * a.cols;
+    const int64_t s = idx / E;
+    const int q = (int)(idx - s * E);
+    int2 *rec = out + s * pair_stride(a.n_neg);
+    if (q == NP) {                                       // the plan slot of the positive
+        rec[q] = make_int2(a.pos_slot != nullptr && s < a.n_pos ? a.pos_slot[s] : -1, 0);
+        return;
+    }
     const int64_t col = a.perm ? (int64_t)a.perm[s] : s;
     int2 r;
     if (q == 0) {
@@ -91,8 +120,10 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         if (ou != a.serial) r.x |= kOwnerBit;
         if (oi != a.serial) r.y |= kOwnerBit;
     }
-    out[idx] = r;
+    rec[q] = r;
 }
+
+__host__ __device__ inline int64_t prepare_threads(int64_t cols, int n_neg) { return (int64_t)(n_neg + 3) * cols; }
 
 __global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *__restrict__ out, int prio) {
     if (prio) __builtin_amdgcn_s_setprio(2);   // small latency-bound kernel running beside the HBM-bound apply
@@ -155,6 +186,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     const int D = a.dim;
     const int n = a.n_neg;
     const bool pairwise = (a.loss == RG_LOSS_BPR) || (a.loss == RG_LOSS_HINGE);
+    RG_STAMP(0);
 
     // ---- ids of every pair, prepared in processing order (one coalesced round trip) ----
     int uid[NP], iid[NP];
@@ -163,14 +195,16 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
 #pragma unroll
     for (int k = 0; k < NMAX; ++k)   // flat negatives that pair with no positive only matter to pointwise / adaptive
         valid[k + 1] = !kScoresFromBuf && active && k < n && (has_pos || !pairwise);
+    // the column's record: every pair's ids and the positive's plan slot in one line
+    const int2 *rec = a.pairs + (active ? s : 0) * (int64_t)pair_stride(n);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        const int2 pr = a.pairs[valid[q] || q == 0 ? (int64_t)q * a.cols + (active ? s : 0) : 0];
+        const int2 pr = rec[(valid[q] || q == 0) ? q : 0];
         uid[q] = pr.x & kIdMask;     // drop the ownership flags
         iid[q] = pr.y & kIdMask;
     }
-    // the positive's plan slot, loaded beside the ids (used after the dot products)
-    const int myslot = (kBackward && plan && has_pos) ? a.pos_slot[s] : -1;
+    const int myslot = (kBackward && plan && has_pos) ? rec[n + 1].x : -1;
+    RG_STAMP(1);
 
     // ---- claim list slots early (their latency hides under the gathers) -------
     int slot[TPL];
@@ -217,6 +251,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         }
     }
 
+    RG_STAMP(2);
     // ---- loss terms and dL/dp ---------------------------------------------------
     float la = 0.0f, lb = 0.0f;
     float dp[NP];
@@ -293,6 +328,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
             for (int q = 0; q < NP; ++q) ldz[ublk * NP + q] = dz[q];
         }
         lds_barrier();
+        RG_STAMP(3);
         bool ovf = false;
 #pragma unroll
         for (int j = 0; j < TPL; ++j) {
@@ -329,6 +365,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                 }
             }
         }
+        RG_STAMP(4);
         if (plan) {
             // block-level segmented sum of the positives' item-side rows, sorted by item
             const int stride = D + 1;
@@ -377,6 +414,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
             a.partials[2 * blk + 1] = sb;
         }
     }
+    RG_STAMP(5);
 }
 
 template <class L, int PHASE, int NMAX>
@@ -743,7 +781,8 @@ __global__ __launch_bounds__(kBlock) void mf_hot_scan_kernel(ApplyArgs a, const 
 // slot k = (pair k >> 1, side k & 1): the row the slot's pair touches on that side,
 // updated here iff the slot owns it (exactly one owner per touched row)
 template <class L>
-__global__ __launch_bounds__(kBlock) void mf_hot_kernel(ApplyArgs a, const int2 *__restrict__ pairs, int64_t n_slots) {
+__global__ __launch_bounds__(kBlock) void mf_hot_kernel(ApplyArgs a, const int2 *__restrict__ pairs, int64_t n_slots,
+                                                       int stride, int np_) {
     constexpr int LPU = L::LPU, UPW = L::UPW;
     const int lane = threadIdx.x & (kWave - 1);
     const int sub = lane & (LPU - 1);
@@ -754,6 +793,7 @@ __global__ __launch_bounds__(kBlock) void mf_hot_kernel(ApplyArgs a, const int2 
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t k = wave * UPW + (lane / LPU);
     if (k >= n_slots) return;
+    if ((int)((k >> 1) % stride) >= np_) return;   // a record's plan-slot / padding entries
     const int2 pr = pairs[k >> 1];
     const int32_t x = (k & 1) ? pr.y : pr.x;
     if (x >= 0) return;                                     // owner flag (bit 31) not set
@@ -903,6 +943,11 @@ struct ScoresLaunchF {
 };
 }  // namespace
 
+extern "C" int64_t rg_mf_pairs_len(int64_t cols, int32_t n_neg) {
+    if (cols <= 0 || n_neg < 1 || n_neg > kNMax) return -1;
+    return 2 * (int64_t)pair_stride(n_neg) * cols;
+}
+
 extern "C" int64_t rg_mf_partials_len(int64_t cols, int32_t dim) {
     int64_t nb = -1;
     PartialsLenF f{cols, &nb};
@@ -1008,6 +1053,7 @@ static int prepare_args(const rg_mf_batch_t *b, const rg_mf_work_t *w, const rg_
     a.pool = reinterpret_cast<const int2 *>(b->pool);
     a.pool_len = b->pool_len; a.n_neg = b->n_neg;
     a.perm = w ? w->plan_perm : nullptr;
+    a.pos_slot = w ? w->plan_pos_slot : nullptr;
     if (mark) {
         a.stamp = mark->stamp;
         a.serial = mark->serial;
@@ -1021,7 +1067,7 @@ extern "C" int rg_mf_prepare_marked(void *stream, const rg_mf_batch_t *b, const 
     PairsArgs a;
     int rc = prepare_args(b, w, mark, a);
     if (rc) return rc;
-    const int64_t total = (int64_t)(1 + b->n_neg) * b->cols;
+    const int64_t total = prepare_threads(b->cols, b->n_neg);
     static const int prio = [] { const char *e = getenv("RG_PREP_PRIO"); return e ? atoi(e) : 1; }();
     hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        (hipStream_t)stream, a, reinterpret_cast<int2 *>(b->pairs), prio);
@@ -1124,6 +1170,7 @@ struct HotLaunchF {
     ApplyArgs *a;
     const int2 *pairs;
     int64_t n_slots;
+    int stride, np_;
     const rg_mf_mark_t *mark;
     hipStream_t s;
     template <class L>
@@ -1138,7 +1185,8 @@ struct HotLaunchF {
         }
         const int64_t waves = (n_slots + L::UPW - 1) / L::UPW;
         const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-        hipLaunchKernelGGL((mf_hot_kernel<L>), dim3(nb < 1 ? 1 : nb), dim3(kBlock), 0, s, *a, pairs, n_slots);
+        hipLaunchKernelGGL((mf_hot_kernel<L>), dim3(nb < 1 ? 1 : nb), dim3(kBlock), 0, s, *a, pairs, n_slots, stride,
+                           np_);
         return check_launch("rg_mf_step_hot");
     }
 };
@@ -1176,7 +1224,7 @@ extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_
     if (next) {
         if ((rc = prepare_args(next, next_w, nullptr, prep))) return rc;
         prep_out = reinterpret_cast<int2 *>(next->pairs);
-        prep_blocks = ((int64_t)(1 + next->n_neg) * next->cols + kBlock - 1) / kBlock;
+        prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
     BackLaunchF f{&a, &prep, prep_out, prep_blocks, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
@@ -1205,7 +1253,7 @@ extern "C" int rg_mf_step_front(void *stream, const rg_mf_tables_t *t, const rg_
         if ((rc = prepare_args(next, next_w, next_mark, prep))) return rc;
         if (next->pairs == cur->pairs) return fail_arg("rg_mf_step_front: next pairs buffer aliases the current");
         f.prep_out = reinterpret_cast<int2 *>(next->pairs);
-        f.prep_blocks = ((int64_t)(1 + next->n_neg) * next->cols + kBlock - 1) / kBlock;
+        f.prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
     FrontLaunchF fl{&pa, &prep, &aa, f, (hipStream_t)stream};
     return dispatch_dim(t->dim, fl);
@@ -1246,7 +1294,8 @@ extern "C" int rg_mf_step_hot(void *stream, const rg_mf_tables_t *t, const rg_mf
     ApplyArgs a;
     int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull, a);
     if (rc) return rc;
-    HotLaunchF f{&a, reinterpret_cast<const int2 *>(cur->pairs), 2 * (int64_t)(1 + cur->n_neg) * cur->cols, mark,
+    HotLaunchF f{&a, reinterpret_cast<const int2 *>(cur->pairs), 2 * (int64_t)pair_stride(cur->n_neg) * cur->cols,
+                 pair_stride(cur->n_neg), 1 + cur->n_neg, mark,
                  (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
@@ -1313,3 +1362,10 @@ extern "C" int rg_mf_scores(void *stream, const float *uw, const float *iw, cons
     ScoresLaunchF f{uw, iw, ub, ib, dim, users, items, n, out, (hipStream_t)stream};
     return dispatch_dim(dim, f);
 }
+
+#ifdef RG_DIAG_STAMPS
+extern "C" int rg_diag_set_stamps(unsigned long long *dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(rg::g_diag_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? RG_OK
+                                                                                                  : RG_E_LAUNCH;
+}
+#endif

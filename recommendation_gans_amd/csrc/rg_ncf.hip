@@ -63,7 +63,7 @@ struct NcfArgs {
     const float *user_w, *item_w;
     const float *mlp;                 // flat parameters (named_parameters order)
     int64_t num_users, num_items;
-    const int2 *pairs;                // prepared, [q * cols + s]
+    const int2 *pairs;                // prepared, one record per column (rg_common.h pair_stride)
     int64_t n_pos, cols, global_cols, col_offset;
     int n_neg, loss, tc;              // tc: columns per tile
     int64_t tiles;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             if (valid && q > 0 && pairwise) valid = s < a.n_pos;
             int u = -1, i = -1;
             if (valid) {
-                const int2 pr = a.pairs[(int64_t)q * a.cols + s];
+                const int2 pr = a.pairs[s * pair_stride(a.n_neg) + q];
                 u = pr.x;
                 i = pr.y;
             }

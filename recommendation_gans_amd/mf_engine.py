@@ -10,10 +10,10 @@ Everything of the step lives in HBM and is only touched by librg_hip.so:
     scratch  per-row contribution counters/lists, overflow accumulators, loss partials
 
 Per step: rg_mf_pairs (forward, loss, dL/dz, contribution lists) then
-rg_mf_apply (pull gradients + optimizer over every row).  The native stepper
-(rg_stepper.cpp) generates the MT19937 words two steps ahead on a stream of its
-own and prepares the next step's pairs on another, so the sequential sampler is
-off the critical path.
+rg_mf_apply_prepare (pull gradients + optimizer over every row, and the next
+step's draws -> pool pairs in the same launch).  The native stepper
+(rg_stepper.cpp) generates the MT19937 words in 8-step slots ahead of use on a
+stream of its own, so the sequential sampler is off the critical path.
 """
 import ctypes
 from collections import namedtuple
@@ -232,8 +232,8 @@ class MFEngine:
         self.grad_buf = None
         self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
         self.mt_buf = _as_u32_tensor(mt_state, dev)
-        self.pairs = [torch.zeros((1 + self.n_neg) * self.batch_size * 2, dtype=torch.int32, device=dev)
-                      for _ in range(2)]
+        self.pairs = [torch.zeros(int(self.lib.rg_mf_pairs_len(self.batch_size, self.n_neg)), dtype=torch.int32,
+                                  device=dev) for _ in range(2)]
         self._work = _lib.MFWork(ptr(self.row_count), ptr(self.row_list), ptr(self.hot_grad), ptr(self.hot_bias),
                                  ptr(self.partials), ptr(self.scores_buf), ptr(self.max_key),
                                  ptr(self.active_count), None, None, None, ptr(self.part_row),

@@ -76,7 +76,7 @@ class NCFEngine:
         self.scores_buf = torch.zeros(self.rows, **f32)
         self.dp_buf = torch.zeros(self.rows, **f32)
         self.loss_out = torch.zeros(1, **f32)
-        self.pairs = [torch.zeros((1 + n) * B * 2, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.pairs = [torch.zeros(int(lib.rg_mf_pairs_len(B, n)), dtype=torch.int32, device=dev) for _ in range(2)]
         self.mt_buf = torch.from_numpy(np.ascontiguousarray(np.asarray(mt_state, np.uint32)).view(np.int32)).to(dev)
         self.seed = int(seed)
         self.t = 0

@@ -8,6 +8,7 @@ R=$GRAFT_REPO_ROOT
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_mf_fused_gpu.py tests/test_mf_gpu.py tests/test_dp_gpu.py tests/test_dropin_gpu.py tests/test_ncf_gpu.py > gpurun_out/ab_tests_$TAG.log 2>&1
 rc=$?; echo "tests exit=$rc"; tail -2 gpurun_out/ab_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/mf_pairs_stamps.py --steps 20 2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('stamps', d['span_us'], d['phase_median_us'], d['ids_phase_us_by_start_quartile'])" || exit $?
 run() {  # dir label env...
   local d=$1 l=$2; shift 2
   (cd $d && env "$@" timeout -k 10 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline > $R/gpurun_out/ab_$TAG.json 2>/dev/null) || return $?
@@ -16,6 +17,5 @@ run() {  # dir label env...
 for k in 1 2; do
   run $R/_ab/old old RG_X=0 || exit $?
   run $R new RG_X=0 || exit $?
-  run $R new_units8 RG_MT_UNITS=8 || exit $?
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $R/gpurun_out/prof_bench_$TAG.json 2>$R/gpurun_out/prof_$TAG.err && echo prof-ok

@@ -462,7 +462,8 @@ def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
         # the consumed pairs buffer of this step: negatives (q >= 1) in draw order
         found = False
         for buf in e.pairs:
-            pr = buf.view(1 + n, B, 2).cpu().numpy() & 0x7FFFFFFF   # ownership flags (bit 31)
+            S = 8 if n + 2 <= 8 else 16                              # per-column records (rg_mf_pairs_len)
+            pr = buf.view(B, S, 2)[:, :1 + n].transpose(0, 1).cpu().numpy() & 0x7FFFFFFF   # minus ownership flags
             if (pr[1:, :, 0].reshape(-1) == out["neg_u"].numpy()).all() and \
                (pr[1:, :, 1].reshape(-1) == out["neg_i"].numpy()).all():
                 found = True
