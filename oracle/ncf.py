@@ -10,10 +10,13 @@ reference's NCF training step:
   * autograd of the above              implicit.py:361 (linear / leaky_relu /
       dropout / sigmoid backward as ATen computes them, dense embedding grads)
   * Adam over every parameter          spotlight/optimizers.py:10-16, implicit.py:363
+  * NeuMF.__init__ / forward           spotlight/dnn_models/neuMF.py:7-55
+      the same tower (no output Linear inside), GMF branch U_mf[u] * I_mf[i],
+      affine_output over cat([tower, gmf]) -> Sigmoid
 
 Dropout masks are inputs (the reference draws them from torch's CPU generator;
 tests/golden records them with forward hooks), scaled by 1 / (1 - 0.5) = 2.
-Pinned by tests/golden/mlp_*.npz (made by importing the reference).
+Pinned by tests/golden/mlp_*.npz and neumf_*.npz (made by importing the reference).
 """
 import torch
 
@@ -105,6 +108,7 @@ class NCFOracle:
         self.P = MLPParams(tensors, names)
         self.loss_kind = loss
         self.n, self.batch_size = n_neg, batch_size
+        self.opt_lr, self.opt_wd, self.opt_betas = lr, weight_decay, betas
         self.opt = omf.Optim("adam", self.P.t, lr, weight_decay, betas=betas)
         self.pool_u = torch.as_tensor(pool_u).long()
         self.pool_i = torch.as_tensor(pool_i).long()
@@ -125,6 +129,99 @@ class NCFOracle:
         loss, dpp, dpn = omf.loss_and_dp(kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n, self.batch_size)
         g1 = backward(self.P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1))
         g2 = backward(self.P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1))
+        grads = [a + b for a, b in zip(g1, g2)]
+        self.opt.step(self.P.t, grads)
+        if return_all:
+            return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx, neg_u=nu, neg_i=ni, grads=grads)
+        return float(loss)
+
+
+class NeuMFParams(MLPParams):
+    """neuMF.py named_parameters() order: embedding_user_mlp, embedding_item_mlp,
+    embedding_user_mf, embedding_item_mf, layers.{3k}.weight/bias, affine_output."""
+
+    def emb(self):
+        return self.t[0], self.t[1]
+
+    def emb_mf(self):
+        return self.t[2], self.t[3]
+
+    def linears(self):
+        return [(self.t[k], self.t[k + 1]) for k in range(4, len(self.t), 2)]
+
+
+def neumf_forward(P, u, i, masks):
+    """neuMF.py:34-55: tower over cat(U_mlp[u], I_mlp[i]), GMF = U_mf[u] * I_mf[i],
+    sigmoid(affine_output(cat(tower, GMF)))."""
+    Ue, Ie = P.emb()
+    Um, Im = P.emb_mf()
+    x = torch.cat([Ue[u], Ie[i]], dim=-1)
+    lin = P.linears()
+    cache = {"z": [], "a": [x]}
+    a = x
+    for k, (W, b) in enumerate(lin[:-1]):
+        z = a.mm(W.t()) + b
+        r = torch.where(z > 0, z, z * LRELU)
+        a = r * (masks[k].to(z.dtype) * DROP_SCALE)
+        cache["z"].append(z)
+        cache["a"].append(a)
+    gmf = Um[u] * Im[i]
+    v = torch.cat([a, gmf], dim=-1)
+    W, b = lin[-1]
+    p = torch.sigmoid(v.mm(W.t()) + b)
+    cache.update(p=p, v=v, gmf_u=Um[u], gmf_i=Im[i])
+    return p, cache
+
+
+def neumf_backward(P, u, i, masks, cache, dp):
+    """Dense grads in parameter order (the reference's autograd, restated)."""
+    p = cache["p"]
+    dz = dp * (1 - p) * p
+    lin = P.linears()
+    W, b = lin[-1]
+    T = lin[-2][0].shape[0] if len(lin) > 1 else 8          # tower width (8)
+    dWo, dbo = dz.t().mm(cache["v"]), dz.sum(0)
+    dv = dz.mm(W)
+    dgmf = dv[:, T:]
+    dUm_rows, dIm_rows = dgmf * cache["gmf_i"], dgmf * cache["gmf_u"]
+    da = dv[:, :T]
+    grads_lin = [(dWo, dbo)]
+    for k in range(len(lin) - 2, -1, -1):
+        Wk, bk = lin[k]
+        z = cache["z"][k]
+        da = da * (masks[k].to(z.dtype) * DROP_SCALE)
+        dzk = torch.where(z > 0, da, da * LRELU)
+        grads_lin.append((dzk.t().mm(cache["a"][k]), dzk.sum(0)))
+        da = dzk.mm(Wk)
+    grads_lin.reverse()
+    Ue, Ie = P.emb()
+    Um, Im = P.emb_mf()
+    E = Ue.shape[1]
+    out = [torch.zeros_like(Ue).index_add_(0, u, da[:, :E]), torch.zeros_like(Ie).index_add_(0, i, da[:, E:]),
+           torch.zeros_like(Um).index_add_(0, u, dUm_rows), torch.zeros_like(Im).index_add_(0, i, dIm_rows)]
+    for dW, db in grads_lin:
+        out += [dW, db]
+    return out
+
+
+class NeuMFOracle(NCFOracle):
+    """One run_train_iteration (implicit.py:347-364) of NeuMF per ``step``."""
+
+    def __init__(self, tensors, names, *a, **k):
+        super().__init__(tensors, names, *a, **k)
+        self.P = NeuMFParams(tensors, names)
+        self.opt = omf.Optim("adam", self.P.t, self.opt_lr, self.opt_wd, betas=self.opt_betas)
+
+    def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
+        u = torch.as_tensor(pos_u).long()
+        i = torch.as_tensor(pos_i).long()
+        p_pos, c_pos = neumf_forward(self.P, u, i, masks_pos)
+        idx, nu, ni = self.draw(self.n * self.batch_size)
+        p_neg, c_neg = neumf_forward(self.P, nu, ni, masks_neg)
+        loss, dpp, dpn = omf.loss_and_dp(self.loss_kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n,
+                                         self.batch_size)
+        g1 = neumf_backward(self.P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1))
+        g2 = neumf_backward(self.P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1))
         grads = [a + b for a, b in zip(g1, g2)]
         self.opt.step(self.P.t, grads)
         if return_all:

@@ -28,6 +28,10 @@ Fixtures:
                     through ImplicitFactorizationModel.run_train_iteration, with
                     every dropout mask recorded by forward hooks (the masks come
                     from torch's CPU generator; the GPU path is fed them).
+  neumf_<loss>_e<E>_m<M>.npz
+                    3 training steps of the reference's NeuMF (spotlight/dnn_models/neuMF.py,
+                    neuMF_spotlight.py's tower sizes), as the MLP fixtures: dropout masks
+                    of the tower recorded by forward hooks.
   gan_<opt>_n<N>.npz
                     6 discriminator steps and the generator step after the 5th
                     (n_critic = 5, CGANs.py:290-301) of the reference's own CGAN
@@ -58,6 +62,7 @@ from spotlight import sampling as ref_sampling  # noqa: E402
 from spotlight.factorization.representations import BilinearNet  # noqa: E402
 from spotlight.interactions import Interactions  # noqa: E402
 from spotlight.dnn_models.mlp import MLP as RefMLP  # noqa: E402
+from spotlight.dnn_models.neuMF import NeuMF as RefNeuMF  # noqa: E402
 from spotlight.dnn_models import cGAN_models as ref_gan_models  # noqa: E402
 import CGANs as ref_cgans  # noqa: E402
 
@@ -289,6 +294,10 @@ def mlp_case(loss, E, seed=0, U=50, I=40, B=16, n=5):
     layers = [2 ** x for x in reversed(range(3, int(top) + 1))]       # ncf_spotlight.py:53-55
     torch.manual_seed(seed)
     net = RefMLP(layers=layers, num_users=U, num_items=I, embedding_dim=E)
+    return _tower_case(net, layers, loss, E, seed, U, I, B, n)
+
+
+def _tower_case(net, layers, loss, E, seed, U, I, B, n, extra_meta=()):
     init = {k: v.detach().clone().numpy() for k, v in net.state_dict().items()}
     prs = np.random.RandomState(seed + 1)
     pool_u, pool_i = prs.randint(0, U, 300), prs.randint(0, I, 300)
@@ -324,7 +333,7 @@ def mlp_case(loss, E, seed=0, U=50, I=40, B=16, n=5):
     rec = {"init_" + k.replace(".", "_"): v for k, v in init.items()}
     rec["layers"] = np.array(layers, dtype=np.int64)
     rec["pool_u"], rec["pool_i"] = pool_u.astype(np.int64), pool_i.astype(np.int64)
-    rec["meta"] = np.array([U, I, E, B, n], dtype=np.int64)
+    rec["meta"] = np.array([U, I, E, B, n] + list(extra_meta), dtype=np.int64)
     names = [k for k, _ in net.named_parameters()]
     rec["param_names"] = np.array(names)
     for s_, (pu, pi) in enumerate(steps_pos):
@@ -374,6 +383,20 @@ def mlp_case(loss, E, seed=0, U=50, I=40, B=16, n=5):
             rec[f"s{s_}_after_" + nm.replace(".", "_")] = p.detach().clone().numpy()
     rec["end_mt_state"] = np.array(random.getstate()[1], dtype=np.uint32)
     return rec
+
+
+def neumf_case(loss, E, M, seed=0, U=50, I=40, B=16, n=5):
+    import math
+    top = math.log2(E * 2)
+    layers = [2 ** x for x in reversed(range(3, int(top) + 1))]       # neuMF_spotlight.py:54-55
+    torch.manual_seed(seed)
+    net = RefNeuMF(layers, U, I, mf_embedding_dim=M, mlp_embedding_dim=E)
+    return _tower_case(net, layers, loss, E, seed, U, I, B, n, extra_meta=[M])
+
+
+def make_neumf():
+    for loss, E, M in (("pointwise", 16, 10), ("bpr", 8, 5), ("adaptive_hinge", 16, 12)):
+        save(f"neumf_{loss}_e{E}_m{M}.npz", **neumf_case(loss, E, M))
 
 
 def make_mlp():
@@ -542,6 +565,10 @@ if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gan":
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "mlp":
     make_mlp()
+    sys.exit(0)
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "neumf":
+    make_neumf()
     sys.exit(0)
 
 if __name__ == "__main__":
