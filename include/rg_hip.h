@@ -354,7 +354,10 @@ typedef struct rg_ncf_model {
     float *user_w_m, *user_w_v, *item_w_m, *item_w_v;
     float *mlp, *mlp_m, *mlp_v;             /* flat MLP parameters, named_parameters() order */
     int64_t num_users, num_items;
-    int32_t dim, pad_;
+    int32_t dim;
+    int32_t mf_dim;                         /* NeuMF: GMF embedding dim M (0: plain MLP) */
+    /* NeuMF GMF tables embedding_user_mf / embedding_item_mf [U, M], [I, M] + optimizer state */
+    float *mf_user_w, *mf_item_w, *mf_user_m, *mf_user_v, *mf_item_m, *mf_item_v;
 } rg_ncf_model_t;
 
 typedef struct rg_ncf_work {
@@ -365,9 +368,14 @@ typedef struct rg_ncf_work {
     const uint8_t *mask_pos, *mask_neg;     /* recorded dropout masks [rows][rg_ncf_mask_units] or null */
     uint64_t seed;                          /* dropout hash seed when no masks are given */
     int32_t training, pad_;                 /* 0: eval (no dropout) */
+    /* NeuMF only: per-example GMF gradient rows [tiles * rows_per_tile * 2M] (user | item),
+     * overflow rows [(U + I) * M] (zero between steps), planned positive partials [cols * M] */
+    float *mf_contrib, *mf_hot_grad, *mf_part_row;
 } rg_ncf_work_t;
 
 int64_t rg_ncf_mlp_len(int32_t dim);
+/* NeuMF flat parameters (tower layers, then affine_output (1 x (8 + M)) and its bias) */
+int64_t rg_neumf_param_len(int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_mask_units(int32_t dim);
 int64_t rg_ncf_cols_per_tile(int32_t n_neg);   /* also the plan's units per block */
 int64_t rg_ncf_rows_per_tile(void);
@@ -383,6 +391,12 @@ int rg_ncf_update(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t
 /* Embedding rows [row_begin, row_end) (users then items): pull + optimizer, in place. */
 int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
                  const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
+/* NeuMF (spotlight/dnn_models/neuMF.py:7-55): rg_ncf_pairs / rg_ncf_update run with
+ * model->mf_dim > 0 (the affine_output sees cat(tower, U_mf[u] * I_mf[i])); this applies
+ * the GMF tables, then the MLP tables (as rg_ncf_apply). */
+#define RG_NEUMF_MAX_MF_DIM 128
+int rg_neumf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
+                   const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
 
 /* ---------------------------------------------------------------- cGAN (C4)
  * The generator / discriminator of spotlight/dnn_models/cGAN_models.py as

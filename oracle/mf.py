@@ -246,7 +246,7 @@ def fit(oracle, train_u, train_i, valid_u, valid_i, np_state, n_iter):
     return rows, best, best_epoch
 
 
-def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0):
+def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None):
     """Parity verdict used by the GPU tests and smoke() (returns (ok, message)).
 
     Passes if ||got - ref32|| <= rtol * ||ref32|| (the north_star's 1e-5 relative,
@@ -255,13 +255,22 @@ def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0):
     small tensor (the biases) can exceed that while both fp32 results are equally
     right; then, given the same computation in float64 (``ref64``), the GPU result
     must be as close to it as the fp32 reference restatement is: ||got - ref64|| <=
-    band * ||ref32 - ref64|| + rtol/10 * ||ref64||."""
+    band * ||ref32 - ref64|| + rtol/10 * ||ref64||.
+
+    ``before`` (the tensor before the step): a step that cancels the tensor to ~0
+    (Adam's first step takes a bias of 0.01 by ~lr = 0.01) leaves only the operands'
+    rounding; then ||got - ref32|| <= rtol * ||before|| passes (relative to the
+    operands, as the oracle tests judge the reference's own steps)."""
     g = torch.as_tensor(got).double().reshape(-1).cpu()
     r = torch.as_tensor(ref32).double().reshape(-1)
     e32 = float((g - r).norm())
     n32 = float(r.norm())
     if e32 <= rtol * max(n32, 1e-30):
         return True, f"rel {e32 / max(n32, 1e-30):.2e}"
+    if before is not None:
+        nb = float(torch.as_tensor(before).double().reshape(-1).cpu().norm())
+        if e32 <= rtol * nb:
+            return True, f"rel-to-operand {e32 / max(nb, 1e-30):.2e}"
     if ref64 is None:
         return False, f"rel {e32 / max(n32, 1e-30):.2e} > {rtol}"
     r64 = torch.as_tensor(ref64).double().reshape(-1)

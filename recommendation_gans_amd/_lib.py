@@ -89,13 +89,16 @@ class NCFModel(ctypes.Structure):
                 ("user_w_v", ctypes.c_void_p), ("item_w_m", ctypes.c_void_p), ("item_w_v", ctypes.c_void_p),
                 ("mlp", ctypes.c_void_p), ("mlp_m", ctypes.c_void_p), ("mlp_v", ctypes.c_void_p),
                 ("num_users", ctypes.c_int64), ("num_items", ctypes.c_int64), ("dim", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
+                ("mf_dim", ctypes.c_int32), ("mf_user_w", ctypes.c_void_p), ("mf_item_w", ctypes.c_void_p),
+                ("mf_user_m", ctypes.c_void_p), ("mf_user_v", ctypes.c_void_p), ("mf_item_m", ctypes.c_void_p),
+                ("mf_item_v", ctypes.c_void_p)]
 
 
 class NCFWork(ctypes.Structure):
     _fields_ = [("contrib", ctypes.c_void_p), ("mlp_partials", ctypes.c_void_p), ("scores", ctypes.c_void_p),
                 ("dp", ctypes.c_void_p), ("mask_pos", ctypes.c_void_p), ("mask_neg", ctypes.c_void_p),
-                ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("mf_contrib", ctypes.c_void_p), ("mf_hot_grad", ctypes.c_void_p), ("mf_part_row", ctypes.c_void_p)]
 
 
 class GANDims(ctypes.Structure):
@@ -155,6 +158,7 @@ SIGNATURES = [
                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                    ctypes.c_int32, ctypes.c_void_p]),
     ("rg_ncf_mlp_len", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_neumf_param_len", ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_mask_units", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_ncf_rows_per_tile", ctypes.c_int64, []),
@@ -168,6 +172,8 @@ SIGNATURES = [
                                      ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p, ctypes.POINTER(MFLoss)]),
     ("rg_ncf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
+    ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
+                                      ctypes.POINTER(NCFWork), ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("rg_mt_window_to_cpython", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_advance_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),

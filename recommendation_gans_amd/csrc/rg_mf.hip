@@ -481,6 +481,7 @@ struct ApplyArgs {
     const float *contrib;
     int64_t contrib_stride;
     bool has_bias;
+    bool keep_count;              // NeuMF: the MF tables read the lists first, the MLP tables reset them
 };
 
 // mf_apply modes: pull the gradient from the lists and update (single GPU);
@@ -593,7 +594,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
                     a.hot_bias_grad[r] = 0.0f;
                 }
             }
-            if (sub == 0) a.row_count[r] = 0;
+            if (sub == 0 && !a.keep_count) a.row_count[r] = 0;
         }
         if (t == 1 && a.item_slot_off != nullptr) {   // planned positive partials of this item
             if (!SPEC) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
@@ -1326,6 +1327,42 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
     a.has_bias = false;
     ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
     return dispatch_dim(m->dim, f);
+}
+
+// NeuMF (spotlight/dnn_models/neuMF.py:7-55): the GMF tables take their gradient rows
+// from ncf_work->mf_contrib through the same per-row lists (kept), then the MLP tables
+// pull theirs and reset the lists (rg_ncf_apply).
+extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                              const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+    if (!m || !w || !nw || !opt) return fail_arg("rg_neumf_apply: null argument");
+    if (m->mf_dim < 1 || m->mf_dim > RG_NEUMF_MAX_MF_DIM) return fail_arg("rg_neumf_apply: mf_dim out of range");
+    if (!m->mf_user_w || !m->mf_item_w || !nw->mf_contrib || !nw->mf_hot_grad)
+        return fail_arg("rg_neumf_apply: null GMF table / scratch");
+    if (w->plan_perm && !nw->mf_part_row) return fail_arg("rg_neumf_apply: plan needs mf_part_row");
+    if (opt->kind == RG_OPT_ADAM && (!m->mf_user_m || !m->mf_item_m)) return fail_arg("rg_neumf_apply: Adam needs m");
+    if (opt->kind != RG_OPT_SGD && (!m->mf_user_v || !m->mf_item_v)) return fail_arg("rg_neumf_apply: needs v");
+    if (!w->row_count || !w->row_list) return fail_arg("rg_neumf_apply: null scratch");
+    const int64_t nrows = m->num_users + m->num_items;
+    int64_t rb = row_begin < 0 ? 0 : row_begin, re = row_end < 0 || row_end > nrows ? nrows : row_end;
+    if (rb > re) return fail_arg("rg_neumf_apply: row_begin > row_end");
+    ApplyArgs a{};
+    a.w_in[0] = m->mf_user_w; a.w_in[1] = m->mf_item_w;
+    a.w_out[0] = m->mf_user_w; a.w_out[1] = m->mf_item_w;
+    a.w_m[0] = m->mf_user_m; a.w_m[1] = m->mf_item_m; a.w_v[0] = m->mf_user_v; a.w_v[1] = m->mf_item_v;
+    a.num_users = m->num_users; a.num_items = m->num_items; a.dim = m->mf_dim;
+    a.row_begin = rb; a.row_end = re;
+    a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
+    a.hot_grad = nw->mf_hot_grad;
+    if (w->plan_perm) { a.item_slot_off = w->plan_item_slot_off; a.part_row = nw->mf_part_row; }
+    a.opt = *opt;
+    a.contrib = nw->mf_contrib;
+    a.contrib_stride = 2 * (int64_t)m->mf_dim;
+    a.has_bias = false;
+    a.keep_count = true;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
+    int rc = dispatch_dim(m->mf_dim, f);
+    if (rc) return rc;
+    return rg_ncf_apply(stream, m, w, nw->contrib, opt, row_begin, row_end);
 }
 
 extern "C" int rg_mf_apply(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,

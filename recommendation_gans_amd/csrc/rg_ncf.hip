@@ -15,6 +15,12 @@
 // (rg_ncf_apply pulls them through the per-row lists), planned per-tile partial
 // rows for the positives' items, the workgroup's weight-gradient partial and
 // deterministic loss partials.
+//
+// NeuMF (spotlight/dnn_models/neuMF.py:7-55) is the same tower plus a GMF branch:
+// the output Linear sees cat(A_NH, U_mf[u] * I_mf[i]) (mf_dim M > 0).  The GMF rows
+// are gathered beside A_0, the output layer adds M products, and the GMF backward
+// (dU_mf = dz w_m I_mf, dI_mf = dz w_m U_mf) runs before the tower's backward and
+// writes its own per-example rows (mf_contrib), overflow rows and planned partials.
 #include <cstdlib>
 
 #include "rg_common.h"
@@ -57,7 +63,12 @@ struct NcfShape {
         return u;
     }
     static constexpr int LDS = SW + SA + SA + P + 11 * kRows + 8;   // W, A, M(=A layout), dW, misc
+    // NeuMF extra floats: dW (M more), output GMF weights (M), GMF rows unless they fit
+    // the dX region (M <= E: row stride 2E + 1 holds U_mf | I_mf)
+    static constexpr int lds_neumf(int M) { return M == 0 ? LDS : LDS + 2 * M + (M <= E ? 0 : kRows * (2 * M + 1)); }
 };
+
+constexpr int kLdsMax = 160 * 1024 / 4;
 
 struct NcfArgs {
     const float *user_w, *item_w;
@@ -81,6 +92,10 @@ struct NcfArgs {
     const uint8_t *mask_pos, *mask_neg;
     uint64_t seed;
     int training;
+    // NeuMF (mf_dim > 0)
+    int mf_dim;
+    const float *mf_user_w, *mf_item_w;
+    float *mf_contrib, *mf_hot_grad, *mf_part_row;
 };
 
 enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2, kNcfLossOnly = 3 };
@@ -129,13 +144,14 @@ __device__ __forceinline__ v4f mma16(const float *A, int ai, int ak, const float
 template <int E, int PHASE>
 __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     using S = NcfShape<E>;
-    constexpr int NH = S::NH, P = S::P, IN0 = 2 * E;
+    constexpr int NH = S::NH, IN0 = 2 * E;
+    const int M = a.mf_dim, P = S::P + M;  // flat parameters: tower, output W (8 + M), output b
+    constexpr int WO = S::w_off(NH);       // flat offset of the output layer
     extern __shared__ float lds[];
     float *sW = lds;                      // padded weights
     float *sA = sW + S::SW;               // activations A_0 .. A_NH, [kRows][H_k + 1]
     float *sM = sA + S::SA;               // multipliers / deltas, same layout as sA (k >= 1)
-    float *sG = sM + S::SA;               // weight-gradient accumulator (flat, P)
-    float *sP = sG + P;                   // p per row
+    float *sP = sM + S::SA;               // p per row
     float *sDz = sP + kRows;              // dL/dlogit per row
     int *sU = reinterpret_cast<int *>(sDz + kRows);
     int *sI = sU + kRows;
@@ -147,6 +163,11 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     int *sLi = sLu + kRows;                                   // per row: item list slot (-1: none / planned)
     int *sPs = sLi + kRows;                                   // per row: plan slot of a positive (-1: none)
     float *sX = sM + S::sa_off(0);                            // dX rows [kRows][IN0 + 1] (M_0 is unused)
+    float *sG = reinterpret_cast<float *>(sPs + kRows) + 8;   // weight-gradient accumulator (flat, P)
+    float *sWm = sG + P;                                      // NeuMF output weights of the GMF units
+    // NeuMF GMF rows: U_mf at [r * gs], I_mf at [r * gs + M] (dX region, free until the tower's last backward)
+    const int gs = M <= E ? IN0 + 1 : 2 * M + 1;
+    float *sGm = M <= E ? sX : sWm + M;
     constexpr int cl_base = 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
@@ -160,7 +181,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         for (int e = tid; e < out * in; e += kNcfThreads) dst[(e / in) * (in + 1) + e % in] = W[e];
         for (int e = tid; e < out; e += kNcfThreads) dst[out * (in + 1) + e] = W[out * in + e];
     }
-    for (int e = tid; e < 9; e += kNcfThreads) sW[S::sw_off(NH) + e] = a.mlp[S::w_off(NH) + e];
+    for (int e = tid; e < 9; e += kNcfThreads) sW[S::sw_off(NH) + e] = a.mlp[WO + (e < 8 ? e : 8 + M)];
+    for (int e = tid; e < M; e += kNcfThreads) sWm[e] = a.mlp[WO + 8 + e];
     for (int e = tid; e < P; e += kNcfThreads) sG[e] = 0.0f;
     __syncthreads();
 
@@ -217,6 +239,13 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             float *d = sA + r * (IN0 + 1) + c4;
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
+        for (int e = tid; e < kRows * 2 * M; e += kNcfThreads) {      // NeuMF GMF rows
+            const int r = e / (2 * M), c = e % (2 * M);
+            float v = 0.0f;
+            if (sU[r] >= 0)
+                v = c < M ? a.mf_user_w[(int64_t)sU[r] * M + c] : a.mf_item_w[(int64_t)sI[r] * M + (c - M)];
+            sGm[r * gs + c] = v;
+        }
         __syncthreads();
         // ---- forward hidden layers ---------------------------------------------------------
         int mask_base = 0;
@@ -266,6 +295,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                 float d = 0.0f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) d = fmaf(AN[tid * 9 + j], wo[j], d);
+                const float *gu = sGm + tid * gs;
+                for (int c = 0; c < M; ++c) d = fmaf(gu[c] * gu[M + c], sWm[c], d);   // GMF = U_mf * I_mf
                 const float p = sigmoidf_ref(d + wo[8]);
                 sP[tid] = p;
                 if (PHASE == kNcfScores) a.scores[tile * kRows + tid] = sU[tid] >= 0 ? p : 0.0f;
@@ -345,14 +376,41 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             const float *wo = sW + S::sw_off(NH);
             const float *AN = sA + S::sa_off(NH);
             float *MN = sM + S::sa_off(NH);
-            if (tid < 9) {
+            for (int e = tid; e < 9 + M; e += kNcfThreads) {     // e: 8 tower units, bias, M GMF units
                 float acc = 0.0f;
-                for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], tid < 8 ? AN[r * 9 + tid] : 1.0f, acc);
-                sG[S::w_off(NH) + tid] += acc;
+                for (int r = 0; r < kRows; ++r) {
+                    const float x = e < 8 ? AN[r * 9 + e] : e == 8 ? 1.0f : sGm[r * gs + e - 9] * sGm[r * gs + M + e - 9];
+                    acc = fmaf(sDz[r], x, acc);
+                }
+                sG[WO + (e < 8 ? e : e == 8 ? 8 + M : e - 1)] += acc;
             }
             for (int e = tid; e < kRows * 8; e += kNcfThreads) {
                 const int r = e / 8, j = e % 8;
                 MN[r * 9 + j] = (sDz[r] * wo[j]) * MN[r * 9 + j];      // delta_{NH-1} = G * m
+            }
+            if (M > 0) {
+                // GMF backward: dU_mf = (dz w_c) I_mf, dI_mf = (dz w_c) U_mf (neuMF.py:43-50 under autograd)
+                for (int e = tid; e < kRows * M; e += kNcfThreads) {
+                    const int r = e / M, c = e % M;
+                    const float dg = sDz[r] * sWm[c];
+                    const float du = dg * sGm[r * gs + M + c], di = dg * sGm[r * gs + c];
+                    float *row = a.mf_contrib + (tile * kRows + r) * (int64_t)(2 * M);
+                    row[c] = du;
+                    row[M + c] = di;
+                    if (sLu[r] >= kNcfCap) atomicAdd(a.mf_hot_grad + (int64_t)sU[r] * M + c, du);
+                    if (sLi[r] >= kNcfCap) atomicAdd(a.mf_hot_grad + (a.num_users + sI[r]) * M + c, di);
+                }
+                if (a.pos_slot != nullptr) {
+                    for (int e = tid; e < tc * M; e += kNcfThreads) {
+                        const int cl = e / M, c = e % M;
+                        const int slot = sPs[cl];
+                        if (slot < 0 || (cl > 0 && sPs[cl - 1] == slot)) continue;
+                        float acc = 0.0f;
+                        for (int cc = cl; cc < tc && sPs[cc] == slot; ++cc)
+                            acc += (sDz[cc] * sWm[c]) * sGm[cc * gs + c];
+                        a.mf_part_row[(int64_t)slot * M + c] = acc;
+                    }
+                }
             }
             __syncthreads();
         }
@@ -524,10 +582,12 @@ struct NcfLaunchF {
     template <int E>
     int run() {
         using S = NcfShape<E>;
-        const size_t lds = (size_t)S::LDS * sizeof(float);
+        const int need = S::lds_neumf(a->mf_dim);
+        if (need > kLdsMax) return fail_arg("rg_ncf_pairs: NeuMF mf_dim too large for this embedding_dim (LDS)");
+        const size_t lds = (size_t)need * sizeof(float);
         static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(ncf_pairs_kernel<E, PHASE>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)lds) == hipSuccess;
+                                                     kLdsMax * (int)sizeof(float)) == hipSuccess;
         if (!attr) return fail_arg("ncf_pairs_kernel: cannot reserve LDS");
         hipLaunchKernelGGL((ncf_pairs_kernel<E, PHASE>), dim3(blocks), dim3(kNcfThreads), lds, s, *a);
         return check_launch("rg_ncf_pairs");
@@ -568,6 +628,13 @@ int ncf_mask_units(int E) {
 using namespace rg;
 
 extern "C" int64_t rg_ncf_mlp_len(int32_t dim) { return ncf_mlp_len(dim); }
+extern "C" int64_t rg_neumf_param_len(int32_t dim, int32_t mf_dim) {
+    const int p = ncf_mlp_len(dim);
+    return p < 0 || mf_dim < 1 || mf_dim > RG_NEUMF_MAX_MF_DIM ? -1 : p + mf_dim;
+}
+static int64_t ncf_param_len(const rg_ncf_model_t *m) {
+    return m->mf_dim == 0 ? ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
+}
 extern "C" int64_t rg_ncf_mask_units(int32_t dim) { return ncf_mask_units(dim); }
 extern "C" int64_t rg_ncf_cols_per_tile(int32_t n_neg) { return n_neg < 0 || n_neg >= kRows ? -1 : kRows / (n_neg + 1); }
 extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg) {
@@ -598,6 +665,14 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     if (nw->training && (nw->mask_pos == nullptr) != (nw->mask_neg == nullptr))
         return fail_arg("rg_ncf_pairs: give both dropout mask arrays or neither");
     if (w->plan_pos_slot && !w->part_row) return fail_arg("rg_ncf_pairs: plan needs part_row");
+    if (ncf_param_len(m) < 0) return fail_arg("rg_ncf_pairs: mf_dim out of range");
+    if (m->mf_dim > 0) {
+        if (!m->mf_user_w || !m->mf_item_w) return fail_arg("rg_ncf_pairs: NeuMF needs the GMF tables");
+        if (phase != kNcfScores && phase != kNcfLossOnly && (!nw->mf_contrib || !nw->mf_hot_grad))
+            return fail_arg("rg_ncf_pairs: NeuMF needs mf_contrib / mf_hot_grad");
+        if (phase != kNcfScores && phase != kNcfLossOnly && w->plan_pos_slot && !nw->mf_part_row)
+            return fail_arg("rg_ncf_pairs: NeuMF plan needs mf_part_row");
+    }
     NcfArgs a{};
     a.user_w = m->user_w; a.item_w = m->item_w; a.mlp = m->mlp;
     a.num_users = m->num_users; a.num_items = m->num_items;
@@ -619,6 +694,8 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     a.loss_partials = w->loss_partials;
     a.contrib = nw->contrib; a.wpart = nw->mlp_partials; a.scores = nw->scores; a.dp_in = nw->dp;
     a.mask_pos = nw->mask_pos; a.mask_neg = nw->mask_neg; a.seed = nw->seed; a.training = nw->training;
+    a.mf_dim = m->mf_dim; a.mf_user_w = m->mf_user_w; a.mf_item_w = m->mf_item_w;
+    a.mf_contrib = nw->mf_contrib; a.mf_hot_grad = nw->mf_hot_grad; a.mf_part_row = nw->mf_part_row;
     const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg);
     if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfScores) { NcfLaunchF<kNcfScores> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
@@ -642,8 +719,8 @@ extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf
     if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_update: Adam needs m state");
     if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_update: optimizer needs v state");
     if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_update: loss needs partials");
-    const int P = ncf_mlp_len(m->dim);
-    if (P < 0) return fail_arg("rg_ncf_update: bad dim");
+    const int P = (int)ncf_param_len(m);
+    if (P < 0) return fail_arg("rg_ncf_update: bad dim / mf_dim");
     const bool with_loss = loss && loss->out;
     hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(256), 0, (hipStream_t)stream, m->mlp,
                        opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,

@@ -113,7 +113,18 @@ class ImplicitFactorizationModel:
         common = dict(loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
                       betas=o.get("betas", (0.9, 0.999)), eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
                       n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
-        if hasattr(net, "embedding_user") and hasattr(net, "layers"):          # NCF MLP (mlp.py:5-46)
+        if hasattr(net, "embedding_user_mlp") and hasattr(net, "affine_output"):   # NeuMF (neuMF.py:7-55)
+            self._kind = "ncf"
+            self._params = [net.embedding_user_mlp.weight, net.embedding_item_mlp.weight,
+                            net.embedding_user_mf.weight, net.embedding_item_mf.weight]
+            for lin in [m_ for m_ in net.layers if isinstance(m_, torch.nn.Linear)] + [net.affine_output]:
+                self._params += [lin.weight, lin.bias]
+            self._embedding_dim = net.embedding_user_mlp.weight.shape[1]
+            w = [p.detach() for p in self._params]
+            self._engine = NCFEngine(w[0], w[1], w[4:], self._pool.user_ids, self._pool.item_ids, _mtstate.current(),
+                                     seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), mf_user_w=w[2],
+                                     mf_item_w=w[3], **common)
+        elif hasattr(net, "embedding_user") and hasattr(net, "layers"):          # NCF MLP (mlp.py:5-46)
             self._kind = "ncf"
             self._params = [net.embedding_user.weight, net.embedding_item.weight]
             for lin in [m_ for m_ in net.layers if isinstance(m_, torch.nn.Linear)]:
@@ -132,7 +143,7 @@ class ImplicitFactorizationModel:
             self._engine = MFEngine(w[0], w[1], w[2].reshape(-1), w[3].reshape(-1), self._pool.user_ids,
                                     self._pool.item_ids, _mtstate.current(), **common)
         else:
-            raise NotImplementedError("the fused steps train BilinearNet and the NCF MLP representations")
+            raise NotImplementedError("the fused steps train BilinearNet, the NCF MLP and NeuMF representations")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,

@@ -8,7 +8,12 @@ rg_ncf_pairs (fused MLP forward / loss / backward on MFMA) -> rg_ncf_update
 (MLP weight-gradient reduce + optimizer) -> rg_ncf_apply (embedding pull +
 optimizer over every row).  Adaptive hinge runs scores -> rg_ncf_adapt_dp ->
 given-dp.  Dropout: recorded masks (parity with the reference's CPU generator)
-or a per-(step, example, unit) hash (the documented device RNG)."""
+or a per-(step, example, unit) hash (the documented device RNG).
+
+NeuMF (spotlight/dnn_models/neuMF.py:7-55): pass the GMF tables (``mf_user_w``,
+``mf_item_w``); the same kernels run with mf_dim = M, the MLP parameters end in
+affine_output (1 x (8 + M)) and its bias, and rg_neumf_apply updates the GMF tables
+before the MLP tables."""
 import ctypes
 
 import numpy as np
@@ -22,7 +27,7 @@ from .mf_engine import build_plan
 class NCFEngine:
     def __init__(self, user_w, item_w, mlp_params, pool_u, pool_i, mt_state, *, loss="pointwise", optimizer="adam",
                  lr=1e-3, weight_decay=0.0, betas=(0.5, 0.999), eps=1e-8, alpha=0.99, n_neg=5, batch_size=256,
-                 device="cuda", seed=0):
+                 device="cuda", seed=0, mf_user_w=None, mf_item_w=None):
         _lib.require_gpu()
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
@@ -34,12 +39,21 @@ class NCFEngine:
         self.device = dev = torch.device(device)
         self.U, self.I = int(user_w.shape[0]), int(item_w.shape[0])
         self.E = E = int(user_w.shape[1])
-        self.P = int(lib.rg_ncf_mlp_len(E))
+        self.neumf = mf_user_w is not None
+        if self.neumf != (mf_item_w is not None):
+            raise ValueError("NeuMF needs both GMF tables")
+        self.M = int(mf_user_w.shape[1]) if self.neumf else 0
+        self.P = int(lib.rg_neumf_param_len(E, self.M) if self.neumf else lib.rg_ncf_mlp_len(E))
         if self.P < 0:
-            raise ValueError("NCF embedding_dim must be 8, 16, 32 or 64")
+            raise ValueError("NCF embedding_dim must be 8, 16, 32 or 64 (NeuMF mf_embedding_dim in [1, 128])")
         f32 = dict(dtype=torch.float32, device=dev)
         self.user_w = torch.as_tensor(user_w, dtype=torch.float32).to(dev).contiguous()
         self.item_w = torch.as_tensor(item_w, dtype=torch.float32).to(dev).contiguous()
+        self.mf_w = [torch.as_tensor(t, dtype=torch.float32).to(dev).contiguous() for t in (mf_user_w, mf_item_w)] \
+            if self.neumf else [None, None]
+        if self.neumf and (self.mf_w[0].shape[0] != self.U or self.mf_w[1].shape[0] != self.I
+                           or self.mf_w[1].shape[1] != self.M):
+            raise ValueError("GMF tables must be [num_users, M] and [num_items, M]")
         flat = torch.cat([torch.as_tensor(p, dtype=torch.float32).reshape(-1) for p in mlp_params])
         if flat.numel() != self.P:
             raise ValueError(f"MLP parameters have {flat.numel()} values, the E={E} layout has {self.P}")
@@ -47,8 +61,9 @@ class NCFEngine:
         self.mlp = flat.to(dev).contiguous()
         self.opt_kind = optimizer
         st = lambda t: torch.zeros_like(t)
-        self.m = [st(self.user_w), st(self.item_w), st(self.mlp)] if optimizer == "adam" else [None] * 3
-        self.v = [st(self.user_w), st(self.item_w), st(self.mlp)] if optimizer != "sgd" else [None] * 3
+        tabs_all = [self.user_w, self.item_w, self.mlp] + (self.mf_w if self.neumf else [])
+        self.m = [st(t) for t in tabs_all] if optimizer == "adam" else [None] * len(tabs_all)
+        self.v = [st(t) for t in tabs_all] if optimizer != "sgd" else [None] * len(tabs_all)
         self.lr, self.wd, self.betas, self.eps, self.alpha = lr, weight_decay, betas, eps, alpha
         pu = np.asarray(pool_u, dtype=np.int64)
         pi = np.asarray(pool_i, dtype=np.int64)
@@ -76,6 +91,10 @@ class NCFEngine:
         self.scores_buf = torch.zeros(self.rows, **f32)
         self.dp_buf = torch.zeros(self.rows, **f32)
         self.loss_out = torch.zeros(1, **f32)
+        M = self.M
+        self.mf_contrib = torch.zeros(self.rows * 2 * M, **f32) if self.neumf else None
+        self.mf_hot_grad = torch.zeros(rows * M, **f32) if self.neumf else None
+        self.mf_part_row = torch.zeros(B * M, **f32) if self.neumf else None
         self.pairs = [torch.zeros(int(lib.rg_mf_pairs_len(B, n)), dtype=torch.int32, device=dev) for _ in range(2)]
         self.mt_buf = torch.from_numpy(np.ascontiguousarray(np.asarray(mt_state, np.uint32)).view(np.int32)).to(dev)
         self.seed = int(seed)
@@ -83,7 +102,12 @@ class NCFEngine:
         self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
-                                    self.U, self.I, E, 0)
+                                    self.U, self.I, E, self.M)
+        if self.neumf:
+            md = self._model
+            md.mf_user_w, md.mf_item_w = ptr(self.mf_w[0]), ptr(self.mf_w[1])
+            md.mf_user_m, md.mf_item_m = ptr(self.m[3]), ptr(self.m[4])
+            md.mf_user_v, md.mf_item_v = ptr(self.v[3]), ptr(self.v[4])
         # the sampler / prepare part of the native stepper (its MF tables are unused here)
         tabs = _lib.MFTables(ptr(self.user_w), ptr(self.item_w), None, None, None, None, None, None,
                              None, None, None, None, None, None, None, None, self.U, self.I, E, 0)
@@ -144,6 +168,9 @@ class NCFEngine:
             mp, mn = masks
             nw.mask_pos, nw.mask_neg = ptr(mp), ptr(mn)
         nw.seed = (self.seed * 0x9E3779B97F4A7C15 + self.t) & 0xFFFFFFFFFFFFFFFF
+        if self.neumf:
+            nw.mf_contrib, nw.mf_hot_grad, nw.mf_part_row = ptr(self.mf_contrib), ptr(self.mf_hot_grad), \
+                ptr(self.mf_part_row)
         return nw
 
     def _loss(self, global_pos, out):
@@ -198,8 +225,12 @@ class NCFEngine:
         check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
                                      ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
               "rg_ncf_update")
-        check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
-                                    ctypes.byref(o), 0, -1), "rg_ncf_apply")
+        if self.neumf:
+            check(self.lib.rg_neumf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
+                                          ctypes.byref(o), 0, -1), "rg_neumf_apply")
+        else:
+            check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
+                                        ctypes.byref(o), 0, -1), "rg_ncf_apply")
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out
 
@@ -235,8 +266,9 @@ class NCFEngine:
         return out
 
     def params(self):
-        """[user table, item table, MLP parameters...] (device tensors of the reference's shapes)."""
-        return [self.user_w, self.item_w] + self.mlp_params()
+        """named_parameters() order as device tensors of the reference's shapes: [user table,
+        item table, (NeuMF: GMF user table, GMF item table), MLP parameters...]."""
+        return [self.user_w, self.item_w] + (self.mf_w if self.neumf else []) + self.mlp_params()
 
     def set_params(self, tensors):
         for dst, src in zip(self.params(), tensors):
@@ -251,6 +283,8 @@ class NCFEngine:
         for k in range(0, len(ps) - 2, 2):
             z = x @ ps[k].T + ps[k + 1]
             x = torch.where(z > 0, z, z * 0.1)
+        if self.neumf:
+            x = torch.cat([x, self.mf_w[0][users] * self.mf_w[1][items]], 1)
         return torch.sigmoid(x @ ps[-2].T + ps[-1]).reshape(-1)
 
     def mt_state(self):

@@ -159,3 +159,19 @@ def test_mlp_module_init_matches_reference(golden_dir, case):
     assert [k for k, _ in net.named_parameters()] == names
     for k, p in net.named_parameters():
         assert torch.equal(p.detach(), torch.from_numpy(z["init_" + k.replace(".", "_")])), k
+
+
+@pytest.mark.parametrize("case", ["neumf_pointwise_e16_m10", "neumf_bpr_e8_m5"])
+def test_neumf_module_init_matches_reference(golden_dir, case):
+    """spotlight/dnn_models/neuMF.py init under torch.manual_seed(0) (the goldens' init)."""
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
+    z = np.load(os.path.join(golden_dir, case + ".npz"))
+    U, I, E, B, n, M = (int(x) for x in z["meta"])
+    assert mlp_layers(E) == list(z["layers"])
+    torch.manual_seed(0)
+    net = NeuMF(mlp_layers(E), U, I, mf_embedding_dim=M, mlp_embedding_dim=E)
+    names = [str(x) for x in z["param_names"]]
+    assert [k for k, _ in net.named_parameters()] == names
+    for k, p in net.named_parameters():
+        assert torch.equal(p.detach(), torch.from_numpy(z["init_" + k.replace(".", "_")])), k

@@ -108,6 +108,33 @@ def test_ncf_fit_and_cli(tmp_path, monkeypatch):
     assert p.shape == (1682,) and np.all((p > 0) & (p < 1))
 
 
+def test_neumf_fit_and_cli(tmp_path, monkeypatch):
+    from recommendation_gans_amd import neuMF_spotlight
+    monkeypatch.chdir(tmp_path)
+    np.random.seed(0)
+    random.seed(0)
+    model = neuMF_spotlight.main(["--use_gpu", "True", "--dataset", "100K", "--training_epochs", "2",
+                                  "--batch_size", "1024", "--mlp_embedding_dim", "16", "--mf_embedding_dim", "50",
+                                  "--experiment_name", "neumf", "--k", "3"])
+    logs = os.path.join("experiments_results", "neumf", "result_outputs")
+    rows = list(csv.reader(open(os.path.join(logs, "summary.csv"))))
+    assert len(rows) == 3 and all(np.isfinite(float(x)) for x in rows[1][:2] + rows[2][:2])
+    assert float(rows[2][0]) < float(rows[1][0])
+    ck = torch.load(os.path.join("experiments_results", "neumf", "saved_models", "best_model"), weights_only=True)
+    assert ck["network"]["embedding_user_mf.weight"].shape == (943, 50)
+    assert ck["network"]["affine_output.weight"].shape == (1, 58)
+    res = json.load(open(os.path.join(logs, "test_summary.json")))
+    assert {"precision", "recall", "map"} <= set(res)
+    p = model.predict(3)
+    assert p.shape == (1682,) and np.all((p > 0) & (p < 1))
+    # the module's own forward (eval mode) scores as the engine does
+    net = model._net.eval()
+    u = torch.full((1682,), 3, dtype=torch.int64, device="cuda")
+    with torch.no_grad():
+        s = net(u, torch.arange(1682, device="cuda")).reshape(-1).cpu().numpy()
+    np.testing.assert_allclose(s, p, rtol=1e-5, atol=1e-6)
+
+
 def test_slate_generation_cli(tmp_path, monkeypatch):
     """python -m recommendation_gans_amd.slate_generation end to end on synthetic
     MovieLens-100K-shaped slates: summary.csv (the reference's columns; training
