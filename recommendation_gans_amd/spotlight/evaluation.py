@@ -1,4 +1,4 @@
-"""Ranking metrics of spotlight/evaluation.py (reference :115-353).
+"""Ranking metrics of spotlight/evaluation.py (reference :13-353).
 
 Same definitions as the reference: per test user with at least one test item,
 rank all items by -score (``argsort``), precision/recall@k over the top k,
@@ -6,6 +6,7 @@ average precision@k, hit ratio; popularity and random baselines.  The scores of 
 block of users against every item come from one GEMM on the device
 (``model.score_users``) instead of one ``predict`` call per user."""
 import numpy as np
+import scipy.stats as st
 
 FLOAT_MAX = np.finfo(np.float32).max
 
@@ -16,8 +17,9 @@ def _get_precision_recall(predictions, targets, k):
     return float(num_hit) / k, float(num_hit) / len(targets)
 
 
-def _ranked(model, test_csr, train_csr=None, block=4096):
-    """Yields (user, row indices, item ranking) for every test user with items."""
+def _scored(model, test_csr, train_csr=None, block=4096):
+    """Yields (user, row indices, -scores with train items at FLOAT_MAX) for every test
+    user with items, in user order."""
     users = np.flatnonzero(np.diff(test_csr.indptr) > 0)
     for s in range(0, len(users), block):
         ub = users[s:s + block]
@@ -26,7 +28,33 @@ def _ranked(model, test_csr, train_csr=None, block=4096):
             pred = scores[r]
             if train_csr is not None:
                 pred[train_csr[u].indices] = FLOAT_MAX
-            yield u, test_csr[u].indices, pred.argsort(axis=0)
+            yield u, test_csr[u].indices, pred
+
+
+def _ranked(model, test_csr, train_csr=None, block=4096):
+    """Yields (user, row indices, item ranking) for every test user with items."""
+    for u, idx, pred in _scored(model, test_csr, train_csr, block):
+        yield u, idx, pred.argsort(axis=0)
+
+
+def mrr_score(model, test, train=None):
+    """Mean reciprocal rank of each test user's items (evaluation.py:13-60): ranks of
+    -score with ties averaged (scipy rankdata), train items pushed to the end."""
+    test_csr = test.tocsr()
+    train_csr = train.tocsr() if train is not None else None
+    return np.array([(1.0 / st.rankdata(pred)[idx]).mean() for _, idx, pred in _scored(model, test_csr, train_csr)])
+
+
+def sequence_mrr_score(model, test, exclude_preceding=False):
+    """Reciprocal rank of each sequence's last item given the rest (evaluation.py:62-106)."""
+    sequences, targets = test.sequences[:, :-1], test.sequences[:, -1:]
+    mrrs = []
+    for i in range(len(sequences)):
+        pred = -model.predict(sequences[i])
+        if exclude_preceding:
+            pred[sequences[i]] = FLOAT_MAX
+        mrrs.append((1.0 / st.rankdata(pred)[targets[i]]).mean())
+    return np.array(mrrs)
 
 
 def precision_recall_score(model, test, train=None, k=10):

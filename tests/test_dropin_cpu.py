@@ -126,6 +126,31 @@ def test_metrics_match_per_user_loop():
     assert evaluation.map_at_k(m, test, k=3) == pytest.approx(np.mean(A))
 
 
+def test_mrr_matches_per_user_loop():
+    """evaluation.py:13-60 written out (scipy rankdata, ties averaged), with and without
+    train items excluded; ties made on purpose by quantising the scores."""
+    import scipy.stats as st
+    rs = np.random.RandomState(1)
+    U, I = 30, 25
+    scores = (rs.rand(U, I) * 8).round().astype(np.float32) / 8
+    tu, ti = rs.randint(0, U, 90), rs.randint(0, I, 90)
+    test = Interactions(tu, ti, ratings=np.ones(90), num_users=U, num_items=I)
+    train = Interactions(rs.randint(0, U, 200), rs.randint(0, I, 200), ratings=np.ones(200), num_users=U,
+                         num_items=I)
+    m = _FakeModel(scores)
+    for tr in (None, train):
+        ref = []
+        for u, row in enumerate(test.tocsr()):
+            if not len(row.indices):
+                continue
+            pred = -m.predict(u).copy()
+            if tr is not None:
+                pred[tr.tocsr()[u].indices] = evaluation.FLOAT_MAX
+            ref.append((1.0 / st.rankdata(pred)[row.indices]).mean())
+        got = evaluation.mrr_score(m, test, tr)
+        np.testing.assert_allclose(got, np.array(ref), rtol=0, atol=0)
+
+
 def test_synthetic_provider_shapes(tmp_path):
     from recommendation_gans_amd.utils.data_provider import data_provider
     np.random.seed(0)
