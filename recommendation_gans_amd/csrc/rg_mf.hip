@@ -75,6 +75,13 @@ constexpr int32_t kIdMask = 0x7fffffff;
 // no stamp code.
 #ifdef RG_DIAG_STAMPS
 __device__ unsigned long long *g_diag_stamps;
+__device__ int g_diag_flags;   // timing only (results are wrong): bit 0 skip the list-slot atomics,
+                               // bit 1 skip the list-entry stores, bit 2 skip the planned partial rows
+#define RG_DIAG_FLAG(b) ((g_diag_flags >> (b)) & 1)
+#else
+#define RG_DIAG_FLAG(b) 0
+#endif
+#ifdef RG_DIAG_STAMPS
 #define RG_STAMP(k)                                                                                   \
     do {                                                                                              \
         if (g_diag_stamps) {                                                                          \
@@ -196,14 +203,17 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     for (int k = 0; k < NMAX; ++k)   // flat negatives that pair with no positive only matter to pointwise / adaptive
         valid[k + 1] = !kScoresFromBuf && active && k < n && (has_pos || !pairwise);
     // the column's record: every pair's ids and the positive's plan slot in one line
+    // (the slot entry is loaded with the ids, unconditionally: issued after them it became a
+    // second round trip that queued behind the gathers of the waves already past this point)
     const int2 *rec = a.pairs + (active ? s : 0) * (int64_t)pair_stride(n);
+    const int2 slot_entry = rec[n + 1];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const int2 pr = rec[(valid[q] || q == 0) ? q : 0];
         uid[q] = pr.x & kIdMask;     // drop the ownership flags
         iid[q] = pr.y & kIdMask;
     }
-    const int myslot = (kBackward && plan && has_pos) ? rec[n + 1].x : -1;
+    const int myslot = (kBackward && plan && has_pos) ? slot_entry.x : -1;
     RG_STAMP(1);
 
     // ---- claim list slots early (their latency hides under the gathers) -------
@@ -214,7 +224,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         const int t = sub + j * LPU;
         if (kBackward && t < 2 * NP && !(plan && t == 1)) {
             const int q = t >> 1;
-            if (pick(valid, q)) {
+            if (pick(valid, q) && !RG_DIAG_FLAG(0)) {
                 const int64_t row = (t & 1) ? a.num_users + pick(iid, q) : (int64_t)pick(uid, q);
                 slot[j] = atomicAdd(a.row_count + row, 1);
             }
@@ -338,8 +348,10 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                 if (pick(valid, q)) {
                     const int u = pick(uid, q), i = pick(iid, q);
                     const int64_t row = (t & 1) ? a.num_users + i : (int64_t)u;
-                    if (slot[j] < kCap)
-                        a.row_list[row * kCap + slot[j]] = make_int2((t & 1) ? u : i, __float_as_int(ldz[ublk * NP + q]));
+                    if (slot[j] < kCap) {
+                        if (!RG_DIAG_FLAG(1))
+                            a.row_list[row * kCap + slot[j]] = make_int2((t & 1) ? u : i, __float_as_int(ldz[ublk * NP + q]));
+                    }
                     else
                         ovf = true;
                 }
@@ -391,8 +403,10 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                     }
                     accb += lrow[v * stride + D];
                 }
-                L::store(a.part_row, myslot, D, sub, acc);
-                if (sub == 0) a.part_bias[myslot] = accb;
+                if (!RG_DIAG_FLAG(2)) {
+                    L::store(a.part_row, myslot, D, sub, acc);
+                    if (sub == 0) a.part_bias[myslot] = accb;
+                }
             }
         }
     }
@@ -1207,7 +1221,13 @@ struct BackLaunchF {
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
         const dim3 grid((unsigned)(nb + prep_blocks));
-        hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+        static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
+        if (nt == 1)
+            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+        else if (nt >= 2)
+            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+        else
+            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
         return check_launch("rg_mf_apply_prepare");
     }
 };
@@ -1404,5 +1424,8 @@ extern "C" int rg_mf_scores(void *stream, const float *uw, const float *iw, cons
 extern "C" int rg_diag_set_stamps(unsigned long long *dev_buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(rg::g_diag_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? RG_OK
                                                                                                   : RG_E_LAUNCH;
+}
+extern "C" int rg_diag_set_flags(int flags) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(rg::g_diag_flags), &flags, sizeof(flags)) == hipSuccess ? RG_OK : RG_E_LAUNCH;
 }
 #endif

@@ -15,7 +15,7 @@ run() {  # dir label env...
   echo "$l" $(tail -1 gpurun_out/ab_$TAG.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e6,2), 'M/s', round(d['ms_per_step']*1e3,1), 'us/step; ev', round(d['roofline']['avg_launch_us'],1), 'us; host', round(d['host_enqueue_us_per_step'],1))")
 }
 for k in 1 2; do
-  run $R/_ab/old old RG_X=0 || exit $?
+  run $R/abold old RG_X=0 || exit $?
   run $R new RG_X=0 || exit $?
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $R/gpurun_out/prof_bench_$TAG.json 2>$R/gpurun_out/prof_$TAG.err && echo prof-ok
