@@ -66,9 +66,12 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true")
-    ap.add_argument("--model", default="mf", choices=["mf", "ncf", "gan"],
+    ap.add_argument("--model", default="mf", choices=["mf", "ncf", "neumf", "gan"],
                     help="mf: the BASELINE metric (MF-BPR); ncf: config 3 (NCF MLP, MFMA roofline); "
+                         "neumf: neuMF_spotlight.py defaults (mlp dim 16, mf dim 50); "
                          "gan: config 4 (cGAN slate generation, MFMA roofline)")
+    ap.add_argument("--mf-dim", type=int, default=50, help="NeuMF GMF dim (arg_extractor --mf_embedding_dim)")
+    ap.add_argument("--mlp-dim", type=int, default=16, help="NeuMF tower dim (arg_extractor --mlp_embedding_dim)")
     ap.add_argument("--gan-batch", type=int, default=256, help="cGAN batch (arg_extractor.py --batch_size)")
     ap.add_argument("--gan-hidden", type=int, default=256)
     ap.add_argument("--gan-slate", type=int, default=5)
@@ -122,24 +125,65 @@ def ncf_flops_per_example(E):
     return 3 * 2 * macs
 
 
+def ncf_cpu_baseline(params, names, data, B, n, neumf, budget_s):
+    """The oracle's NCF / NeuMF step (torch-CPU fp32, dropout masks drawn on the CPU as
+    torch's Dropout does) on full-size batches for ~budget_s seconds (kind "port")."""
+    from oracle import ncf as oncf
+    from oracle import rng as orng
+    random.seed(0)
+    cls = oncf.NeuMFOracle if neumf else oncf.NCFOracle
+    o = cls([p.clone() for p in params], names, data.pool_u, data.pool_i,
+            orng.state_from_python(random.getstate()), loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n,
+            batch_size=B)
+    units = oncf.layer_sizes(int(params[0].shape[1]))[1:]
+    pu, pi = torch.from_numpy(data.train_u), torch.from_numpy(data.train_i)
+
+    def one(s):
+        mp = [torch.randint(0, 2, (B, h), dtype=torch.uint8) for h in units]
+        mn = [torch.randint(0, 2, (n * B, h), dtype=torch.uint8) for h in units]
+        o.step(pu[s * B:(s + 1) * B], pi[s * B:(s + 1) * B], mp, mn)
+    one(0)                                           # warm-up
+    steps, t0 = 0, time.time()
+    while True:
+        one(steps + 1)
+        steps += 1
+        el = time.time() - t0
+        if el >= budget_s or steps >= 200:
+            break
+    return {"value": steps * B / el, "unit": "interactions/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{steps} full steps (B={B}, n={n}, pointwise, Adam over every parameter) after 1 warm-up "
+                      f"step, {el:.1f} s timed"}
+
+
 def bench_ncf(args):
     """Config 3: ncf_spotlight.py MovieLens-20M, mlp_embedding_dim=64, 1 GPU (pointwise, the CLI's
-    loss; dropout from the device hash RNG)."""
+    loss; dropout from the device hash RNG).  --model neumf: neuMF_spotlight.py with the
+    CLI's defaults (mlp_embedding_dim 16, mf_embedding_dim 50), same data and loop."""
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
     dev = torch.device("cuda:0")
-    E, B, n = args.dim, args.batch, args.neg
+    neumf = args.model == "neumf"
+    E, B, n = (args.mlp_dim if neumf else args.dim), args.batch, args.neg
+    M = args.mf_dim if neumf else 0
     data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
     U, I = data.num_users, data.num_items
     torch.manual_seed(0)
     from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
     from recommendation_gans_amd.ncf_spotlight import mlp_layers
-    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    if neumf:
+        net = NeuMF(mlp_layers(E), U, I, mf_embedding_dim=M, mlp_embedding_dim=E)
+    else:
+        net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    names = [k for k, _ in net.named_parameters()]
     params = [p.detach() for p in net.parameters()]
     random.seed(0)
     mt = np.asarray(random.getstate()[1], dtype=np.uint32)
-    eng = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt, loss="pointwise",
-                    optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0)
+    extra = dict(mf_user_w=params[2], mf_item_w=params[3]) if neumf else {}
+    mlp_params = params[4:] if neumf else params[2:]
+    eng = NCFEngine(params[0], params[1], mlp_params, data.pool_u, data.pool_i, mt, loss="pointwise",
+                    optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0,
+                    **extra)
     tu = torch.from_numpy(data.train_u).to(dev)
     ti = torch.from_numpy(data.train_i).to(dev)
     nb = len(data.train_u) // B
@@ -165,19 +209,28 @@ def bench_ncf(args):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
-    flops = ncf_flops_per_example(E) * B * (1 + n)
+    # NeuMF adds per example: GMF product (M) + output dot (2M) forward; dW_out (2M), the GMF
+    # unit gradients (M) and both table gradients (2M) backward
+    flops = (ncf_flops_per_example(E) + 8 * M) * B * (1 + n)
     ach = flops / (ms * 1e-3) / 1e12
-    out = {"metric": "train interactions/sec, NCF MLP dim=64 MovieLens-20M (config 3)", "value": args.steps * B / el,
+    metric = (f"train interactions/sec, NeuMF mlp dim={E} mf dim={M} MovieLens-20M" if neumf else
+              "train interactions/sec, NCF MLP dim=64 MovieLens-20M (config 3)")
+    workload = (f"NeuMF tower {mlp_layers(E)} + GMF {M} -> affine_output({8 + M}), " if neumf else
+                f"NCF MLP {mlp_layers(E)}->1, ")
+    out = {"metric": metric, "value": args.steps * B / el,
            "unit": "interactions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "f32", "data": f"synthetic ML-20M-shaped (U={U}, I={I}); MLP init as the reference",
-           "config": {"workload": f"NCF MLP {mlp_layers(E)}->1, batch {B}, {n} negatives, pointwise, adam, "
-                                  f"dropout 0.5 (device hash RNG)", "global_batch": B, "embedding_dim": E,
-                      "parallelism": "dp1"},
+           "config": {"workload": workload + f"batch {B}, {n} negatives, pointwise, adam, "
+                                             f"dropout 0.5 (device hash RNG)", "global_batch": B, "embedding_dim": E,
+                      "mf_embedding_dim": M, "parallelism": "dp1"},
            "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (ncf_pairs_kernel)", "achieved": ach,
                         "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
                         "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
            "final_loss": float(eng.loss_out[0])}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = ncf_cpu_baseline([p.clone() for p in params], names, data, B, n, neumf,
+                                               args.cpu_baseline_seconds)
     print(json.dumps(out), flush=True)
 
 
@@ -277,7 +330,7 @@ def bench_gan(args):
 
 def main():
     args = parse()
-    if args.model == "ncf":
+    if args.model in ("ncf", "neumf"):
         return bench_ncf(args)
     if args.model == "gan":
         return bench_gan(args)

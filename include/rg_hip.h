@@ -380,7 +380,9 @@ int64_t rg_ncf_mask_units(int32_t dim);
 int64_t rg_ncf_cols_per_tile(int32_t n_neg);   /* also the plan's units per block */
 int64_t rg_ncf_rows_per_tile(void);
 int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg);
-int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg);
+/* workgroups of rg_ncf_pairs (= weight-gradient partials): tiles, capped at 256 x the workgroups
+ * per CU that the dim's LDS allows (1 for the E = 64 MLP, up to 4) */
+int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim);
 /* phase 0: fused step (pointwise / bpr / hinge); 1: forward scores only; 2: fused with given dL/dp;
  * 3: forward + loss partials only (validation, run with training = 0) */
 int rg_ncf_pairs(void *stream, const rg_ncf_model_t *model, const rg_mf_batch_t *batch, rg_mf_work_t *work,

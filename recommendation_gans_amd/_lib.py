@@ -163,7 +163,7 @@ SIGNATURES = [
     ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_ncf_rows_per_tile", ctypes.c_int64, []),
     ("rg_ncf_tiles", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
-    ("rg_ncf_blocks", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_ncf_blocks", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFBatch),
                                     ctypes.POINTER(MFWork), ctypes.POINTER(NCFWork), ctypes.c_int32]),
     ("rg_ncf_adapt_dp", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(NCFWork),

@@ -122,7 +122,8 @@ __device__ __forceinline__ float opt_update(const rg_opt_t &o, float p, float gd
 // ---------------------------------------------------------------- row layouts
 // A table row of D floats is spread over LPU lanes.  VEC: D == 4 * LPU and each
 // lane owns one contiguous float4 (rows are 16-B aligned when D % 4 == 0).
-// !VEC: LPU == 64, lane l owns elements l, l + 64, ... (runtime D <= 64 * EPL).
+// !VEC: lane l of the row's LPU owns elements l, l + LPU, ... (runtime D <= LPU * EPL);
+// consecutive lanes read consecutive floats, so a row is LPU-float coalesced segments.
 template <int LPU_, int EPL_, bool VEC_>
 struct RowLayout {
     static constexpr int LPU = LPU_;
@@ -130,7 +131,7 @@ struct RowLayout {
     static constexpr bool VEC = VEC_;
     static constexpr int UPW = kWave / LPU;   // rows (units) per wave
 
-    __device__ static __forceinline__ int elem(int sub, int e) { return VEC ? sub * 4 + e : sub + 64 * e; }
+    __device__ static __forceinline__ int elem(int sub, int e) { return VEC ? sub * 4 + e : sub + LPU * e; }
 
     __device__ static __forceinline__ void load(float (&v)[EPL], const float *__restrict__ base,
                                                 int64_t row, int D, int sub) {
@@ -140,7 +141,7 @@ struct RowLayout {
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                const int c = sub + 64 * e;
+                const int c = sub + LPU * e;
                 v[e] = c < D ? base[row * (int64_t)D + c] : 0.0f;
             }
         }
@@ -155,7 +156,7 @@ struct RowLayout {
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                const int c = sub + 64 * e;
+                const int c = sub + LPU * e;
                 v[e] = c < D ? base[row * stride + c] : 0.0f;
             }
         }
@@ -169,7 +170,7 @@ struct RowLayout {
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                const int c = sub + 64 * e;
+                const int c = sub + LPU * e;
                 if (c < D) base[row * (int64_t)D + c] = v[e];
             }
         }
@@ -186,7 +187,7 @@ struct RowLayout {
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                const int c = sub + 64 * e;
+                const int c = sub + LPU * e;
                 if (c < D) __builtin_nontemporal_store(v[e], base + row * (int64_t)D + c);
             }
         }
@@ -201,7 +202,7 @@ struct RowLayout {
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                const int c = sub + 64 * e;
+                const int c = sub + LPU * e;
                 v[e] = c < D ? __builtin_nontemporal_load(base + row * (int64_t)D + c) : 0.0f;
             }
         }
@@ -225,7 +226,10 @@ inline int dispatch_dim(int dim, F &&f) {
         case 256: return f.template operator()<RowLayout<64, 4, true>>();
         default: break;
     }
-    if (dim >= 1 && dim <= 64) return f.template operator()<RowLayout<64, 1, false>>();
+    // other dims <= 64: 16 lanes per row (4 rows per wave) instead of a wave per row
+    if (dim >= 1 && dim <= 16) return f.template operator()<RowLayout<16, 1, false>>();
+    if (dim <= 32) return f.template operator()<RowLayout<16, 2, false>>();
+    if (dim <= 64) return f.template operator()<RowLayout<16, 4, false>>();
     if (dim <= 128) return f.template operator()<RowLayout<64, 2, false>>();
     if (dim <= 192) return f.template operator()<RowLayout<64, 3, false>>();
     if (dim <= 256) return f.template operator()<RowLayout<64, 4, false>>();

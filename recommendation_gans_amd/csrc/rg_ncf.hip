@@ -486,14 +486,15 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
 }
 
 // reduce the weight-gradient partials + optimizer update of the MLP parameters in
-// place: a block owns 64 parameters, its 4 waves sum fixed quarters of the
-// partials (coalesced 256-B loads) and combine in LDS in a fixed order
-// (deterministic); block 0 also finalises the loss
-__global__ __launch_bounds__(256) void ncf_update_kernel(float *mlp, float *m, float *v, const float *wpart,
+// place: a block owns 64 parameters, its kUpdWaves waves sum fixed slices of the
+// partials (coalesced 256-B loads, four independent chains so the loads pipeline)
+// and combine in LDS in a fixed order (deterministic); block 0 also finalises the loss
+constexpr int kUpdWaves = 16;
+__global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, float *m, float *v, const float *wpart,
                                                         int nparts, int P, rg_opt_t opt, const float *loss_partials,
                                                         int64_t n_partials, double inv_a, double inv_b,
                                                         float *loss_out) {
-    __shared__ float red[4][64];
+    __shared__ float red[kUpdWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (loss_out && blockIdx.x == 0 && wave == 0) {
         double sa = 0.0, sb = 0.0;
@@ -508,14 +509,24 @@ __global__ __launch_bounds__(256) void ncf_update_kernel(float *mlp, float *m, f
         if (lane == 0) *loss_out = (float)(sa * inv_a + sb * inv_b);
     }
     const int e = blockIdx.x * 64 + lane;
-    const int q = (nparts + 3) / 4, k0 = wave * q, k1 = min(nparts, k0 + q);
+    const int q = (nparts + kUpdWaves - 1) / kUpdWaves, k0 = wave * q, k1 = min(nparts, k0 + q);
     float g = 0.0f;
-    if (e < P)
-        for (int k = k0; k < k1; ++k) g += wpart[(int64_t)k * P + e];
+    if (e < P) {
+        float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        int k = k0;
+        for (; k + 4 <= k1; k += 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c[j] += wpart[(int64_t)(k + j) * P + e];
+        }
+        for (; k < k1; ++k) c[0] += wpart[(int64_t)k * P + e];
+        g = (c[0] + c[1]) + (c[2] + c[3]);
+    }
     red[wave][lane] = g;
     __syncthreads();
     if (wave != 0 || e >= P) return;
-    g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    g = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < kUpdWaves; ++w) g += red[w][lane];
     float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
     const float p = opt_update(opt, mlp[e], g, mm, vv);
     mlp[e] = p;
@@ -642,9 +653,27 @@ extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg) {
     return tc <= 0 ? -1 : (cols + tc - 1) / tc;
 }
 extern "C" int64_t rg_ncf_rows_per_tile(void) { return kRows; }
-extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg) {
+// workgroups resident per CU by LDS (at most 4): the E = 64 MLP takes a CU's LDS alone,
+// the small towers (and NeuMF's) leave room for several tiles in flight per CU, which is
+// what hides their gather / barrier latency
+static int ncf_lds_floats(int E, int M) {
+    switch (E) {
+        case 8: return NcfShape<8>::lds_neumf(M);
+        case 16: return NcfShape<16>::lds_neumf(M);
+        case 32: return NcfShape<32>::lds_neumf(M);
+        case 64: return NcfShape<64>::lds_neumf(M);
+        default: return -1;
+    }
+}
+
+extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim) {
     const int64_t t = rg_ncf_tiles(cols, n_neg);
-    return t <= 0 ? -1 : (t < 256 ? t : 256);      // one resident workgroup per CU (LDS-bound)
+    const int lds = ncf_lds_floats(dim, mf_dim);
+    if (t <= 0 || lds <= 0 || lds > kLdsMax || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
+    int per_cu = kLdsMax / lds;
+    if (per_cu > 4) per_cu = 4;
+    const int64_t cap = 256 * (int64_t)per_cu;
+    return t < cap ? t : cap;
 }
 
 extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_batch_t *b, rg_mf_work_t *w,
@@ -696,7 +725,8 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     a.mask_pos = nw->mask_pos; a.mask_neg = nw->mask_neg; a.seed = nw->seed; a.training = nw->training;
     a.mf_dim = m->mf_dim; a.mf_user_w = m->mf_user_w; a.mf_item_w = m->mf_item_w;
     a.mf_contrib = nw->mf_contrib; a.mf_hot_grad = nw->mf_hot_grad; a.mf_part_row = nw->mf_part_row;
-    const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg);
+    const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg, m->dim, m->mf_dim);
+    if (blocks <= 0) return fail_arg("rg_ncf_pairs: no launch shape for this dim / mf_dim");
     if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfScores) { NcfLaunchF<kNcfScores> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfGivenDp) { NcfLaunchF<kNcfGivenDp> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
@@ -722,7 +752,7 @@ extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf
     const int P = (int)ncf_param_len(m);
     if (P < 0) return fail_arg("rg_ncf_update: bad dim / mf_dim");
     const bool with_loss = loss && loss->out;
-    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(256), 0, (hipStream_t)stream, m->mlp,
+    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(kUpdWaves * 64), 0, (hipStream_t)stream, m->mlp,
                        opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,
                        nw->mlp_partials, (int)nparts, P, *opt, with_loss ? loss_partials : nullptr,
                        with_loss ? loss->n_partials : 0, with_loss ? loss->inv_a : 0.0,

@@ -76,7 +76,7 @@ class NCFEngine:
         self.tc = int(lib.rg_ncf_cols_per_tile(n))
         self.tiles = int(lib.rg_ncf_tiles(B, n))
         self.rows = self.tiles * int(lib.rg_ncf_rows_per_tile())
-        self.blocks = int(lib.rg_ncf_blocks(B, n))
+        self.blocks = int(lib.rg_ncf_blocks(B, n, E, self.M))
         self.units = int(lib.rg_ncf_mask_units(E))
         rows = self.U + self.I
         self.row_count = torch.zeros(rows, dtype=torch.int32, device=dev)
