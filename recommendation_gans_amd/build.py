@@ -57,7 +57,8 @@ def build(force=False, verbose=False, jobs=8, diag=False):
     objdir = os.path.join(PKG, "_obj_diag" if diag else "_obj")
     os.makedirs(objdir, exist_ok=True)
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
-              "-Wall", "-Wno-unused-function", "-ffp-contract=fast"] + (["-DRG_DIAG_STAMPS"] if diag else [])
+              "-Wall", "-Wno-unused-function", "-ffp-contract=fast"] + (["-DRG_DIAG_STAMPS"] if diag else []) + \
+        (os.environ.get("RG_EXTRA_CFLAGS", "").split() if diag else [])
     procs, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)

@@ -76,7 +76,8 @@ constexpr int32_t kIdMask = 0x7fffffff;
 #ifdef RG_DIAG_STAMPS
 __device__ unsigned long long *g_diag_stamps;
 __device__ int g_diag_flags;   // timing only (results are wrong): bit 0 skip the list-slot atomics,
-                               // bit 1 skip the list-entry stores, bit 2 skip the planned partial rows
+                               // bit 1 skip the list-entry stores, bit 2 skip the planned partial rows,
+                               // bit 3 return right after the ids
 #define RG_DIAG_FLAG(b) ((g_diag_flags >> (b)) & 1)
 #else
 #define RG_DIAG_FLAG(b) 0
@@ -214,7 +215,22 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         iid[q] = pr.y & kIdMask;
     }
     const int myslot = (kBackward && plan && has_pos) ? slot_entry.x : -1;
+    // each list task's own pair, loaded from the record beside the ids: indexing uid[] /
+    // iid[] / valid[] by the lane-dependent pair index made the compiler keep them as a
+    // per-thread LDS array (18 KB per workgroup), which slowed this whole phase ~10x
+    int tu[TPL], ti[TPL];
+    bool tv[TPL];
+#pragma unroll
+    for (int j = 0; j < TPL; ++j) {
+        const int t = sub + j * LPU, q = t >> 1;
+        const bool inb = t < 2 * NP && q <= n;
+        tv[j] = inb && (q == 0 ? has_pos : (!kScoresFromBuf && active && (has_pos || !pairwise)));
+        const int2 e = rec[inb ? q : 0];
+        tu[j] = e.x & kIdMask;
+        ti[j] = e.y & kIdMask;
+    }
     RG_STAMP(1);
+    if (RG_DIAG_FLAG(3)) return;
 
     // ---- claim list slots early (their latency hides under the gathers) -------
     int slot[TPL];
@@ -223,9 +239,8 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         slot[j] = 0;
         const int t = sub + j * LPU;
         if (kBackward && t < 2 * NP && !(plan && t == 1)) {
-            const int q = t >> 1;
-            if (pick(valid, q) && !RG_DIAG_FLAG(0)) {
-                const int64_t row = (t & 1) ? a.num_users + pick(iid, q) : (int64_t)pick(uid, q);
+            if (tv[j] && !RG_DIAG_FLAG(0)) {
+                const int64_t row = (t & 1) ? a.num_users + ti[j] : (int64_t)tu[j];
                 slot[j] = atomicAdd(a.row_count + row, 1);
             }
         }
@@ -345,8 +360,8 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
             const int t = sub + j * LPU;
             if (t < 2 * NP && !(plan && t == 1)) {
                 const int q = t >> 1;
-                if (pick(valid, q)) {
-                    const int u = pick(uid, q), i = pick(iid, q);
+                if (tv[j]) {
+                    const int u = tu[j], i = ti[j];
                     const int64_t row = (t & 1) ? a.num_users + i : (int64_t)u;
                     if (slot[j] < kCap) {
                         if (!RG_DIAG_FLAG(1))
