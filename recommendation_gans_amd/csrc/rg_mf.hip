@@ -706,7 +706,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
 // the dense update of rows [row_begin, row_end) (blocks [0, apply_blocks), as
 // mf_apply_kernel) and the prepare pass of the NEXT step (the remaining blocks) in one
 // launch: the split step then needs no side stream and no per-step cross-stream event
-template <class L, int NT>
+template <class L, int NT, bool SPEC = false>
 __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
                                                         int64_t apply_blocks) {
     const int64_t blk = blockIdx.x;
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs 
     const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item rows first, as mf_apply_kernel
     const int64_t ni = re > ia0 ? re - ia0 : 0;
     const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
-    apply_row<L, kApplyPull, NT, false>(a, r, sub);
+    apply_row<L, kApplyPull, NT, false, SPEC>(a, r, sub);
 }
 
 // ---------------------------------------------------------------------------- overlapped step
@@ -1237,7 +1237,12 @@ struct BackLaunchF {
         if (nb < 1) nb = 1;
         const dim3 grid((unsigned)(nb + prep_blocks));
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
-        if (nt == 1)
+        // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
+        // RG_APPLY_SPEC=0 turns it off)
+        static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
+        if (spec)
+            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+        else if (nt == 1)
             hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
         else if (nt >= 2)
             hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
