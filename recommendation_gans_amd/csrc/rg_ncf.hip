@@ -22,6 +22,7 @@
 // (dU_mf = dz w_m I_mf, dI_mf = dz w_m U_mf) runs before the tower's backward and
 // writes its own per-example rows (mf_contrib), overflow rows and planned partials.
 #include <cstdlib>
+#include <utility>
 
 #include "rg_common.h"
 
@@ -57,6 +58,11 @@ struct NcfShape {
         return o;
     }
     static constexpr int SA = sa_off(NH + 1);
+    static constexpr int mask_off(int k) {    // first dropout unit of hidden layer k
+        int u = 0;
+        for (int j = 1; j <= k; ++j) u += H(j);
+        return u;
+    }
     static constexpr int mask_units() {
         int u = 0;
         for (int k = 1; k <= NH; ++k) u += H(k);
@@ -100,6 +106,37 @@ struct NcfArgs {
 
 enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2, kNcfLossOnly = 3 };
 
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): the layer loops
+// contain barriers and were not unrolled, which left every layer's shapes (and so the
+// MFMA K loop) runtime values -- an LDS round trip between consecutive MFMA pairs
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Diagnostic build only (RG_DIAG_STAMPS): s_memrealtime at the tile phase boundaries of
+// the first two tiles of every workgroup (thread 0, after the phase's barrier), for
+// scripts/ncf_stamps.py.  The product library has no stamp code.
+#ifdef RG_DIAG_STAMPS
+__device__ unsigned long long *g_ncf_stamps;
+#define NS(k)                                                                                        \
+    do {                                                                                             \
+        if (g_ncf_stamps && threadIdx.x == 0 && tl_ < 2) {                                           \
+            unsigned long long t_;                                                                   \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+            g_ncf_stamps[((int64_t)blockIdx.x * 2 + tl_) * 8 + (k)] = t_;                            \
+        }                                                                                            \
+    } while (0)
+#else
+#define NS(k) \
+    do {      \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdULL;
@@ -119,32 +156,44 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     return h;
 }
 
-// C tile (16x16 at i0, j0) of A.B on LDS operands, K a multiple of 4.
+// C tile (16x16 at i0, j0) of A.B on LDS operands, K a compile-time multiple of 4.
 // A(i, k) = A[i * ai + k * ak], B(k, j) = B[k * bk + j * bj]; rows >= imax / cols >= jmax read 0.
+// Every operand of the tile is read first (one batch of LDS reads; rows outside the
+// tile read row 0 and are zeroed after), then the K/4 MFMAs issue over four
+// independent accumulators: no LDS round trip or MFMA dependency between
+// consecutive MFMAs.
+template <int K>
 __device__ __forceinline__ v4f mma16(const float *A, int ai, int ak, const float *B, int bk, int bj, int i0, int j0,
-                                     int K, int imax, int jmax, int lane) {
-    // called with compile-time shapes (the layer loops are unrolled): the k loop
-    // unrolls, LDS reads get immediate offsets and issue ahead of the MFMAs, and
-    // two accumulators alternate so the 40-cycle dependency does not serialise them
-    v4f acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+                                     int imax, int jmax, int lane) {
+    constexpr int NK = K / 4;
     const int li = lane & 15, lk = lane >> 4;
     const bool iv = i0 + li < imax, jv = j0 + li < jmax;
     const float *pa = A + (iv ? (i0 + li) : 0) * ai + lk * ak;
     const float *pb = B + lk * bk + (jv ? (j0 + li) : 0) * bj;
+    float av[NK], bv[NK];
 #pragma unroll
-    for (int k = 0; k < K; k += 8) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[k * ak] : 0.0f, jv ? pb[k * bk] : 0.0f, acc0, 0, 0, 0);
-        if (k + 4 < K)
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? pa[(k + 4) * ak] : 0.0f, jv ? pb[(k + 4) * bk] : 0.0f,
-                                                        acc1, 0, 0, 0);
+    for (int s = 0; s < NK; ++s) {
+        av[s] = pa[4 * s * ak];
+        bv[s] = pb[4 * s * bk];
     }
-    return acc0 + acc1;
+    __builtin_amdgcn_sched_barrier(0);   // keep the read batch ahead of the MFMAs
+    v4f acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+        acc[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? av[s] : 0.0f, jv ? bv[s] : 0.0f, acc[s & 3], 0, 0, 0);
+    return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 template <int E, int PHASE>
 __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     using S = NcfShape<E>;
     constexpr int NH = S::NH, IN0 = 2 * E;
+    // E = 64 takes a CU's LDS alone (one wave per SIMD, registers to spare): its serial
+    // LDS reductions are unrolled into one batch of reads; the small towers keep their
+    // registers for occupancy (several tiles per CU)
+    constexpr bool kWide = E >= 64;
     const int M = a.mf_dim, P = S::P + M;  // flat parameters: tower, output W (8 + M), output b
     constexpr int WO = S::w_off(NH);       // flat offset of the output layer
     extern __shared__ float lds[];
@@ -187,6 +236,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     __syncthreads();
 
     for (int64_t tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
+        const int tl_ = (int)((tile - blockIdx.x) / gridDim.x);
+        NS(0);
         const int64_t c0 = tile * tc;
         // ---- row ids: row r = q * tc + cl ----------------------------------------------
         if (tid < kRows) {
@@ -229,6 +280,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             sPs[r] = ps;
         }
         __syncthreads();
+        NS(1);
         // ---- gather A_0 = [U[u] | I[i]] ------------------------------------------------
         for (int e = tid; e < kRows * (IN0 / 4); e += kNcfThreads) {
             const int r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
@@ -247,20 +299,20 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             sGm[r * gs + c] = v;
         }
         __syncthreads();
+        NS(2);
         // ---- forward hidden layers ---------------------------------------------------------
-        int mask_base = 0;
-#pragma unroll
-        for (int k = 0; k < NH; ++k) {
-            const int in = S::H(k), out = S::H(k + 1);
+        static_for<NH>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int in = S::H(k), out = S::H(k + 1), mask_base = S::mask_off(k);
             const float *Ak = sA + S::sa_off(k);
             float *An = sA + S::sa_off(k + 1);
             float *Mn = sM + S::sa_off(k + 1);
             const float *Wk = sW + S::sw_off(k);
             const float *bk = Wk + out * (in + 1);
-            const int ct = out < 16 ? 1 : out / 16;
+            constexpr int ct = out < 16 ? 1 : out / 16;
             for (int t = wave; t < 2 * ct; t += 4) {
                 const int i0 = (t / ct) * 16, j0 = (t % ct) * 16;
-                const v4f z = mma16(Ak, in + 1, 1, Wk, 1, in + 1, i0, j0, in, kRows, out, lane);
+                const v4f z = mma16<in>(Ak, in + 1, 1, Wk, 1, in + 1, i0, j0, kRows, out, lane);
                 const int col = j0 + (lane & 15);
                 if (col < out) {
 #pragma unroll
@@ -284,9 +336,9 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                     }
                 }
             }
-            mask_base += out;
             __syncthreads();
-        }
+            if (k == 0) NS(3);
+        });
         // ---- output layer, scores, loss ---------------------------------------------------
         {
             const float *wo = sW + S::sw_off(NH);
@@ -296,6 +348,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) d = fmaf(AN[tid * 9 + j], wo[j], d);
                 const float *gu = sGm + tid * gs;
+#pragma unroll 8
                 for (int c = 0; c < M; ++c) d = fmaf(gu[c] * gu[M + c], sWm[c], d);   // GMF = U_mf * I_mf
                 const float p = sigmoidf_ref(d + wo[8]);
                 sP[tid] = p;
@@ -303,6 +356,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
         }
         __syncthreads();
+        NS(4);
         if (PHASE == kNcfScores) continue;
         // dL/dlogit per row (columns: one thread each) and the tile's loss partials
         if (tid < kRows) sDz[tid] = 0.0f;
@@ -311,32 +365,41 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             float la = 0.0f, lb = 0.0f;
             {
                 const int cl = tid;
-                float dp[RG_MF_MAX_NEG + 1];
-                for (int q = 0; q < NP; ++q) dp[q] = 0.0f;
+                // loops over the column's pairs run to the compile-time bound with a guard (the
+                // loads come from a clamped row), so dp[] stays in registers and the LDS
+                // reads of all pairs issue together
+                constexpr int QM = RG_MF_MAX_NEG + 1;
+                float dp[QM];
+#pragma unroll
+                for (int q = 0; q < QM; ++q) dp[q] = 0.0f;
                 const int r0 = cl;
                 const bool has_pos = sU[r0] >= 0;
                 if (PHASE == kNcfGivenDp) {
-                    for (int q = 0; q < NP; ++q)
-                        if (sU[q * tc + cl] >= 0) dp[q] = a.dp_in[tile * kRows + q * tc + cl];
+#pragma unroll
+                    for (int q = 0; q < QM; ++q)
+                        if (q < NP && sU[q * tc + cl] >= 0) dp[q] = a.dp_in[tile * kRows + q * tc + cl];
                 } else if (a.loss == RG_LOSS_POINTWISE) {
                     if (has_pos) {
                         const float p = sP[r0];
                         la += -fmaxf(logf(p), -100.0f);
                         dp[0] = ((p - 1.0f) / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_a;
                     }
-                    for (int q = 1; q < NP; ++q) {
-                        const int r = q * tc + cl;
-                        if (sU[r] >= 0) {
-                            const float p = sP[r];
+#pragma unroll
+                    for (int q = 1; q < QM; ++q) {
+                        const int r = min(q * tc + cl, kRows - 1);
+                        const bool ok = q < NP && sU[r] >= 0;
+                        const float p = sP[r];
+                        if (ok) {
                             lb += -fmaxf(logf(1.0f - p), -100.0f);
                             dp[q] = (p / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_b;
                         }
                     }
                 } else if (has_pos) {   // bpr / hinge on the neg.view(n, B) pairing
                     const float g = 1.0f / a.n_a, pp = sP[r0];
-                    for (int q = 1; q < NP; ++q) {
-                        const int r = q * tc + cl;
-                        if (sU[r] < 0) continue;
+#pragma unroll
+                    for (int q = 1; q < QM; ++q) {
+                        const int r = min(q * tc + cl, kRows - 1);
+                        if (q >= NP || sU[r] < 0) continue;
                         if (a.loss == RG_LOSS_BPR) {
                             const float sg = sigmoidf_ref(pp - sP[r]);
                             la += 1.0f - sg;
@@ -352,10 +415,11 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                         }
                     }
                 }
-                for (int q = 0; q < NP; ++q) {
-                    const int r = q * tc + cl;
+#pragma unroll
+                for (int q = 0; q < QM; ++q) {
+                    const int r = min(q * tc + cl, kRows - 1);
                     const float p = sP[r];
-                    sDz[r] = sU[r] >= 0 ? (dp[q] * (1.0f - p)) * p : 0.0f;
+                    if (q < NP) sDz[r] = sU[r] >= 0 ? (dp[q] * (1.0f - p)) * p : 0.0f;
                 }
             }
             sLa[cl_base + tid] = la;
@@ -369,6 +433,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             a.loss_partials[2 * tile + 1] = lb;
         }
         __syncthreads();
+        NS(5);
         if (PHASE == kNcfLossOnly) continue;         // validation: loss only (run_val_iteration)
         // ---- backward ------------------------------------------------------------------------
         {
@@ -378,9 +443,14 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             float *MN = sM + S::sa_off(NH);
             for (int e = tid; e < 9 + M; e += kNcfThreads) {     // e: 8 tower units, bias, M GMF units
                 float acc = 0.0f;
-                for (int r = 0; r < kRows; ++r) {
-                    const float x = e < 8 ? AN[r * 9 + e] : e == 8 ? 1.0f : sGm[r * gs + e - 9] * sGm[r * gs + M + e - 9];
-                    acc = fmaf(sDz[r], x, acc);
+                auto term = [&](int r) {
+                    return e < 8 ? AN[r * 9 + e] : e == 8 ? 1.0f : sGm[r * gs + e - 9] * sGm[r * gs + M + e - 9];
+                };
+                if constexpr (kWide) {
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], term(r), acc);
+                } else {
+                    for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], term(r), acc);
                 }
                 sG[WO + (e < 8 ? e : e == 8 ? 8 + M : e - 1)] += acc;
             }
@@ -414,18 +484,18 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
             __syncthreads();
         }
-#pragma unroll
-        for (int k = NH - 1; k >= 0; --k) {
-            const int in = S::H(k), out = S::H(k + 1);
+        static_for<NH>([&](auto kc) {
+            constexpr int k = NH - 1 - decltype(kc)::value;
+            constexpr int in = S::H(k), out = S::H(k + 1);
             const float *Ak = sA + S::sa_off(k);
             const float *Dk = sM + S::sa_off(k + 1);     // delta_k: [kRows][out + 1]
             const float *Wk = sW + S::sw_off(k);
             float *gW = sG + S::w_off(k);
             // dW_k (out x in) += delta^T A_k ; db_k += column sums of delta
-            const int ro = out < 16 ? 1 : out / 16, ci = in / 16;
+            constexpr int ro = out < 16 ? 1 : out / 16, ci = in / 16;
             for (int t = wave; t < ro * ci; t += 4) {
                 const int i0 = (t / ci) * 16, j0 = (t % ci) * 16;
-                const v4f c = mma16(Dk, 1, out + 1, Ak, in + 1, 1, i0, j0, kRows, out, in, lane);
+                const v4f c = mma16<kRows>(Dk, 1, out + 1, Ak, in + 1, 1, i0, j0, out, in, lane);
                 const int col = j0 + (lane & 15);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
@@ -435,19 +505,27 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
             for (int o = tid; o < out; o += kNcfThreads) {
                 float acc = 0.0f;
-                for (int r = 0; r < kRows; ++r) acc += Dk[r * (out + 1) + o];
+                if constexpr (kWide) {   // one batch of LDS reads, then the same in-order sum
+                    float col[kRows];
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) col[r] = Dk[r * (out + 1) + o];
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) acc += col[r];
+                } else {
+                    for (int r = 0; r < kRows; ++r) acc += Dk[r * (out + 1) + o];
+                }
                 gW[out * in + o] += acc;
             }
             // dA_k = delta W_k (kRows x in): k > 0 -> delta_{k-1} = dA * m_k ; k == 0 -> dX
-            const int cj = in / 16;
+            constexpr int cj = in / 16;
             for (int t = wave; t < 2 * cj; t += 4) {
                 const int i0 = (t / cj) * 16, j0 = (t % cj) * 16;
-                const v4f c = mma16(Dk, out + 1, 1, Wk, in + 1, 1, i0, j0, out, kRows, in, lane);
+                const v4f c = mma16<(out < 4 ? 4 : out)>(Dk, out + 1, 1, Wk, in + 1, 1, i0, j0, kRows, in, lane);
                 const int col = j0 + (lane & 15);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int row = i0 + (lane >> 4) * 4 + rr;
-                    if (k > 0) {
+                    if constexpr (k > 0) {
                         float *Mk = sM + S::sa_off(k);
                         Mk[row * (in + 1) + col] = c[rr] * Mk[row * (in + 1) + col];
                     } else {
@@ -457,7 +535,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                 }
             }
             __syncthreads();
-        }
+            if (k == NH - 1) NS(6);
+        });
         // ---- embedding gradient: overflow rows (hot users/items), planned item partials -----------
         for (int e = tid; e < 2 * kRows * E; e += kNcfThreads) {
             const int r = e / (2 * E), half = (e / E) & 1, c = e % E;
@@ -479,6 +558,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
         }
         __syncthreads();
+        NS(7);
     }
     // ---- the workgroup's weight-gradient partial ------------------------------------------------
     if (kBackward)
@@ -759,3 +839,10 @@ extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf
                        with_loss ? loss->inv_b : 0.0, with_loss ? loss->out : nullptr);
     return check_launch("rg_ncf_update");
 }
+
+#ifdef RG_DIAG_STAMPS
+extern "C" int rg_diag_set_ncf_stamps(unsigned long long *dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(rg::g_ncf_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? RG_OK
+                                                                                                  : RG_E_LAUNCH;
+}
+#endif

@@ -1,0 +1,76 @@
+"""Where the NCF / NeuMF pair kernel spends a tile: per-phase s_memrealtime stamps of the
+first two tiles of every workgroup, from the diagnostic library (python -m
+recommendation_gans_amd.build --diag -> librg_hip_diag.so).
+
+    python scripts/ncf_stamps.py [--dim 64] [--mf-dim 0] [--steps 10]
+
+Runs the bench configuration (ML-20M-shaped, B=8192, 5 negatives, pointwise, Adam,
+device dropout) through NCFEngine and prints median phase durations (us)."""
+import argparse
+import ctypes
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from recommendation_gans_amd import _lib, build  # noqa: E402
+
+PHASES = ["ids+slots", "gather", "forward layer 0", "forward rest + output", "loss", "backward first layer", "backward rest + rows"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--mf-dim", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    lib = _lib.load(build.DIAG_LIB)
+    lib.rg_diag_set_ncf_stamps.argtypes = [ctypes.c_void_p]
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
+    dev = torch.device("cuda:0")
+    E, M, B, n = args.dim, args.mf_dim, 8192, 5
+    data = movielens_like(ML20M, seed=0, zipf_s=1.0)
+    U, I = data.num_users, data.num_items
+    torch.manual_seed(0)
+    net = NeuMF(mlp_layers(E), U, I, mf_embedding_dim=M, mlp_embedding_dim=E) if M else \
+        MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    ps = [p.detach() for p in net.parameters()]
+    random.seed(0)
+    mt = np.asarray(random.getstate()[1], dtype=np.uint32)
+    extra = dict(mf_user_w=ps[2], mf_item_w=ps[3]) if M else {}
+    e = NCFEngine(ps[0], ps[1], ps[4:] if M else ps[2:], data.pool_u, data.pool_i, mt, loss="pointwise", lr=1e-3,
+                  weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0, **extra)
+    tu, ti = torch.from_numpy(data.train_u).to(dev), torch.from_numpy(data.train_i).to(dev)
+    plans = [e.make_plan(ti[s * B:(s + 1) * B]) for s in range(args.steps)]
+    buf = torch.zeros(e.blocks * 2 * 8, dtype=torch.int64, device=dev)
+    res = {p: [] for p in PHASES}
+    tile_us, starts = [], []
+    for s in range(args.steps):
+        on = s >= args.steps // 2
+        _lib.check(lib.rg_diag_set_ncf_stamps(buf.data_ptr() if on else None), "stamps")
+        e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s])
+        torch.cuda.synchronize()
+        if on:
+            st = buf.view(e.blocks, 2, 8).cpu().numpy().astype(np.int64)
+            t = (st - st[:, 0, 0].min()) * 0.01
+            for k, p in enumerate(PHASES):
+                res[p].append(float(np.median(t[:, :, k + 1] - t[:, :, k])))
+            tile_us.append(float(np.median(t[:, :, 7] - t[:, :, 0])))
+            starts.append(float(np.percentile(t[:, 0, 0], 90)))
+    _lib.check(lib.rg_diag_set_ncf_stamps(None), "stamps")
+    print(json.dumps({"dim": E, "mf_dim": M, "blocks": e.blocks, "tile_us_median": round(float(np.median(tile_us)), 2),
+                      "block_start_p90_us": round(float(np.median(starts)), 2),
+                      "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()}}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
