@@ -400,6 +400,15 @@ int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, 
 int rg_neumf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
                    const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
 
+/* ------------------------------------------------------------------------------
+ * Evaluation top-k (rg_eval.hip): the first k entries of argsort(-scores) per row, as
+ * precision_recall_score / hit_ratio / map_at_k read them (spotlight/evaluation.py:
+ * 108-213, 278-353).  scores [rows][ld] (device, fp32), out_idx [rows][k] (device,
+ * int32, rank order; equal scores: lower column first; NaN ranks last), 1 <= k <= 32.
+ * ---------------------------------------------------------------------------- */
+int rg_topk_rows(void *stream, const float *scores, int64_t rows, int64_t cols, int64_t ld, int32_t k,
+                 int32_t *out_idx);
+
 /* ---------------------------------------------------------------- cGAN (C4)
  * The generator / discriminator of spotlight/dnn_models/cGAN_models.py as
  * slate_generation.py:46-54 builds them (G hidden [H/2, H], D hidden [2H, H, H/2])

@@ -174,6 +174,8 @@ SIGNATURES = [
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                       ctypes.POINTER(NCFWork), ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
+    ("rg_topk_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("rg_mt_window_to_cpython", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_advance_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),

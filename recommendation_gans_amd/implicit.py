@@ -246,18 +246,43 @@ class ImplicitFactorizationModel:
             u = u.expand(i.numel())
         return self._engine.scores(u, i).detach().cpu().numpy().flatten()
 
-    def score_users(self, users):
-        """Scores of every item for a block of users, (len(users), num_items) float32 on
-        the host (evaluation helper): one GEMM of the tables (MF), or the eval-mode MLP
-        over the block x items pairs (NCF)."""
-        u = torch.as_tensor(np.asarray(users, dtype=np.int64), device=self._engine.device)
+    def _device_scores(self, u):
+        """(len(u), num_items) fp32 scores on the device: one GEMM of the tables (MF), or
+        the eval-mode MLP / NeuMF over the block x items pairs."""
         if self._kind == "mf":
             U, I, ub, ib = self._engine.params()
-            z = U[u] @ I.T + ub[u][:, None] + ib[None, :]
-            return torch.sigmoid(z).cpu().numpy()
+            return torch.sigmoid(U[u] @ I.T + ub[u][:, None] + ib[None, :])
         items = torch.arange(self._num_items, device=u.device)
         s = self._engine.scores(u.repeat_interleave(self._num_items), items.repeat(len(u)))
-        return s.reshape(len(u), self._num_items).detach().cpu().numpy()
+        return s.reshape(len(u), self._num_items).detach()
+
+    def score_users(self, users):
+        """Scores of every item for a block of users, (len(users), num_items) float32 on
+        the host (evaluation helper)."""
+        u = torch.as_tensor(np.asarray(users, dtype=np.int64), device=self._engine.device)
+        return self._device_scores(u).cpu().numpy()
+
+    def topk_users(self, users, k, exclude_csr=None):
+        """The first k entries of argsort(-scores) for a block of users (evaluation.py:
+        precision/recall@k, hit ratio, MAP@k), ranked on the device by rg_topk_rows;
+        items of ``exclude_csr``'s rows rank last (the reference's FLOAT_MAX).  Returns
+        (len(users), k) int64 on the host."""
+        from . import _lib
+        dev = self._engine.device
+        ub = np.asarray(users, dtype=np.int64)
+        u = torch.as_tensor(ub, device=dev)
+        s = self._device_scores(u).to(torch.float32).contiguous()
+        if exclude_csr is not None:
+            sub = exclude_csr[ub]
+            if sub.nnz:
+                rows = np.repeat(np.arange(len(ub)), np.diff(sub.indptr))
+                s[torch.as_tensor(rows, device=dev), torch.as_tensor(sub.indices.astype(np.int64), device=dev)] = \
+                    float("-inf")
+        out = torch.empty(len(ub), k, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        _lib.check(lib.rg_topk_rows(_lib.stream_handle(), _lib.ptr(s), len(ub), self._num_items, self._num_items,
+                                    int(k), _lib.ptr(out)), "rg_topk_rows")
+        return out.cpu().numpy().astype(np.int64)
 
     def test(self, test_set, item_popularity, k=5, rmse_flag=False, precision_recall=False, map_recall=True):
         test_results = {"k": k}

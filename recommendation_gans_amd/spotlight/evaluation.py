@@ -4,7 +4,10 @@ Same definitions as the reference: per test user with at least one test item,
 rank all items by -score (``argsort``), precision/recall@k over the top k,
 average precision@k, hit ratio; popularity and random baselines.  The scores of a
 block of users against every item come from one GEMM on the device
-(``model.score_users``) instead of one ``predict`` call per user."""
+(``model.score_users``) instead of one ``predict`` call per user; the metrics that read
+only the first k ranks (precision/recall@k, hit ratio, MAP@k) take them from the
+device top-k (``model.topk_users`` -> rg_topk_rows) when the model has one and
+k <= 32, so only users x k ids reach the host."""
 import numpy as np
 import scipy.stats as st
 
@@ -31,8 +34,20 @@ def _scored(model, test_csr, train_csr=None, block=4096):
             yield u, test_csr[u].indices, pred
 
 
-def _ranked(model, test_csr, train_csr=None, block=4096):
-    """Yields (user, row indices, item ranking) for every test user with items."""
+TOPK_MAX = 32
+
+
+def _ranked(model, test_csr, train_csr=None, block=4096, k=None):
+    """Yields (user, row indices, item ranking) for every test user with items; with k,
+    the ranking may hold only its first k entries (the device top-k)."""
+    if k is not None and k <= TOPK_MAX and hasattr(model, "topk_users"):
+        users = np.flatnonzero(np.diff(test_csr.indptr) > 0)
+        for s in range(0, len(users), block):
+            ub = users[s:s + block]
+            top = model.topk_users(ub, int(k), train_csr)      # (len(ub), k) int64, host
+            for r, u in enumerate(ub):
+                yield u, test_csr[u].indices, top[r]
+        return
     for u, idx, pred in _scored(model, test_csr, train_csr, block):
         yield u, idx, pred.argsort(axis=0)
 
@@ -63,7 +78,7 @@ def precision_recall_score(model, test, train=None, k=10):
     ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
     precision, recall = [], []
     cold = 0
-    for u, targets, ranking in _ranked(model, test_csr, train_csr):
+    for u, targets, ranking in _ranked(model, test_csr, train_csr, k=int(ks.max())):
         if train_csr is not None and not len(train_csr[u].indices):
             cold += 1
         p, r = zip(*[_get_precision_recall(ranking, targets, x) for x in ks])
@@ -81,7 +96,7 @@ def rmse_score(net, user_ids, item_ids):
 
 def hit_ratio(model, test, k=10):
     hits = users = 0
-    for _, target, ranking in _ranked(model, test.tocsr()):
+    for _, target, ranking in _ranked(model, test.tocsr(), k=k):
         users += 1
         if target in ranking[:k]:
             hits += 1
@@ -106,7 +121,7 @@ def mapk(actual, predicted, k=10):
 
 
 def map_at_k(model, test, k=5):
-    vals = [apk(targets, ranking, k=k) for _, targets, ranking in _ranked(model, test.tocsr())]
+    vals = [apk(targets, ranking, k=k) for _, targets, ranking in _ranked(model, test.tocsr(), k=k)]
     return np.mean(np.array(vals).squeeze())
 
 
