@@ -66,10 +66,11 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true")
-    ap.add_argument("--model", default="mf", choices=["mf", "ncf", "neumf", "gan"],
+    ap.add_argument("--model", default="mf", choices=["mf", "ncf", "neumf", "gan", "eval"],
                     help="mf: the BASELINE metric (MF-BPR); ncf: config 3 (NCF MLP, MFMA roofline); "
                          "neumf: neuMF_spotlight.py defaults (mlp dim 16, mf dim 50); "
-                         "gan: config 4 (cGAN slate generation, MFMA roofline)")
+                         "gan: config 4 (cGAN slate generation, MFMA roofline); "
+                         "eval: precision/recall@5 + MAP@5 of an ML-20M-shaped MF model (device top-k)")
     ap.add_argument("--mf-dim", type=int, default=50, help="NeuMF GMF dim (arg_extractor --mf_embedding_dim)")
     ap.add_argument("--mlp-dim", type=int, default=16, help="NeuMF tower dim (arg_extractor --mlp_embedding_dim)")
     ap.add_argument("--gan-batch", type=int, default=256, help="cGAN batch (arg_extractor.py --batch_size)")
@@ -328,8 +329,68 @@ def bench_gan(args):
     print(json.dumps(out), flush=True)
 
 
+def bench_eval(args):
+    """ImplicitFactorizationModel.test's ranking metrics
+    (precision_recall_score + map_at_k, k = 5, evaluation.py:115-185, 334-353) over the
+    synthetic ML-20M test split, for a d = 64 MF model of that shape.  A "step" is one
+    block of 4096 test users: one GEMM of the tables + sigmoid (library GEMM) and
+    rg_topk_rows; `value` = test users ranked per second over the whole split.  The CPU
+    leg is the reference's ranking (numpy argsort of each user's scores) on a bounded
+    sample of users."""
+    import types
+    from recommendation_gans_amd.implicit import ImplicitFactorizationModel
+    from recommendation_gans_amd.spotlight import evaluation
+    from recommendation_gans_amd.spotlight.interactions import Interactions
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    dev = torch.device("cuda:0")
+    d, k = args.dim, 5
+    data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
+    U, I = data.num_users, data.num_items
+    test = Interactions(data.test_u, data.test_i, num_users=U, num_items=I)
+    torch.manual_seed(0)
+    tabs = [torch.randn(U, d, device=dev) / d, torch.randn(I, d, device=dev) / d, torch.zeros(U, device=dev),
+            torch.zeros(I, device=dev)]
+    m = types.SimpleNamespace(_kind="mf", _num_items=I,
+                              _engine=types.SimpleNamespace(device=dev, params=lambda: tabs))
+    for name in ("_device_scores", "score_users", "topk_users"):
+        setattr(m, name, types.MethodType(getattr(ImplicitFactorizationModel, name), m))
+    csr = test.tocsr()
+    n_users = int((np.diff(csr.indptr) > 0).sum())
+    evaluation.precision_recall_score(m, Interactions(data.test_u[:2000], data.test_i[:2000], num_users=U,
+                                                      num_items=I), k=k)       # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    p, r = evaluation.precision_recall_score(m, test, k=k)
+    mp = evaluation.map_at_k(m, test, k=k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "evaluation test users/sec (precision/recall@5 + MAP@5), MF dim=64 MovieLens-20M",
+           "value": 2 * n_users / el, "unit": "users/s", "n_gpus": 1, "steps": 2, "warmup": 1,
+           "ms_per_step": el / 2 * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": f"synthetic ML-20M-shaped test split ({n_users} users, {len(data.test_u)} "
+                                   f"interactions), N(0,1/d) tables",
+           "config": {"workload": f"rank {I} items per test user, top {k}, two metric passes", "embedding_dim": d,
+                      "parallelism": "dp1"},
+           "precision": float(p), "recall": float(r), "map": float(mp), "roofline": None, "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        host = types.SimpleNamespace(score_users=m.score_users)
+        users = np.flatnonzero(np.diff(csr.indptr) > 0)
+        sel = np.isin(data.test_u, users[:1000])
+        sub = Interactions(data.test_u[sel], data.test_i[sel], num_users=U, num_items=I)
+        t0 = time.perf_counter()
+        evaluation.precision_recall_score(host, sub, k=k)
+        evaluation.map_at_k(host, sub, k=k)
+        elc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 2 * 1000 / elc, "unit": "users/s", "cores": 1, "kind": "port",
+                               "sample": "1000 test users x 2 passes: scores from the device block, then the "
+                                         "reference's per-user numpy argsort over all items on the host"}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.model == "eval":
+        return bench_eval(args)
     if args.model in ("ncf", "neumf"):
         return bench_ncf(args)
     if args.model == "gan":

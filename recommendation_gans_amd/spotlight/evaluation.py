@@ -20,6 +20,11 @@ def _get_precision_recall(predictions, targets, k):
     return float(num_hit) / k, float(num_hit) / len(targets)
 
 
+def _row(csr, u):
+    """csr[u].indices without building a row matrix (per-user slicing dominated the loop)."""
+    return csr.indices[csr.indptr[u]:csr.indptr[u + 1]]
+
+
 def _scored(model, test_csr, train_csr=None, block=4096):
     """Yields (user, row indices, -scores with train items at FLOAT_MAX) for every test
     user with items, in user order."""
@@ -30,8 +35,8 @@ def _scored(model, test_csr, train_csr=None, block=4096):
         for r, u in enumerate(ub):
             pred = scores[r]
             if train_csr is not None:
-                pred[train_csr[u].indices] = FLOAT_MAX
-            yield u, test_csr[u].indices, pred
+                pred[_row(train_csr, u)] = FLOAT_MAX
+            yield u, _row(test_csr, u), pred
 
 
 TOPK_MAX = 32
@@ -46,7 +51,7 @@ def _ranked(model, test_csr, train_csr=None, block=4096, k=None):
             ub = users[s:s + block]
             top = model.topk_users(ub, int(k), train_csr)      # (len(ub), k) int64, host
             for r, u in enumerate(ub):
-                yield u, test_csr[u].indices, top[r]
+                yield u, _row(test_csr, u), top[r]
         return
     for u, idx, pred in _scored(model, test_csr, train_csr, block):
         yield u, idx, pred.argsort(axis=0)
@@ -79,7 +84,7 @@ def precision_recall_score(model, test, train=None, k=10):
     precision, recall = [], []
     cold = 0
     for u, targets, ranking in _ranked(model, test_csr, train_csr, k=int(ks.max())):
-        if train_csr is not None and not len(train_csr[u].indices):
+        if train_csr is not None and not len(_row(train_csr, u)):
             cold += 1
         p, r = zip(*[_get_precision_recall(ranking, targets, x) for x in ks])
         precision.append(p)
