@@ -347,12 +347,15 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
 #pragma unroll
         for (int q = 0; q < NP; ++q) dz[q] = (dp[q] * (1.0f - p[q])) * p[q];
         // the list tasks index dz by a lane-dependent pair: stage it through LDS
-        // (a register select chain is turned back into scratch by the compiler)
+        // (a register select chain is turned back into scratch by the compiler).  A
+        // unit's lanes share one wave and a wave's LDS operations complete in order, so
+        // only the compiler must keep the reads after the writes (no workgroup barrier)
         if (sub == 0) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) ldz[ublk * NP + q] = dz[q];
         }
-        lds_barrier();
+        static_assert(kWave % LPU == 0, "a unit's lanes must share a wave");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         RG_STAMP(3);
         bool ovf = false;
 #pragma unroll
