@@ -409,6 +409,17 @@ int rg_neumf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work
 int rg_topk_rows(void *stream, const float *scores, int64_t rows, int64_t cols, int64_t ld, int32_t k,
                  int32_t *out_idx);
 
+/* ------------------------------------------------------------------------------
+ * Negative pool (rg_pool.cpp, host code): spotlight/sampling.py:46-70
+ * get_negative_samples, continuing NumPy's legacy global MT19937 (mt_key[624], mt_pos
+ * from np.random.get_state(), advanced in place).  users / items of n draws
+ * (np.random.choice), then the has_key redraws in index order against the training CSR
+ * (indptr [U + 1], column-sorted indices, summed ratings; all three null: no redraws).
+ * ---------------------------------------------------------------------------- */
+int rg_pool_build(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int64_t num_users, int64_t num_items,
+                  const int64_t *indptr, const int32_t *indices, const float *ratings, int64_t *out_users,
+                  int64_t *out_items);
+
 /* ---------------------------------------------------------------- cGAN (C4)
  * The generator / discriminator of spotlight/dnn_models/cGAN_models.py as
  * slate_generation.py:46-54 builds them (G hidden [H/2, H], D hidden [2H, H, H/2])

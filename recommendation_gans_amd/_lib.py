@@ -174,6 +174,9 @@ SIGNATURES = [
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                       ctypes.POINTER(NCFWork), ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
+    ("rg_pool_build", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
     ("rg_topk_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

@@ -5,9 +5,11 @@ NumPy's global legacy generator -- ``np.random.choice(U, n)``, then
 ``np.random.choice(I, n)``, then, in index order, one
 ``np.random.randint(0, I - len(pos_u), 1)`` for every pair whose raw rating is 1
 (``has_key``), remapped past the user's positives by binary search
-(sampling.py:37-44) -- but vectorised, and returns a ``NegativePool`` (two int64
-arrays that behave like the reference's list of (user, item) tuples) instead of
-n Python tuples."""
+(sampling.py:37-44) -- in native code (rg_pool_build, rg_pool.cpp) that continues and
+stores back NumPy's generator state, and returns a ``NegativePool`` (two int64 arrays
+that behave like the reference's list of (user, item) tuples) instead of n Python
+tuples."""
+import ctypes
 import logging
 import time
 
@@ -54,18 +56,34 @@ def sample_items(interaction, user_ids, num_items, shape, random_state=None):
 
 
 def get_negative_samples(train, num_samples):
+    """The pool, drawn by rg_pool_build (native, librg_hip.so) from NumPy's global legacy
+    generator, whose state it continues and stores back."""
+    from .. import _lib
     num_items, num_users = train.num_items, train.num_users
     logging.info("Generating %d Samples" % num_samples)
     start = time.time()
-    users = np.random.choice(num_users, num_samples)
-    items = np.random.choice(num_items, num_samples)
-    csr = train.csr_matrix
-    if csr.nnz:
-        hit = np.flatnonzero(np.asarray(csr[users, items]).ravel() == 1)
-        for k in hit:                       # in index order, as the reference loop draws
-            pos = np.sort(csr[users[k], :].toarray().nonzero()[1])
-            raw = np.random.randint(0, num_items - len(pos), size=1)
-            adj = pos - np.arange(len(pos))
-            items[k] = raw[0] + np.searchsorted(adj, raw[0], side="right")
+    csr = train.csr_matrix.tocsr(copy=True)
+    csr.sum_duplicates()
+    csr.sort_indices()
+    indptr = np.ascontiguousarray(csr.indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(csr.indices, dtype=np.int32)
+    ratings = np.ascontiguousarray(csr.data, dtype=np.float32)
+    name, key, pos, has_gauss, cached = np.random.get_state(legacy=True)
+    key = np.array(key, dtype=np.uint32)
+    mt_pos = np.array([pos], dtype=np.int32)
+    users = np.empty(num_samples, dtype=np.int64)
+    items = np.empty(num_samples, dtype=np.int64)
+    c = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    has = csr.nnz > 0
+    lib = _lib.load()
+    rc = lib.rg_pool_build(c(key), c(mt_pos), int(num_samples), int(num_users), int(num_items),
+                           c(indptr) if has else None, c(indices) if has else None, c(ratings) if has else None,
+                           c(users), c(items))
+    np.random.set_state((name, key, int(mt_pos[0]), has_gauss, cached))
+    if rc != 0:
+        msg = lib.rg_last_error().decode(errors="replace")
+        if "no negative" in msg:    # the reference's np.random.randint(0, 0) -> ValueError
+            raise ValueError("high <= 0: " + msg)
+        _lib.check(rc, "rg_pool_build")
     logging.info("Took %d seconds" % (time.time() - start))
     return NegativePool(users, items)
