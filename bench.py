@@ -206,7 +206,8 @@ def bench_ncf(args):
             evs.append((a, b_))
         else:
             eng.kernel_events = None
-        eng.train_step(u, i, plan=plans[g])
+        g2 = (args.warmup + s + 1) % nplan
+        eng.train_step(u, i, plan=plans[g], next_step=(tu[g2 * B:(g2 + 1) * B], ti[g2 * B:(g2 + 1) * B], plans[g2]))
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))

@@ -332,6 +332,10 @@ int rg_mf_stepper_train(void *stepper, void *stream, const rg_mf_step_in_t *cur,
 int rg_mf_stepper_acquire(void *stepper, void *stream, const rg_mf_step_in_t *cur, rg_mf_batch_t *batch_out,
                           rg_mf_work_t *work_out);
 int rg_mf_stepper_release(void *stepper, void *stream);
+/* After a step's release: prepare the next unit's pairs for `next` on the side stream now
+ * (ordered after the work `stream` holds), so the next acquire with the same input finds
+ * them ready.  A different input there prepares again. */
+int rg_mf_stepper_prefetch(void *stepper, void *stream, const rg_mf_step_in_t *next);
 /* Optimizer scalars for optimizer step `step` (1-based). */
 int rg_mf_stepper_opt(void *stepper, int64_t step, rg_opt_t *opt_out);
 int rg_mf_stepper_state(void *stepper, int32_t *current_set, int64_t *step);

@@ -177,6 +177,7 @@ SIGNATURES = [
     ("rg_pool_build", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]),
+    ("rg_mf_stepper_prefetch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn)]),
     ("rg_topk_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

@@ -547,6 +547,17 @@ extern "C" int rg_mf_stepper_release(void *h, void *stream) {
     return release(*st, (hipStream_t)stream);
 }
 
+// the pairs of the next unit (`taken`, i.e. called after the current step's release) for
+// `next`, prepared now on the side stream behind the work `stream` holds so far: a split
+// consumer (NCF / NeuMF) then finds them ready at its acquire instead of serialising a
+// prepare between its steps.  A different input at that acquire prepares again.
+extern "C" int rg_mf_stepper_prefetch(void *h, void *stream, const rg_mf_step_in_t *next) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !next) return rg::fail_arg("rg_mf_stepper_prefetch: null argument");
+    if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next)) return RG_OK;
+    return prepare_side(*st, (hipStream_t)stream, st->taken, *next);
+}
+
 extern "C" int rg_mf_stepper_opt(void *h, int64_t step, rg_opt_t *out) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !out) return rg::fail_arg("rg_mf_stepper_opt: null argument");

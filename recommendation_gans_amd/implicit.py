@@ -188,8 +188,10 @@ class ImplicitFactorizationModel:
                 if self._kind == "mf":
                     e.train_step_in(inputs[s], inputs[s + 1] if s + 1 < nb else None, loss_out=losses[s:s + 1])
                 else:
+                    nxt = (tu[(s + 1) * B:(s + 2) * B], ti[(s + 1) * B:(s + 2) * B], plans[s + 1]) \
+                        if s + 1 < nb else None
                     e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s],
-                                 loss_out=losses[s:s + 1])
+                                 loss_out=losses[s:s + 1], next_step=nxt)
             tl = [float(x) for x in losses.cpu().numpy()]          # loss.item() per batch
             train_epoch_loss = sum(tl) / nb
             if np.isnan(train_epoch_loss) or train_epoch_loss == 0.0:

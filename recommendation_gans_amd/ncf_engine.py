@@ -196,17 +196,25 @@ class NCFEngine:
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 0), "rg_ncf_pairs")
 
-    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None):
-        """One step; ``masks`` = (mask_pos [B, units] uint8, mask_neg [n*B, units] uint8) device
-        tensors recorded from the reference, or None for the device dropout RNG.  The loss
-        goes to ``loss_out`` (float32 device tensor) or the engine's own slot."""
+    @staticmethod
+    def _step_in_of(pos_u, pos_i, global_pos, plan):
         n_pos = int(pos_u.numel())
-        global_pos = n_pos if global_pos is None else int(global_pos)
-        x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos, global_pos,
-                          None, None, None)
+        x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos,
+                          n_pos if global_pos is None else int(global_pos), None, None, None)
         if plan is not None:
             x.plan_perm, x.plan_pos_slot, x.plan_item_slot_off = ptr(plan.perm), ptr(plan.pos_slot), \
                 ptr(plan.item_slot_off)
+        return x
+
+    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None, next_step=None):
+        """One step; ``masks`` = (mask_pos [B, units] uint8, mask_neg [n*B, units] uint8) device
+        tensors recorded from the reference, or None for the device dropout RNG.  The loss
+        goes to ``loss_out`` (float32 device tensor) or the engine's own slot.  ``next_step``
+        = (pos_u, pos_i, plan) of the following step: its negatives are prepared on the
+        side stream while this step's updates run (rg_mf_stepper_prefetch)."""
+        n_pos = int(pos_u.numel())
+        global_pos = n_pos if global_pos is None else int(global_pos)
+        x = self._step_in_of(pos_u, pos_i, global_pos, plan)
         stream = _lib.stream_handle()
         batch, work = _lib.MFBatch(), _lib.MFWork()
         check(self.lib.rg_mf_stepper_acquire(self._stepper, stream, ctypes.byref(x), ctypes.byref(batch),
@@ -219,6 +227,11 @@ class NCFEngine:
         if self.kernel_events is not None:
             self.kernel_events[1].record()
         check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
+        if next_step is not None:
+            nu, ni, nplan = next_step
+            self._next_in = self._step_in_of(nu, ni, None, nplan)
+            check(self.lib.rg_mf_stepper_prefetch(self._stepper, stream, ctypes.byref(self._next_in)),
+                  "rg_mf_stepper_prefetch")
         o = self._opt(self.t)
         parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials
         out = self.loss_out if loss_out is None else loss_out

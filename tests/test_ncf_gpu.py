@@ -86,3 +86,40 @@ def test_ncf_device_dropout_trains():
         assert all(np.isfinite(ls))
     np.testing.assert_allclose(losses[0], losses[1], rtol=1e-6)
     assert losses[0][-1] < losses[0][0]
+
+
+def test_prefetched_negatives_leave_the_trajectory_unchanged():
+    """rg_mf_stepper_prefetch (next step's negatives prepared during this step's updates)
+    draws the same negatives (MT stream bit-exact) and gives the unprefetched trajectory:
+    losses and parameters within 1e-5 relative (a row's listed contributions are summed
+    in the order their slots were claimed by atomics, so repeated runs differ in the last
+    bits with or without prefetch)."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from oracle import rng as orng
+    dev = torch.device("cuda:0")
+    U, I, E, B, n = 40000, 30000, 16, 256, 5
+    torch.manual_seed(1)
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E), torch.randn(I, E)]
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+        w = torch.empty(b_, a_)
+        torch.nn.init.xavier_uniform_(w)
+        params += [w, torch.full((b_,), 0.01)]
+    rs = np.random.RandomState(2)
+    pool_u, pool_i = rs.randint(0, U, 40000), rs.randint(0, I, 40000)
+    batches = [(torch.from_numpy(rs.choice(U, B, replace=False)).to(dev),
+                torch.from_numpy(rs.choice(I, B, replace=False)).to(dev)) for _ in range(5)]
+    out = []
+    for prefetch in (False, True):
+        e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, orng.py_seed_state(4), loss="pointwise",
+                      lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=3)
+        plans = [e.make_plan(b[1]) for b in batches]
+        ls = []
+        for s, (u, i) in enumerate(batches):
+            nxt = (batches[s + 1][0], batches[s + 1][1], plans[s + 1]) if prefetch and s + 1 < len(batches) else None
+            ls.append(float(e.train_step(u, i, plan=plans[s], next_step=nxt)[0]))
+        out.append((ls, [t.detach().cpu().clone() for t in e.params()], e.mt_state()))
+    assert (out[0][2] == out[1][2]).all()
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-5)
+    for a, b in zip(out[0][1], out[1][1]):
+        assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-12
