@@ -256,6 +256,37 @@ def gan_flops(N, S, H, E, Z, B):
     return d_step, g_step
 
 
+def gan_cpu_baseline(g_sd, d_sd, np_batches, N, S, H, E, Z, budget_s):
+    """The oracle's cGAN iterations (oracle/gan.py, float64 NumPy, the reference's
+    CGANs.py:370-457 restated) at the bench's full size: D iterations with a G iteration
+    every 5th, random z and dropout masks, for ~budget_s seconds (kind "port")."""
+    from oracle import gan as og
+    o = og.GANOracle({k: v.numpy() for k, v in g_sd.items()}, {k: v.numpy() for k, v in d_sd.items()}, N, S, H, E,
+                     Z, opt="rms", lr=1e-3)
+    rs = np.random.RandomState(0)
+    scales = (1.0 / 0.9, 1.0 / 0.7)
+    gd, dd = og.g_hidden(H), og.d_hidden(H)
+
+    def masks(B, widths, p):
+        return [(rs.rand(B, w) >= p).astype(np.float64) for w in widths]
+    steps, t0 = 0, time.time()
+    while True:
+        hist, sl = np_batches[steps % len(np_batches)]
+        B = hist.shape[0]
+        m = masks(B, dd, 0.3) + masks(B, gd, 0.1) + masks(B, dd, 0.3)
+        o.d_step(hist, sl, rs.rand(B, Z), m, scales)
+        if (steps + 1) % 5 == 0:
+            o.g_step(hist, rs.rand(B, Z), masks(B, gd, 0.1) + masks(B, dd, 0.3), scales)
+        steps += 1
+        el = time.time() - t0
+        if el >= budget_s or steps >= 50:
+            break
+    B = np_batches[0][0].shape[0]
+    return {"value": steps * B / el, "unit": "slates/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{steps} steps (D iteration each, G iteration every 5th) of the float64 NumPy oracle at the "
+                      f"bench size (N={N}, B={B}), {el:.1f} s"}
+
+
 def bench_gan(args):
     """Config 4: slate_generation.py cGAN, MovieLens-20M, slate_size 5, gan_hidden_layer 256,
     batch 256, RMSprop (optim_gan default), n_critic 5: one step = one discriminator
@@ -276,7 +307,7 @@ def bench_gan(args):
     users = np.nonzero(counts > S)[0]
     L = int((counts[users] - S).max())
     nb = min(len(users) // B, 40)
-    batches = []
+    batches, np_batches = [], []
     for g in range(nb):
         hist = np.full((B, L), N, np.int64)
         sl = np.zeros((B, S), np.int64)
@@ -285,9 +316,13 @@ def bench_gan(args):
             hist[r, :len(items) - S] = items[:-S]
             sl[r] = items[-S:]
         batches.append(GANBatch(hist, sl, N, S, dev))
+        if g < 2:
+            np_batches.append((hist, sl))
     torch.manual_seed(0)
     G = generator(num_items=N, noise_dim=Z, embedding_dim=E, hidden_layer=[H // 2, H], output_dim=S)
     D = discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
+    g_sd = {k: v.detach().clone() for k, v in G.state_dict().items()}
+    d_sd = {k: v.detach().clone() for k, v in D.state_dict().items()}
     eng = GANEngine(G.state_dict(), D.state_dict(), N, S, H, E, Z, batch_max=B, optimizer="rms", lr=1e-3, device=dev)
     del G, D
     steps = max(5, args.steps // 5 * 5)
@@ -327,6 +362,8 @@ def bench_gan(args):
                         "g_iter_gflop": fg / 1e9},
            "cpu_baseline": None,
            "final": [float(x) for x in eng.d_step(batches[0]).cpu()]}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = gan_cpu_baseline(g_sd, d_sd, np_batches, N, S, H, E, Z, args.cpu_baseline_seconds)
     print(json.dumps(out), flush=True)
 
 
