@@ -110,16 +110,22 @@ def test_prefetched_negatives_leave_the_trajectory_unchanged():
     batches = [(torch.from_numpy(rs.choice(U, B, replace=False)).to(dev),
                 torch.from_numpy(rs.choice(I, B, replace=False)).to(dev)) for _ in range(5)]
     out = []
-    for prefetch in (False, True):
+    # mode 0: no prefetch; 1: the next step's batch prefetched; 2: a wrong batch prefetched
+    # (the next acquire sees another input and prepares again)
+    for mode in (0, 1, 2):
         e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, orng.py_seed_state(4), loss="pointwise",
                       lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=3)
         plans = [e.make_plan(b[1]) for b in batches]
         ls = []
         for s, (u, i) in enumerate(batches):
-            nxt = (batches[s + 1][0], batches[s + 1][1], plans[s + 1]) if prefetch and s + 1 < len(batches) else None
+            nxt = None
+            if mode and s + 1 < len(batches):
+                k = s + 1 if mode == 1 else 0
+                nxt = (batches[k][0], batches[k][1], plans[k])
             ls.append(float(e.train_step(u, i, plan=plans[s], next_step=nxt)[0]))
         out.append((ls, [t.detach().cpu().clone() for t in e.params()], e.mt_state()))
-    assert (out[0][2] == out[1][2]).all()
-    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-5)
-    for a, b in zip(out[0][1], out[1][1]):
-        assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-12
+    for m in (1, 2):
+        assert (out[0][2] == out[m][2]).all()
+        np.testing.assert_allclose(out[m][0], out[0][0], rtol=1e-5)
+        for a, b in zip(out[0][1], out[m][1]):
+            assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-12
