@@ -68,7 +68,7 @@ struct NcfShape {
         for (int k = 1; k <= NH; ++k) u += H(k);
         return u;
     }
-    static constexpr int LDS = SW + SA + SA + P + 11 * kRows + 8;   // W, A, M(=A layout), dW, misc
+    static constexpr int LDS = SW + SA + SA + P + 13 * kRows + 8;   // W, A, M(=A layout), dW, misc
     // NeuMF extra floats: dW (M more), output GMF weights (M), GMF rows unless they fit
     // the dX region (M <= E: row stride 2E + 1 holds U_mf | I_mf)
     static constexpr int lds_neumf(int M) { return M == 0 ? LDS : LDS + 2 * M + (M <= E ? 0 : kRows * (2 * M + 1)); }
@@ -212,7 +212,9 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     int *sLi = sLu + kRows;                                   // per row: item list slot (-1: none / planned)
     int *sPs = sLi + kRows;                                   // per row: plan slot of a positive (-1: none)
     float *sX = sM + S::sa_off(0);                            // dX rows [kRows][IN0 + 1] (M_0 is unused)
-    float *sG = reinterpret_cast<float *>(sPs + kRows) + 8;   // weight-gradient accumulator (flat, P)
+    int *sUn = sPs + kRows;                                   // next tile's ids (pipelined E = 64 path)
+    int *sIn = sUn + kRows;
+    float *sG = reinterpret_cast<float *>(sIn + kRows) + 8;   // weight-gradient accumulator (flat, P)
     float *sWm = sG + P;                                      // NeuMF output weights of the GMF units
     // NeuMF GMF rows: U_mf at [r * gs], I_mf at [r * gs + M] (dX region, free until the tower's last backward)
     const int gs = M <= E ? IN0 + 1 : 2 * M + 1;
@@ -221,6 +223,16 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
     const int n = a.n_neg, NP = n + 1, tc = a.tc;
+    // E = 64 training: the next tile's pair ids are loaded at this tile's start, its list
+    // slots claimed and its A_0 rows gathered into registers during this tile's backward,
+    // so a tile starts with its inputs in hand (the id and gather phases were ~4 us of a
+    // ~26 us tile).  The small towers keep their registers for occupancy.
+    constexpr bool kPipe = kWide && kBackward;
+    constexpr int kPG = kPipe ? kRows * (IN0 / 4) / kNcfThreads : 1;   // float4 per thread of A_0
+    static_assert(!kPipe || kRows * (IN0 / 4) % kNcfThreads == 0, "A_0 prefetch shape");
+    bool pre_ok = false;                  // registers hold this tile's ids, slots and A_0
+    int nu = -1, ni = -1, nps = -1, nlu = -1, nli = -1, ncol = 0;
+    float4 pg[kPG];
 
     // ---- parameters into LDS (row stride H_k + 1), gradient accumulator zeroed ----
     for (int k = 0; k < NH; ++k) {
@@ -248,7 +260,10 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             if (valid && q == 0) valid = s < a.n_pos;
             if (valid && q > 0 && pairwise) valid = s < a.n_pos;
             int u = -1, i = -1;
-            if (valid) {
+            if (kPipe && pre_ok) {
+                u = nu;
+                i = ni;
+            } else if (valid) {
                 const int2 pr = a.pairs[s * pair_stride(a.n_neg) + q];
                 u = pr.x;
                 i = pr.y;
@@ -256,14 +271,24 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             sU[r] = u;
             sI[r] = i;
             // the example's identity for dropout: recorded-mask row, or the hash key
-            const int64_t colid = a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
+            const int64_t colid = (kPipe && pre_ok) ? (int64_t)ncol : a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
             const int64_t gj = q == 0 ? colid : (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
             sR[r] = (int)gj;
             sK[r] = hash32(a.seed ^ ((uint64_t)(q == 0 ? 0 : 1) << 40) ^ ((uint64_t)gj * 0x9E3779B97F4A7C15ULL));
             // list slots are claimed now (the entry does not depend on the gradient), so the
             // atomics' round trip overlaps the gather; overflow rows add from LDS at the end
             int lu = -1, li = -1, ps = -1;
-            if (kBackward && u >= 0) {
+            if (kPipe && pre_ok) {
+                // slots claimed during the previous tile's backward; their entries are
+                // written now that the atomics have long returned
+                lu = nlu;
+                li = nli;
+                ps = nps;
+                const int64_t ex = tile * kRows + r;
+                if (lu >= 0 && lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+                if (li >= 0 && li < kNcfCap)
+                    a.row_list[(a.num_users + i) * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+            } else if (kBackward && u >= 0) {
                 const int64_t ex = tile * kRows + r;
                 lu = atomicAdd(a.row_count + u, 1);
                 if (lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
@@ -278,10 +303,32 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             sLu[r] = lu;
             sLi[r] = li;
             sPs[r] = ps;
+            if constexpr (kPipe) {      // the next tile's record entries, consumed at backward start
+                nu = ni = -1;
+                const int64_t nt = tile + gridDim.x, s2 = nt * tc + cl;
+                bool v2 = nt < a.tiles && q < NP && s2 < a.cols;
+                if (v2 && q == 0) v2 = s2 < a.n_pos;
+                if (v2 && q > 0 && pairwise) v2 = s2 < a.n_pos;
+                if (v2) {
+                    const int2 pr = a.pairs[s2 * pair_stride(a.n_neg) + q];
+                    nu = pr.x;
+                    ni = pr.y;
+                }
+                nps = (v2 && q == 0 && a.pos_slot != nullptr) ? a.pos_slot[s2] : -1;
+                ncol = (int)(a.perm && s2 < a.cols ? (int64_t)a.perm[s2] : s2);
+            }
         }
         __syncthreads();
         NS(1);
         // ---- gather A_0 = [U[u] | I[i]] ------------------------------------------------
+        if (kPipe && pre_ok) {
+#pragma unroll
+            for (int j = 0; j < kPG; ++j) {
+                const int e = tid + j * kNcfThreads, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
+                float *d = sA + r * (IN0 + 1) + c4;
+                d[0] = pg[j].x; d[1] = pg[j].y; d[2] = pg[j].z; d[3] = pg[j].w;
+            }
+        } else
         for (int e = tid; e < kRows * (IN0 / 4); e += kNcfThreads) {
             const int r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -436,6 +483,21 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         NS(5);
         if (PHASE == kNcfLossOnly) continue;         // validation: loss only (run_val_iteration)
         // ---- backward ------------------------------------------------------------------------
+        const bool has_next = tile + gridDim.x < a.tiles;
+        if constexpr (kPipe) {
+            if (tid < kRows && has_next) {
+                const int r = tid, q = r / tc;
+                const int64_t nt = tile + gridDim.x, ex = nt * kRows + r;
+                nlu = nli = -1;
+                (void)ex;
+                if (nu >= 0) {   // entries are written at the next tile's start (results not waited on here)
+                    nlu = atomicAdd(a.row_count + nu, 1);
+                    if (!(q == 0 && a.pos_slot != nullptr)) nli = atomicAdd(a.row_count + a.num_users + ni, 1);
+                }
+                sUn[r] = nu;
+                sIn[r] = ni;
+            }
+        }
         {
             // output layer: dW_out += sum_r dz_r A_NH[r], db_out += sum_r dz_r; G_NH = dz w_out^T
             const float *wo = sW + S::sw_off(NH);
@@ -483,6 +545,19 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                 }
             }
             __syncthreads();
+        }
+        if constexpr (kPipe) {
+            if (has_next) {
+#pragma unroll
+                for (int j = 0; j < kPG; ++j) {
+                    const int e = tid + j * kNcfThreads, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
+                    const int u2 = sUn[r], i2 = sIn[r];
+                    pg[j] = u2 < 0 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
+                                   : c4 < E ? *reinterpret_cast<const float4 *>(a.user_w + (int64_t)u2 * E + c4)
+                                            : *reinterpret_cast<const float4 *>(a.item_w + (int64_t)i2 * E + (c4 - E));
+                }
+            }
+            pre_ok = has_next;
         }
         static_for<NH>([&](auto kc) {
             constexpr int k = NH - 1 - decltype(kc)::value;
