@@ -19,6 +19,9 @@ Fixtures:
                     ImplicitFactorizationModel.run_train_iteration (implicit.py:347);
                     bpr / hinge run the reference loss functions on the
                     neg.view(n, B) pairing the build defines.
+  mf_init_golden.npz
+                    torch.manual_seed(0) -> BilinearNet(U, I, d) tables (mf_spotlight.py:36-37,
+                    spotlight/layers.py:30-56, representations.py:40-60) at two sizes.
   mf_fit_golden.npz ImplicitFactorizationModel.fit over 2 epochs with
                     validation interleaving (shared random stream) + test-time
                     predict scores.
@@ -557,6 +560,23 @@ def make_gan():
     save("gan_sgd_n64.npz", **gan_case("sgd", seed=2, N=64, H=32, E=8, B=16, L=9, nb=2, d_steps=5, lr=1e-2,
                                        d_max=0.004))
     save("gan_rms_refinit.npz", **gan_case("rms", seed=3, d_steps=1))
+
+
+def make_init():
+    """the MF tables exactly as mf_spotlight.py:36-37 builds them."""
+    out = {}
+    for k, (U, I, d) in enumerate([(300, 200, 64), (943, 40, 32)]):
+        torch.manual_seed(0)
+        net = BilinearNet(U, I, d, sparse=False)
+        out[f"shape{k}"] = np.array([U, I, d], dtype=np.int64)
+        for name, t in net.state_dict().items():
+            out[f"{name}_{k}"] = t.numpy().copy()
+    save("mf_init_golden.npz", **out)
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "init":
+    make_init()
+    sys.exit(0)
 
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gan":

@@ -200,3 +200,32 @@ def test_neumf_module_init_matches_reference(golden_dir, case):
     assert [k for k, _ in net.named_parameters()] == names
     for k, p in net.named_parameters():
         assert torch.equal(p.detach(), torch.from_numpy(z["init_" + k.replace(".", "_")])), k
+
+
+def test_mf_init_matches_reference(golden_dir):
+    """torch.manual_seed(0) -> BilinearNet(U, I, d) reproduces the reference's
+    tables bit for bit (mf_spotlight.py:36-37 -> spotlight/layers.py:30-56,
+    representations.py:40-60; golden from the reference's own BilinearNet)."""
+    from recommendation_gans_amd.spotlight.factorization.representations import BilinearNet
+    z = np.load(os.path.join(golden_dir, "mf_init_golden.npz"))
+    for k in range(2):
+        U, I, d = (int(x) for x in z[f"shape{k}"])
+        torch.manual_seed(0)
+        net = BilinearNet(U, I, d, sparse=False)
+        sd = net.state_dict()
+        assert list(sd) == ["user_embeddings.weight", "item_embeddings.weight", "user_biases.weight",
+                            "item_biases.weight"]
+        for name, t in sd.items():
+            assert torch.equal(t, torch.from_numpy(z[f"{name}_{k}"])), (k, name)
+
+
+def test_mf_cli_init_order(tmp_path, monkeypatch):
+    """The CLI's data provider draws no torch random numbers between torch.manual_seed(0)
+    and BilinearNet (mf_spotlight.py:36-57), so the CLI's tables are the golden init."""
+    from recommendation_gans_amd.utils.data_provider import data_provider
+    monkeypatch.chdir(tmp_path)
+    torch.manual_seed(0)
+    before = torch.get_rng_state().clone()
+    loader = data_provider("datasets/movielens/", "100K", 5, movies_to_keep=-1, synthetic=True)
+    loader.get_timebased_data()
+    assert torch.equal(torch.get_rng_state(), before)
