@@ -246,6 +246,22 @@ int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t
                         int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss, const rg_mf_batch_t *next,
                         const rg_mf_work_t *next_work);
 
+/* An MT19937 walk to run inside another launch (one extra workgroup): advances
+ * `state` (CPython getstate()[1] layout, device) by nwords raw words into out
+ * (nwords + RG_MT_PAD words), copying the entry state to state_before (optional) --
+ * rg_mt_generate's work, without a launch or stream of its own. */
+typedef struct rg_mt_gen {
+    uint32_t *state, *out, *state_before;
+    int64_t nwords;                 /* 0: no walk */
+} rg_mt_gen_t;
+
+/* rg_mf_apply_prepare plus, in one more workgroup of the same launch, the MT walk of a
+ * later step's words (gen may be null).  The single-GPU native step uses it so the
+ * sampler stream needs neither a generator stream nor a per-step event. */
+int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
+                            int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
+                            const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mt_gen_t *gen);
+
 /* Pull the DATA gradient (no weight decay) of the rows in range into the flat
  * buffer grad_dev = [n*dim row grads | n bias grads | loss], n = row_end - row_begin
  * (the loss slot is written when loss->out is non-null).  Resets the lists like

@@ -73,6 +73,11 @@ class Opt(ctypes.Structure):
                 ("bias_correction2_sqrt", ctypes.c_float)]
 
 
+class MTGen(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_void_p), ("out", ctypes.c_void_p), ("state_before", ctypes.c_void_p),
+                ("nwords", ctypes.c_int64)]
+
+
 class MFStepperConfig(ctypes.Structure):
     _fields_ = [("tables", MFTables * 2), ("work", MFWork), ("mt_state", ctypes.c_void_p),
                 ("pairs", ctypes.c_void_p * 2),
@@ -202,6 +207,10 @@ SIGNATURES = [
     ("rg_mf_apply_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
                                            ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss),
                                            ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
+    ("rg_mf_apply_prepare_gen", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                               ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64,
+                                               ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch),
+                                               ctypes.POINTER(MFWork), ctypes.POINTER(MTGen)]),
     ("rg_mf_step_front", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
                                         ctypes.POINTER(MFWork), ctypes.POINTER(MFMark), ctypes.POINTER(Opt),
                                         ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFBatch),

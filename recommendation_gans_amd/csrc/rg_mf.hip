@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "rg_common.h"
+#include "rg_mt.h"
 
 namespace rg {
 
@@ -709,10 +710,27 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
 // the dense update of rows [row_begin, row_end) (blocks [0, apply_blocks), as
 // mf_apply_kernel) and the prepare pass of the NEXT step (the remaining blocks) in one
 // launch: the split step then needs no side stream and no per-step cross-stream event
+// Optional: workgroup 0 walks a LATER step's MT19937 words (rg_mt_gen_t) -- the walk
+// (~0.47 ns/word, one workgroup) hides under the HBM-bound pass, so a single-GPU step
+// needs no generator stream and no cross-stream event.
+struct MtGenArgs {
+    uint32_t *state, *out, *state_before;
+    int64_t nwords;
+};
+
 template <class L, int NT, bool SPEC = false>
 __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
-                                                        int64_t apply_blocks) {
-    const int64_t blk = blockIdx.x;
+                                                        int64_t apply_blocks, MtGenArgs gen) {
+    static_assert(kBlock == kGenThreads, "the MT walk runs on one full workgroup");
+    int64_t blk = blockIdx.x;
+    if (gen.nwords > 0) {
+        if (blk == 0) {
+            __shared__ uint32_t X[kRing + 2];
+            mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
+            return;
+        }
+        --blk;
+    }
     if (blk >= apply_blocks) {
         prepare_one(prep, prep_out, (blk - apply_blocks) * kBlock + threadIdx.x);
         return;
@@ -1231,6 +1249,7 @@ struct BackLaunchF {
     PairsArgs *prep;
     int2 *prep_out;
     int64_t prep_blocks;
+    MtGenArgs gen;
     hipStream_t s;
     template <class L>
     int operator()() {
@@ -1238,19 +1257,19 @@ struct BackLaunchF {
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
-        const dim3 grid((unsigned)(nb + prep_blocks));
+        const dim3 grid((unsigned)(nb + prep_blocks + (gen.nwords > 0 ? 1 : 0)));
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
         // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
         // RG_APPLY_SPEC=0 turns it off)
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
         if (spec)
-            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
         else if (nt == 1)
-            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
         else if (nt >= 2)
-            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
         else
-            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb);
+            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
         return check_launch("rg_mf_apply_prepare");
     }
 };
@@ -1259,6 +1278,18 @@ struct BackLaunchF {
 extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
                                    int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
                                    const rg_mf_batch_t *next, const rg_mf_work_t *next_w) {
+    return rg_mf_apply_prepare_gen(stream, t, w, opt, row_begin, row_end, loss, next, next_w, nullptr);
+}
+
+extern "C" int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                                       int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
+                                       const rg_mf_batch_t *next, const rg_mf_work_t *next_w,
+                                       const rg_mt_gen_t *gen) {
+    MtGenArgs g{};
+    if (gen && gen->nwords > 0) {
+        if (!gen->state || !gen->out) return fail_arg("rg_mf_apply_prepare_gen: null MT state / output");
+        g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
+    }
     ApplyArgs a;
     int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull, a);
     if (rc) return rc;
@@ -1270,7 +1301,7 @@ extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_
         prep_out = reinterpret_cast<int2 *>(next->pairs);
         prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
-    BackLaunchF f{&a, &prep, prep_out, prep_blocks, (hipStream_t)stream};
+    BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
 

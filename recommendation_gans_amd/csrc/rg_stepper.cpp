@@ -4,7 +4,8 @@
 // (implicit.py:290-298 -> run_train_iteration :347-364) so that one call per step
 // enqueues everything, without per-step Python/ctypes overhead.
 //
-// Word stream.  The words a step consumes do not depend on the step's input: draw
+// Word stream (default for a single-GPU split step: the inline walk below).  The words a
+// step consumes do not depend on the step's input: draw
 // j of any consumer (training step or validation batch) is just the next 2 words
 // of CPython's stream, and every consumer of this stepper takes the same number of
 // words W = 2 * n_neg * global_cols (one "unit").  The stream is cut into ring
@@ -14,6 +15,13 @@
 // launch and two events per G steps).  The state CPython would hold after the
 // consumed units is the start state of their slot advanced by the units consumed
 // inside it (rg_mf_stepper_sync_mt).
+//
+// Inline walk (split step, one GPU, when the walk hides under the dense pass): slots of
+// one unit; the words of unit t+2 are walked by one extra workgroup of step t's dense
+// pass (rg_mf_apply_prepare_gen), so the steady state has no generator launch and no
+// event: the generator stream only makes up for gaps (the first two units, validation
+// consumers that ran ahead).  Events between streams are recorded lazily, when a
+// different stream has to be ordered after a production or a consumer.
 //
 // Overlapped step (RG_FUSED=1; pointwise / bpr / hinge; measured slower):
 //   main  rg_mf_step_front(pairs of t | marked prepare of t+1 | cold-row update of t)
@@ -54,15 +62,25 @@ struct Stepper {
     uint32_t *start_state[kSlots] = {nullptr, nullptr, nullptr};   // [625] state before the slot
     hipEvent_t gen_done[kSlots] = {nullptr, nullptr, nullptr};
     hipEvent_t consumed[kSlots] = {nullptr, nullptr, nullptr};     // after the slot's last consumer
-    bool consumed_valid[kSlots] = {false, false, false};
+    // Who produced / has seen / last consumed each slot.  Events are recorded lazily,
+    // only when a DIFFERENT stream has to be ordered after that work (same-stream
+    // order is free): the single-GPU split step then issues no event at all.
+    // (a null hipStream_t is the legacy default stream, a real consumer: validity is tracked
+    // by flags, never by null handles)
+    hipStream_t prod[kSlots] = {nullptr, nullptr, nullptr};        // producing stream
+    bool gen_rec[kSlots] = {false, false, false};                  // gen_done recorded after the production
+    hipStream_t seen[kSlots] = {nullptr, nullptr, nullptr};        // a stream ordered after the production
+    bool seen_ok[kSlots] = {false, false, false};
+    hipStream_t cons_on[kSlots] = {nullptr, nullptr, nullptr};     // stream of the last consumer
+    bool cons_ok[kSlots] = {false, false, false};                  // the slot was consumed since its production
+    bool cons_rec[kSlots] = {false, false, false};                 // consumed recorded after that consumer
+    bool inline_gen = false;              // split step: the walk of unit t+2 rides in step t's dense pass
     hipEvent_t ready[2] = {nullptr, nullptr};                      // side-stream prepared pairs buffers
     bool side_pending[2] = {false, false};                         // ready[b] not yet waited by the consumer
     hipEvent_t mark = nullptr;                                     // consumer-stream point a side prepare follows
     int64_t unit_base = 0;                // unit of relative slot 0 (reset when the state is loaded)
     int64_t gen_slots = 0;                // relative slots generated
     int64_t taken = 0;                    // units consumed
-    hipStream_t waited_stream = nullptr;  // the consumer stream has waited for gen_done of slots <= waited_slot
-    int64_t waited_slot = -1;
     // prepared pairs of unit prep_unit for input prep_in, in pairs buffer prep_unit % 2
     bool prepared = false;
     int64_t prep_unit = -1;
@@ -130,32 +148,81 @@ bool same_input(const rg_mf_step_in_t &a, const rg_mf_step_in_t &b) {
     return std::memcmp(&a, &b, sizeof(a)) == 0;
 }
 
+// `stream` is ordered after the production of `slot` (an event wait only across streams)
+int see(Stepper &st, hipStream_t stream, int slot) {
+    if ((st.seen_ok[slot] && st.seen[slot] == stream) || st.prod[slot] == stream) {
+        st.seen[slot] = stream;
+        st.seen_ok[slot] = true;
+        return RG_OK;
+    }
+    hipError_t e = hipSuccess;
+    if (!st.gen_rec[slot]) {
+        e = hipEventRecord(st.gen_done[slot], st.prod[slot]);
+        st.gen_rec[slot] = true;
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, st.gen_done[slot], 0);
+    if (e != hipSuccess) return hip_fail("stepper: wait gen", e);
+    st.seen[slot] = stream;
+    st.seen_ok[slot] = true;
+    return RG_OK;
+}
+
+// producer stream `p` may overwrite `slot`: ordered after the slot's last consumer
+int free_for(Stepper &st, hipStream_t p, int slot) {
+    if (!st.cons_ok[slot] || st.cons_on[slot] == p) return RG_OK;
+    hipError_t e = hipSuccess;
+    if (!st.cons_rec[slot]) {
+        e = hipEventRecord(st.consumed[slot], st.cons_on[slot]);
+        st.cons_rec[slot] = true;
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(p, st.consumed[slot], 0);
+    return e == hipSuccess ? RG_OK : hip_fail("stepper: wait consumed", e);
+}
+
+// bookkeeping of a slot production enqueued on `p` (the walk advances the one MT state,
+// so productions are ordered: a production on another stream than the previous one waits)
+int begin_production(Stepper &st, hipStream_t p, int slot) {
+    int rc = free_for(st, p, slot);
+    if (rc) return rc;
+    if (st.gen_slots > 0 && (rc = see(st, p, (int)((st.gen_slots - 1) % kSlots)))) return rc;
+    st.win_at[slot] = st.window_form;
+    st.pos_at[slot] = st.cp_pos;
+    return RG_OK;
+}
+
+void end_production(Stepper &st, hipStream_t p, int slot) {
+    st.cp_pos = (int32_t)((st.cp_pos + st.G * st.W - 1) % 624 + 1);
+    st.prod[slot] = p;
+    st.gen_rec[slot] = false;
+    st.seen[slot] = p;
+    st.seen_ok[slot] = true;
+    st.cons_ok[slot] = false;
+    st.cons_rec[slot] = false;
+    ++st.gen_slots;
+}
+
 // generate the next ring slot (G units) on the gen stream
 int generate_one(Stepper &st) {
     const int slot = (int)(st.gen_slots % kSlots);
-    hipError_t e;
-    if (st.consumed_valid[slot] && (e = hipStreamWaitEvent(st.gen, st.consumed[slot], 0)) != hipSuccess)
-        return hip_fail("stepper: wait consumed", e);
-    st.win_at[slot] = st.window_form;
-    st.pos_at[slot] = st.cp_pos;
-    const int64_t nwords = st.G * st.W;
-    int rc;
+    int rc = begin_production(st, st.gen, slot);
+    if (rc) return rc;
     if (st.jump) {
         rc = rg::mt_produce_jump(st.gen, *st.jump, st.cfg.mt_state, st.words[slot], st.start_state[slot]);
         st.window_form = true;
     } else {
-        rc = rg_mt_generate(st.gen, st.cfg.mt_state, st.words[slot], nwords, st.start_state[slot]);
+        rc = rg_mt_generate(st.gen, st.cfg.mt_state, st.words[slot], st.G * st.W, st.start_state[slot]);
     }
     if (rc) return rc;
-    st.cp_pos = (int32_t)((st.cp_pos + nwords - 1) % 624 + 1);
-    if ((e = hipEventRecord(st.gen_done[slot], st.gen)) != hipSuccess) return hip_fail("stepper: record gen", e);
-    ++st.gen_slots;
+    end_production(st, st.gen, slot);
+    hipError_t e = hipEventRecord(st.gen_done[slot], st.gen);
+    if (e != hipSuccess) return hip_fail("stepper: record gen", e);
+    st.gen_rec[slot] = true;
     return RG_OK;
 }
 
-// slots up to the one holding `unit`, plus kAheadSlots more, are generated (or queued)
-int keep_ahead(Stepper &st, int64_t unit) {
-    const int64_t upto = rel_slot(st, unit) + 1 + kAheadSlots;
+// slots up to the one holding `unit` (+ `ahead` more) are generated or queued
+int generate_upto(Stepper &st, int64_t unit, int ahead) {
+    const int64_t upto = rel_slot(st, unit) + 1 + ahead;
     while (st.gen_slots < upto) {
         int rc = generate_one(st);
         if (rc) return rc;
@@ -163,15 +230,11 @@ int keep_ahead(Stepper &st, int64_t unit) {
     return RG_OK;
 }
 
-// make the words of `unit` visible to `stream` (one event wait per slot and stream)
+int keep_ahead(Stepper &st, int64_t unit) { return generate_upto(st, unit, kAheadSlots); }
+
+// make the words of `unit` visible to `stream`
 int wait_words(Stepper &st, hipStream_t stream, int64_t unit) {
-    const int64_t rel = rel_slot(st, unit);
-    if (st.waited_stream == stream && st.waited_slot >= rel) return RG_OK;
-    hipError_t e = hipStreamWaitEvent(stream, st.gen_done[rel % kSlots], 0);
-    if (e != hipSuccess) return hip_fail("stepper: wait gen", e);
-    st.waited_stream = stream;
-    st.waited_slot = rel;
-    return RG_OK;
+    return see(st, stream, (int)(rel_slot(st, unit) % kSlots));
 }
 
 // an outstanding side-stream write of pairs buffer b must land before `stream` uses it
@@ -191,8 +254,8 @@ int prepare_side(Stepper &st, hipStream_t consumer, int64_t unit, const rg_mf_st
     if (rc) return rc;
     hipError_t e = hipEventRecord(st.mark, consumer);
     if (e == hipSuccess) e = hipStreamWaitEvent(st.prep, st.mark, 0);
-    if (e == hipSuccess) e = hipStreamWaitEvent(st.prep, st.gen_done[rel_slot(st, unit) % kSlots], 0);
     if (e != hipSuccess) return hip_fail("stepper: order prepare", e);
+    if ((rc = wait_words(st, st.prep, unit))) return rc;
     const rg_mf_work_t w = work_for(st, in);
     const rg_mf_batch_t batch = make_batch(st, in, unit);
     if ((rc = rg_mf_prepare(st.prep, &batch, &w))) return rc;
@@ -239,11 +302,11 @@ int release(Stepper &st, hipStream_t stream) {
     if (st.prepared && st.prep_unit < st.taken) st.prepared = false;
     if ((rel + 1) % st.G == 0) {                         // the slot's last unit
         const int slot = (int)((rel / st.G) % kSlots);
-        hipError_t e = hipEventRecord(st.consumed[slot], stream);
-        if (e != hipSuccess) return hip_fail("stepper: record consumed", e);
-        st.consumed_valid[slot] = true;
+        st.cons_on[slot] = stream;                       // its event is recorded when a producer needs it
+        st.cons_ok[slot] = true;
+        st.cons_rec[slot] = false;
     }
-    return keep_ahead(st, st.taken);
+    return st.inline_gen ? RG_OK : keep_ahead(st, st.taken);
 }
 
 // words + pairs of unit `taken` for `in`, visible to `stream` (split-step consumers)
@@ -308,7 +371,9 @@ int record(void *ev, hipStream_t s) {
 int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
                 float *loss_out, void *ev0, void *ev1) {
     const int64_t unit = st.taken;
-    int rc = keep_ahead(st, unit);
+    // inline: units t, t+1 must exist (the gen stream makes up for any gap, e.g. after a
+    // validation pass); unit t+2 is walked inside this step's dense pass
+    int rc = st.inline_gen ? generate_upto(st, unit + 1, 0) : keep_ahead(st, unit);
     if (rc) return rc;
     rg_mf_work_t w = work_for(st, cur);
     const rg_mf_batch_t batch = make_batch(st, cur, unit);
@@ -328,11 +393,21 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     rg_mf_batch_t nbatch{};
     rg_mf_work_t nw{};
     if (next) {
-        if ((rc = keep_ahead(st, unit + 1))) return rc;
+        if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
         if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
         if ((rc = wait_words(st, s, unit + 1))) return rc;
         nbatch = make_batch(st, *next, unit + 1);
         nw = work_for(st, *next);
+    }
+    rg_mt_gen_t gen{};
+    int gen_slot = -1;
+    if (st.inline_gen && !st.cfg.item_grad && st.gen_slots == rel_slot(st, unit + 2)) {
+        gen_slot = (int)(st.gen_slots % kSlots);
+        if ((rc = begin_production(st, s, gen_slot))) return rc;
+        gen.state = st.cfg.mt_state;
+        gen.out = st.words[gen_slot];
+        gen.state_before = st.start_state[gen_slot];
+        gen.nwords = st.G * st.W;
     }
     st.cfg.step += 1;
     const rg_opt_t o = opt_at(st, st.cfg.step);
@@ -345,9 +420,10 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
             return rc;
     }
     if ((rc = record(ev0, s))) return rc;
-    if ((rc = rg_mf_apply_prepare(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
-                                  next ? &nbatch : nullptr, next ? &nw : nullptr)))
+    if ((rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
+                                      next ? &nbatch : nullptr, next ? &nw : nullptr, gen_slot >= 0 ? &gen : nullptr)))
         return rc;
+    if (gen_slot >= 0) end_production(st, s, gen_slot);
     if ((rc = record(ev1, s))) return rc;
     if (st.cfg.item_grad) {
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
@@ -470,13 +546,24 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->set = cfg->current_set;
     st->W = 2 * (int64_t)cfg->n_neg * cfg->global_cols;
     if (st->cfg.neg_cols <= 0) st->cfg.neg_cols = cfg->global_cols;
+    st->fused = env_flag("RG_FUSED", false);
     {
+        // inline walk (default): one unit per slot, walked inside the dense pass two steps
+        // ahead, when the walk (~0.47 ns/word on one workgroup) hides under that pass
+        // (~5 TB/s over p, m, v of every row); otherwise 8-unit slots on the gen stream
+        const rg_mf_tables_t &t = cfg->tables[0];
+        const double walk_us = 0.47e-3 * (double)st->W;
+        const double dense_us = 6.0 * (double)(t.num_users + t.num_items) * (4.0 * t.dim + 4.0) / 5.0e6;
+        // RG_MT_INLINE: 0 off, 1 (default) when it hides, 2 always (tests at small sizes)
+        const char *im = getenv("RG_MT_INLINE");
+        const int mode = im ? atoi(im) : 1;
+        st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
+                         (mode == 2 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
-        st->G = g ? atoi(g) : 8;
+        st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
         if (st->G < 1) st->G = 1;
         if (st->G > 64) st->G = 64;
     }
-    st->fused = env_flag("RG_FUSED", false);
     st->hot_scan = env_flag("RG_HOT_SCAN", true);
     // separate priorities keep the streams on separate hardware queues: the walk is
     // background work (lowest), the short side prepare is on the step's path (highest)
@@ -606,8 +693,10 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
     // host -> device: words generated ahead are dropped; unit numbering restarts here
     st->unit_base = st->taken;
     st->gen_slots = 0;
-    st->waited_slot = -1;
-    st->waited_stream = nullptr;
+    for (int i = 0; i < kSlots; ++i) {
+        st->prod[i] = st->seen[i] = st->cons_on[i] = nullptr;
+        st->gen_rec[i] = st->cons_rec[i] = st->seen_ok[i] = st->cons_ok[i] = false;
+    }
     st->prepared = false;
     st->window_form = false;
     st->cp_pos = (int32_t)host_state[624];

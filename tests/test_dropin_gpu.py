@@ -22,8 +22,12 @@ from oracle import mf as omf
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("inline", ["1", "2"])
 @pytest.mark.parametrize("loss", ["pointwise", "adaptive_hinge"])
-def test_fit_matches_reference_golden(golden_dir, tmp_path, monkeypatch, loss):
+def test_fit_matches_reference_golden(golden_dir, tmp_path, monkeypatch, loss, inline):
+    """inline "2" forces the stepper's inline MT walk (words of step t+2 walked inside step t's
+    dense pass) at this small size, mixed with the generator stream that validation uses."""
+    monkeypatch.setenv("RG_MT_INLINE", inline)
     from recommendation_gans_amd.implicit import ImplicitFactorizationModel
     from recommendation_gans_amd.spotlight import optimizers
     from recommendation_gans_amd.spotlight.factorization.representations import BilinearNet

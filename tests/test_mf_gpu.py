@@ -425,7 +425,7 @@ def test_large_full_size_properties(dev):
     assert (e.mt_state() == st).all()
 
 
-@pytest.mark.parametrize("jump", [0, 1])
+@pytest.mark.parametrize("jump", [0, 1, "inline"])
 @pytest.mark.parametrize("n", [5, 8])
 def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
     """Full-size steps through the stepper's word ring (chunks generated two steps
@@ -435,7 +435,9 @@ def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
     export and re-import of the state: negative pairs bit-exact, MT state exact,
     losses/tables as the oracle."""
     from recommendation_gans_amd.mf_engine import MFEngine
-    monkeypatch.setenv("RG_MT_JUMP", str(jump))
+    # "inline": one-unit slots, unit t+2 walked inside step t's dense pass (forced at this size)
+    monkeypatch.setenv("RG_MT_JUMP", "1" if jump == 1 else "0")
+    monkeypatch.setenv("RG_MT_INLINE", "2" if jump == "inline" else "0")
     U, I, d, B = 300, 200, 16, 8192
     g = torch.Generator().manual_seed(3)
     tabs = [torch.randn(U, d, generator=g) / d, torch.randn(I, d, generator=g) / d,
