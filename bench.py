@@ -14,11 +14,14 @@ update and the next step's prepare in one launch); RG_FUSED=1 selects the
 overlapped two-launch step (rg_mf_step_front + rg_mf_step_hot, measured slower).
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
-With N > 1 ranks (one process per GPU) the step is user-sharded
-(recommendation_gans_amd/sharding.py): rank r owns users u % N == r (rows,
-optimizer state, positives, pool entries, its own MT stream), items are
-replicated and their gradient is all-reduced with RCCL inside the native step,
-overlapped with the user-shard update.
+With N > 1 ranks (one process per GPU) the default is the reference-exact
+replicated step: global batch N*B, rank r takes columns [r*B, (r+1)*B)
+of it and of ONE global negative draw over the full pool, the rank-major gradient
+is reduce-scattered with RCCL, each rank updates its row shard (p, m, v), the tables
+are all-gathered -- N ranks compute exactly the reference's step at batch N*B.
+--dp user_shard selects the faster user-sharded opt-in (sharding.py: rank r owns
+users u % N == r, its own positives, sub-pool and MT stream; item gradient
+all-reduce), which is NOT the reference's sampling at N > 1.
 
 Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
 max over ranks of the timed wall time.  `roofline` is for the dominant kernel
@@ -77,6 +80,12 @@ def parse():
     ap.add_argument("--gan-hidden", type=int, default=256)
     ap.add_argument("--gan-slate", type=int, default=5)
     ap.add_argument("--gan-emb", type=int, default=5)
+    ap.add_argument("--dp", default="global_stream", choices=["global_stream", "user_shard"],
+                    help="multi-GPU layout (N > 1): global_stream = reference-exact replicated step "
+                         "(reduce-scatter + all-gather); user_shard = user-sharded opt-in (not the reference's "
+                         "sampling at N > 1)")
+    ap.add_argument("--dp-at-1", action="store_true",
+                    help="run the replicated DP code path at N = 1 too (identity exchange; bench-path check)")
     ap.add_argument("--events-every", type=int, default=8,
                     help="record the dominant kernel's timing events on every k-th timed step")
     return ap.parse_args()
@@ -466,25 +475,45 @@ def main():
     if world > 1:
         from recommendation_gans_amd.comm import RcclComm
         comm = RcclComm(dev)
-    pool_u, pool_i = sharding.shard_pool(data.pool_u, data.pool_i, rank, world)
-    train_u, train_i = sharding.shard_interactions(data.train_u, data.train_i, rank, world)
-    U_local = sharding.num_local_users(U, rank, world)
-    eng = MFEngine(sharding.shard_rows(Uw, rank, world), Iw, torch.zeros(U_local), torch.zeros(I), pool_u, pool_i,
-                   sharding.rank_mt_state(mt, rank), loss=args.loss, optimizer=args.optim, lr=1e-3,
-                   weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, rank=rank, world_size=world,
-                   prefetch=not args.no_prefetch, comm=comm)
+    gs = args.dp == "global_stream" and (world > 1 or args.dp_at_1)
+    if gs:
+        # replicated, reference-exact: full tables / pool on every rank, global batches of
+        # B * world positives, this rank's columns [rank*B, (rank+1)*B) of each
+        eng = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), data.pool_u, data.pool_i, mt, loss=args.loss,
+                       optimizer=args.optim, lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev,
+                       rank=rank, world_size=world, dp="global_stream", prefetch=not args.no_prefetch, comm=comm)
+        train_u, train_i = data.train_u, data.train_i
+        U_local = U
+        gb = B * world
+        nbatches = len(train_u) // gb
+        batch_lo = [g * gb + rank * B for g in range(nbatches)]
+    else:
+        pool_u, pool_i = sharding.shard_pool(data.pool_u, data.pool_i, rank, world)
+        train_u, train_i = sharding.shard_interactions(data.train_u, data.train_i, rank, world)
+        U_local = sharding.num_local_users(U, rank, world)
+        eng = MFEngine(sharding.shard_rows(Uw, rank, world), Iw, torch.zeros(U_local), torch.zeros(I), pool_u,
+                       pool_i, sharding.rank_mt_state(mt, rank), loss=args.loss, optimizer=args.optim, lr=1e-3,
+                       weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, rank=rank, world_size=world,
+                       dp="user_shard" if world > 1 else None, prefetch=not args.no_prefetch, comm=comm)
+        gb = B * world
+        nbatches = len(train_u) // B
+        batch_lo = [g * B for g in range(nbatches)]
     tu = torch.from_numpy(train_u).to(dev)
     ti = torch.from_numpy(train_i).to(dev)
-    gb = B * world
-    nbatches = len(train_u) // B
     # per-batch plans: the epoch order is fixed for the whole fit (implicit.py:262), so
-    # they are built once, before timing (like the reference's own data preparation)
+    # they are built once per fit, before timing (like the reference's own data
+    # preparation); their cost is measured and reported beside the step
     nplan = min(nbatches, args.warmup + args.steps)
-    plans = [eng.make_plan(ti[g * B:g * B + B]) for g in range(nplan)]
+    torch.cuda.synchronize()
+    tp0 = time.perf_counter()
+    plans = [eng.make_plan(ti[batch_lo[g]:batch_lo[g] + B]) for g in range(nplan)]
+    torch.cuda.synchronize()
+    plan_us = (time.perf_counter() - tp0) / nplan * 1e6
 
     def batch(s):
         g = s % nbatches
-        return tu[g * B:g * B + B], ti[g * B:g * B + B], plans[g % nplan]
+        lo = batch_lo[g]
+        return tu[lo:lo + B], ti[lo:lo + B], plans[g % nplan]
 
     # step inputs (ids + plan pointers) built before timing; each call also hands the
     # NEXT step's input to the native stepper, which generates its words ahead
@@ -533,7 +562,13 @@ def main():
                        f"pool {len(data.pool_u)} uniform pairs; tables N(0,1/d) init",
                "config": {"workload": f"MF-{args.loss.upper()} ML-20M-shaped, embedding_dim={d}, "
                                       f"batch {B}/GPU, {n} negatives, {args.optim} (coupled L2 1e-5) over all rows",
-                          "global_batch": gb, "embedding_dim": d, "parallelism": f"dp{world}"}}
+                          "global_batch": gb, "embedding_dim": d,
+                          "parallelism": f"dp{world}" + ("" if world == 1 else
+                                                         " replicated (reduce-scatter + all-gather, reference-exact)"
+                                                         if gs else " user-sharded (opt-in, not reference sampling)")},
+               "plan_build_us_per_batch": plan_us,
+               "plan_build_note": "item-sorted plan of one batch (torch ops), built once per fit for every batch "
+                                  "(the reference shuffles once, implicit.py:262); not in the timed region"}
         step_bytes = gather + ids + adam
         out["step_roofline"] = {"bytes_per_step": step_bytes,
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
@@ -543,7 +578,11 @@ def main():
             from recommendation_gans_amd import _lib
             ms = [_lib.elapsed_ms(a, b) for a, b in (ev for ev in evs if ev is not None)]
             avg = float(np.mean(ms)) * 1e-3
-            if fused:
+            if gs:
+                # rg_mf_grads_sharded: every row's pulled gradient written rank-major (the exchange's input)
+                alg = gather + world * eng.chunk * 4
+                kname = "rg_mf_grads_sharded (mf_apply_kernel<kGradOnly>, rank-major gradient for the reduce-scatter)"
+            elif fused:
                 # the events bracket rg_mf_step_front (pairs | next prepare | cold-row update)
                 # and rg_mf_step_hot (touched-row update): the whole step's algorithmic bytes
                 # (DP: up to the user-shard update; the item update follows the exchange)

@@ -269,6 +269,25 @@ int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *tables, rg_mf_wo
 int rg_mf_grads(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, float *grad_dev,
                 int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss);
 
+/* Replicated data-parallel step (one process per GPU, every rank holds every row;
+ * the reference-exact layout of SURVEY §8e): the flat gradient is RANK-MAJOR so that
+ * ncclReduceScatter hands rank s the summed gradient of exactly its row shard --
+ * chunk s (rg_mf_grad_chunk floats, a multiple of 4) holds
+ *   [user rows s*Us .. (s+1)*Us | item rows s*Is .. (s+1)*Is] (dim floats each),
+ *   their biases (Us + Is), the loss;
+ * Us * world >= num_users, Is * world >= num_items (rows past the tables stay zero).
+ * rg_mf_grads_sharded pulls every row's data gradient (the lists of rg_mf_pairs) into
+ * that layout and writes this rank's loss share into every chunk's loss slot (the
+ * reduce-scatter sums it); rg_mf_apply_shard updates rank `rank`'s rows from its
+ * (summed) chunk into the *_out tables; an all-gather of the four *_out tables
+ * (counts Us*dim, Is*dim, Us, Is; tables allocated with world*Us / world*Is rows)
+ * completes the step. */
+int64_t rg_mf_grad_chunk(int64_t shard_users, int64_t shard_items, int32_t dim);
+int rg_mf_grads_sharded(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, float *grad_dev,
+                        int64_t shard_users, int64_t shard_items, int32_t world, const rg_mf_loss_t *loss);
+int rg_mf_apply_shard(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
+                      int64_t shard_users, int64_t shard_items, int32_t world, int32_t rank, float *loss_out_dev);
+
 /* Optimizer update of the rows in range from a (summed) flat gradient
  * (+ weight_decay * p).  loss_out_dev (optional) receives grad_dev's loss slot. */
 int rg_mf_apply_dense(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
@@ -295,6 +314,12 @@ int rg_comm_destroy(void *comm);
 /* In-place sum over ranks, stream-ordered with respect to `stream` (runs on the
  * communicator's own stream between two events). */
 int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf_dev, int64_t n);
+/* In-place reduce-scatter (sum): rank r receives the sum of every rank's chunk r at
+ * buf_dev + r * chunk.  On `stream` itself. */
+int rg_comm_reduce_scatter_f32(void *comm, void *stream, float *buf_dev, int64_t chunk);
+/* In-place all-gather of n buffers in one group: rank r's counts[k] floats at
+ * bufs[k] + r * counts[k] go to every rank.  On `stream` itself. */
+int rg_comm_allgather_f32(void *comm, void *stream, int32_t n, float *const *bufs_dev, const int64_t *counts);
 
 /* ------------------------------------------------------------------------------
  * Native step runtime (rg_stepper.cpp): one call per training step enqueues
@@ -327,6 +352,13 @@ typedef struct rg_mf_stepper_config {
     int64_t step;                   /* optimizer steps already taken */
     int64_t n_partials;
     int32_t current_set, pad_;
+    /* dp_mode 1: the replicated, reference-exact data-parallel step (rg_mf_grads_sharded ->
+     * reduce-scatter -> rg_mf_apply_shard -> all-gather), rank `rank` of `world`; every rank
+     * consumes columns [col_offset, col_offset + cols) of one global draw of global_cols
+     * columns.  grad_buf: [world * rg_mf_grad_chunk(shard_users, shard_items, dim)]. */
+    int32_t dp_mode, rank, world, pad2_;
+    int64_t shard_users, shard_items;
+    float *grad_buf;
 } rg_mf_stepper_config_t;
 
 typedef struct rg_mf_step_in {
@@ -352,6 +384,15 @@ int rg_mf_stepper_release(void *stepper, void *stream);
  * (ordered after the work `stream` holds), so the next acquire with the same input finds
  * them ready.  A different input there prepares again. */
 int rg_mf_stepper_prefetch(void *stepper, void *stream, const rg_mf_step_in_t *next);
+/* The replicated data-parallel step (dp_mode 1) in two halves around a caller-run
+ * exchange (comm == NULL; tests, gloo): dp_begin = prepare / pairs / release / the next
+ * step's prepare / rg_mf_grads_sharded into grad_buf; the caller reduce-scatters grad_buf;
+ * dp_end = rg_mf_apply_shard of this rank's chunk + flip of the table sets; the caller
+ * then all-gathers the four current tables.  With a communicator rg_mf_stepper_train
+ * runs both halves and both collectives itself. */
+int rg_mf_stepper_dp_begin(void *stepper, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
+                           float *loss_out_dev);
+int rg_mf_stepper_dp_end(void *stepper, void *stream, float *loss_out_dev);
 /* Optimizer scalars for optimizer step `step` (1-based). */
 int rg_mf_stepper_opt(void *stepper, int64_t step, rg_opt_t *opt_out);
 int rg_mf_stepper_state(void *stepper, int32_t *current_set, int64_t *step);

@@ -212,6 +212,33 @@ class MFOracle:
         return float(loss)
 
 
+def step_columns(oracle, pos_u, pos_i, col_offset, global_cols, global_pos, exchange):
+    """One rank's share of the replicated data-parallel step: the step of a
+    single process at batch ``global_cols`` (implicit.py:347-364), cut by columns.
+
+    The draw is the global one -- k = n * global_cols indices from the full pool
+    (implicit.py:351-354), viewed as (n, global_cols) -- and this rank keeps columns
+    [col_offset, col_offset + batch_size) with its positives ``pos_u/pos_i`` (the same
+    columns of the global batch); loss means run over the global batch
+    (``global_pos`` positives, n * global_cols negatives); ``exchange(grads)`` sums the
+    dense gradients over ranks before the (replicated) optimizer update."""
+    U, I, ub, ib = oracle.params
+    n, B = oracle.n, oracle.batch_size
+    pos_u = torch.as_tensor(pos_u).long()
+    pos_i = torch.as_tensor(pos_i).long()
+    p_pos = scores(U, I, ub, ib, pos_u, pos_i)
+    idx, nu, ni = oracle.draw(n * global_cols)
+    cols = slice(col_offset, col_offset + B)
+    nu = nu.view(n, global_cols)[:, cols].reshape(-1)
+    ni = ni.view(n, global_cols)[:, cols].reshape(-1)
+    p_neg = scores(U, I, ub, ib, nu, ni)
+    loss, dpp, dpn = loss_and_dp(oracle.loss_kind, p_pos, p_neg, n, B, den=(global_pos, n * global_cols))
+    dz = torch.cat([dpp * (1.0 - p_pos) * p_pos, dpn * (1.0 - p_neg) * p_neg])
+    grads = exchange(dense_grads(U, I, ub, ib, torch.cat([pos_u, nu]), torch.cat([pos_i, ni]), dz))
+    oracle.opt.step(oracle.params, grads)
+    return float(loss), nu, ni
+
+
 def val_loss(oracle, pos_u, pos_i):
     """run_val_iteration (implicit.py:366-379): same draw, loss only, no update."""
     U, I, ub, ib = oracle.params

@@ -86,7 +86,10 @@ class MFStepperConfig(ctypes.Structure):
                 ("global_cols", ctypes.c_int64), ("neg_cols", ctypes.c_int64), ("item_grad", ctypes.c_void_p),
                 ("comm", ctypes.c_void_p), ("opt", Opt), ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double),
                 ("beta2_d", ctypes.c_double), ("step", ctypes.c_int64), ("n_partials", ctypes.c_int64),
-                ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("dp_mode", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("pad2_", ctypes.c_int32), ("shard_users", ctypes.c_int64), ("shard_items", ctypes.c_int64),
+                ("grad_buf", ctypes.c_void_p)]
 
 
 class NCFModel(ctypes.Structure):
@@ -222,6 +225,20 @@ SIGNATURES = [
                                       ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
     ("rg_mf_grads", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFLoss)]),
+    ("rg_mf_grad_chunk", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]),
+    ("rg_mf_grads_sharded", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.POINTER(MFLoss)]),
+    ("rg_mf_apply_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,
+                                         ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_void_p]),
+    ("rg_mf_stepper_dp_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                              ctypes.POINTER(MFStepIn), ctypes.c_void_p]),
+    ("rg_mf_stepper_dp_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_comm_reduce_scatter_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int64]),
+    ("rg_comm_allgather_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     ("rg_mf_apply_dense", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,
                                          ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]),
     ("rg_loss_finalize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,

@@ -1,8 +1,10 @@
 """RCCL communicator of the librg_hip.so data-parallel step (include/rg_hip.h,
 rg_comm_*).  torch.distributed sets up the process group (one process per GPU,
 RANK / WORLD_SIZE / MASTER_ADDR from torchrun) and carries the 128-byte unique
-id; the per-step item-gradient all-reduce then runs inside rg_mf_stepper_train on
-the communicator's own stream, overlapped with the user-shard update."""
+id.  The per-step collectives then run inside rg_mf_stepper_train: the reduce-scatter
+of the rank-major gradient and the all-gather of the tables (replicated, reference-exact
+step), or the item-gradient all-reduce on the communicator's own stream overlapped with
+the user-shard update (user-sharded opt-in)."""
 import ctypes
 
 import numpy as np
@@ -38,6 +40,19 @@ class RcclComm:
         check(self.lib.rg_comm_allreduce_sum_f32(self.handle, _lib.stream_handle(), ptr(t), t.numel()),
               "rg_comm_allreduce_sum_f32")
         return t
+
+    def reduce_scatter_(self, t, chunk):
+        """In-place sum: rank r's chunk t[r*chunk:(r+1)*chunk] becomes the sum over ranks."""
+        check(self.lib.rg_comm_reduce_scatter_f32(self.handle, _lib.stream_handle(), ptr(t), int(chunk)),
+              "rg_comm_reduce_scatter_f32")
+        return t
+
+    def all_gather_(self, bufs, counts):
+        """In-place all-gather of each buffer's rank shards (one RCCL group)."""
+        arr = (ctypes.c_void_p * len(bufs))(*[ptr(b) for b in bufs])
+        cnt = (ctypes.c_int64 * len(counts))(*[int(c) for c in counts])
+        check(self.lib.rg_comm_allgather_f32(self.handle, _lib.stream_handle(), len(bufs), arr, cnt),
+              "rg_comm_allgather_f32")
 
     def close(self):
         if getattr(self, "handle", None):

@@ -1,4 +1,5 @@
-// RCCL communicator for the user-sharded data-parallel MF step (host code).
+// RCCL communicator for the data-parallel MF steps (host code): the item-gradient
+// all-reduce of the user-sharded step, the reduce-scatter / all-gather of the replicated one.
 //
 // One process per GPU.  The unique id is created by rank 0 (rg_comm_unique_id)
 // and broadcast by the caller (torch.distributed), then every rank builds its
@@ -53,7 +54,35 @@ int comm_end(void *h, hipStream_t stream) {
     return RG_OK;
 }
 
+int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c || !buf || chunk < 0) return fail_arg("rg_comm_reduce_scatter_f32: bad argument");
+    const ncclResult_t r = ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
+                                             ncclSum, c->comm, stream);
+    return r == ncclSuccess ? RG_OK : nccl_fail("ncclReduceScatter", r);
+}
+
+int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const int64_t *counts) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c || n < 0 || (n > 0 && (!bufs || !counts))) return fail_arg("rg_comm_allgather_f32: bad argument");
+    ncclResult_t r = ncclGroupStart();
+    for (int k = 0; k < n && r == ncclSuccess; ++k)
+        r = ncclAllGather(bufs[k] + (int64_t)c->rank * counts[k], bufs[k], (size_t)counts[k], ncclFloat32, c->comm,
+                          stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail("ncclAllGather", r);
+    return r2 == ncclSuccess ? RG_OK : nccl_fail("ncclGroupEnd", r2);
+}
+
 }  // namespace rg
+
+extern "C" int rg_comm_reduce_scatter_f32(void *comm, void *stream, float *buf, int64_t chunk) {
+    return rg::comm_reduce_scatter(comm, (hipStream_t)stream, buf, chunk);
+}
+
+extern "C" int rg_comm_allgather_f32(void *comm, void *stream, int32_t n, float *const *bufs, const int64_t *counts) {
+    return rg::comm_allgather(comm, (hipStream_t)stream, n, bufs, counts);
+}
 
 extern "C" int rg_comm_unique_id(uint8_t *out, int64_t len) {
     if (!out || len < RG_COMM_ID_BYTES) return rg::fail_arg("rg_comm_unique_id: buffer too small");

@@ -17,6 +17,8 @@ int check_launch(const char *what);
 // rg_comm.cpp: all-reduce of buf on the communicator stream, fenced against `stream`
 int comm_begin(void *comm, hipStream_t stream, float *buf, int64_t n);
 int comm_end(void *comm, hipStream_t stream);
+int comm_reduce_scatter(void *comm, hipStream_t stream, float *buf, int64_t chunk);
+int comm_allgather(void *comm, hipStream_t stream, int n, float *const *bufs, const int64_t *counts);
 
 // ---------------------------------------------------------------- MT jump-ahead
 // One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,

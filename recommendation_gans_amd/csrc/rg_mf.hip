@@ -22,6 +22,7 @@
 //             pre-step row, which is why the parameter tables ping-pong) plus
 //             weight_decay * p; Adam / SGD / RMSprop; p', m, v out; the list
 //             counter and overflow accumulators are reset in the same pass.
+#include <algorithm>
 #include <cstdlib>
 
 #include "rg_common.h"
@@ -515,7 +516,28 @@ struct ApplyArgs {
     int64_t contrib_stride;
     bool has_bias;
     bool keep_count;              // NeuMF: the MF tables read the lists first, the MLP tables reset them
+    // rank-major flat gradient of the replicated data-parallel step (rg_mf_grads_sharded /
+    // rg_mf_apply_shard; shard_users == 0: the plain [(re-rb)*D | (re-rb) | loss] layout):
+    // chunk s (chunk floats) = [user rows s*Us .. (s+1)*Us | item rows s*Is .. | their
+    // biases (Us + Is) | loss], D floats per row
+    int64_t shard_users, shard_items, chunk;
+    int32_t world, rank;
 };
+
+// location of unified row r's gradient in the flat buffer: *row_base + k*D, bias at *bias
+__device__ __forceinline__ void grad_loc(const ApplyArgs &a, int t, int64_t lr_, int64_t gk, int64_t nr,
+                                         const float *&row_base, int64_t &k, int64_t &bias) {
+    if (a.shard_users > 0) {
+        const int64_t s = t ? lr_ / a.shard_items : lr_ / a.shard_users;
+        k = t ? a.shard_users + lr_ % a.shard_items : lr_ % a.shard_users;
+        row_base = a.grad + s * a.chunk;
+        bias = s * a.chunk + (a.shard_users + a.shard_items) * (int64_t)a.dim + k;
+    } else {
+        row_base = a.grad;
+        k = gk;
+        bias = nr * (int64_t)a.dim + gk;
+    }
+}
 
 // mf_apply modes: pull the gradient from the lists and update (single GPU);
 // pull into the flat dense gradient (before an all-reduce);
@@ -573,8 +595,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     float gb = 0.0f;
 
     if (MODE == kApplyDense) {
-        L::load(g, a.grad, gk, D, sub);
-        if (sub == 0) gb = a.grad[nr * (int64_t)D + gk];
+        const float *gbase;
+        int64_t gkk, gbi;
+        grad_loc(a, t, lr_, gk, nr, gbase, gkk, gbi);
+        L::load(g, gbase, gkk, D, sub);
+        if (sub == 0) gb = a.grad[gbi];
     } else if (!COLD) {
         const int c = a.row_count[r];
         // SPEC: the list and the item's partial-slot range are loaded beside the count
@@ -651,8 +676,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             }
         }
         if (MODE == kGradOnly) {
-            L::store(a.grad, gk, D, sub, g);
-            if (sub == 0) a.grad[nr * (int64_t)D + gk] = gb;
+            const float *gbase;
+            int64_t gkk, gbi;
+            grad_loc(a, t, lr_, gk, nr, gbase, gkk, gbi);
+            L::store(const_cast<float *>(gbase), gkk, D, sub, g);
+            if (sub == 0) a.grad[gbi] = gb;
             return;
         }
     }
@@ -690,20 +718,32 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
     const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
     const int D = a.dim;
 
+    const int64_t slot_off = (a.shard_users + a.shard_items) * (int64_t)(D + 1);   // loss slot in a chunk
     if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
         const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) {
-            *a.loss_out = lv;
-            if (MODE == kGradOnly) a.grad[nr * (int64_t)(D + 1)] = lv;
+        if (lane == 0) *a.loss_out = lv;
+        if (MODE == kGradOnly && a.shard_users > 0) {
+            for (int s = lane; s < a.world; s += kWave) a.grad[s * a.chunk + slot_off] = lv;   // summed by the RS
+        } else if (MODE == kGradOnly && lane == 0) {
+            a.grad[nr * (int64_t)(D + 1)] = lv;
         }
     }
     if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-        *a.loss_out = a.grad[nr * (int64_t)(D + 1)];
+        *a.loss_out = a.shard_users > 0 ? a.grad[a.rank * a.chunk + slot_off] : a.grad[nr * (int64_t)(D + 1)];
 
     if (k >= nr) return;
-    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item part [ia0, re)
-    const int64_t ni = re > ia0 ? re - ia0 : 0;
-    const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
+    int64_t r;
+    if (MODE == kApplyDense && a.shard_users > 0) {
+        // this rank's shard: [rb, rb + nu) users, then items from U + rank * Is
+        const int64_t u0 = a.rank * a.shard_users, i0 = a.rank * a.shard_items;
+        const int64_t u1 = u0 + a.shard_users < a.num_users ? u0 + a.shard_users : a.num_users;
+        const int64_t nu = u1 > u0 ? u1 - u0 : 0;
+        r = k < nu ? u0 + k : a.num_users + i0 + (k - nu);
+    } else {
+        const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item part [ia0, re)
+        const int64_t ni = re > ia0 ? re - ia0 : 0;
+        r = k < ni ? ia0 + k : rb + (k - ni);
+    }
     apply_row<L, MODE, NT, false, SPEC>(a, r, sub);
 }
 
@@ -1455,6 +1495,49 @@ extern "C" int rg_mf_apply_dense(void *stream, const rg_mf_tables_t *t, const fl
     if (!grad_dev) return fail_arg("rg_mf_apply_dense: null grad");
     return apply_common(stream, t, nullptr, grad_dev, nullptr, opt, row_begin, row_end, nullptr, loss_out_dev,
                         kApplyDense);
+}
+
+extern "C" int64_t rg_mf_grad_chunk(int64_t shard_users, int64_t shard_items, int32_t dim) {
+    if (shard_users < 1 || shard_items < 1 || dim < 1) return -1;
+    return ((shard_users + shard_items) * (int64_t)(dim + 1) + 1 + 3) / 4 * 4;
+}
+
+static int shard_args(const rg_mf_tables_t *t, int64_t su, int64_t si, int32_t world, int32_t rank, ApplyArgs &a) {
+    if (world < 1 || rank < 0 || rank >= world) return fail_arg("rg_mf sharded: bad rank / world");
+    if (su < 1 || si < 1 || su * world < t->num_users || si * world < t->num_items)
+        return fail_arg("rg_mf sharded: shards do not cover the tables");
+    a.shard_users = su;
+    a.shard_items = si;
+    a.chunk = rg_mf_grad_chunk(su, si, t->dim);
+    a.world = world;
+    a.rank = rank;
+    return RG_OK;
+}
+
+extern "C" int rg_mf_grads_sharded(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, float *grad_dev,
+                                   int64_t shard_users, int64_t shard_items, int32_t world, const rg_mf_loss_t *loss) {
+    if (!grad_dev) return fail_arg("rg_mf_grads_sharded: null grad");
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, grad_dev, nullptr, 0, -1, loss, nullptr, kGradOnly, a);
+    if (rc || (rc = shard_args(t, shard_users, shard_items, world, 0, a))) return rc;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kGradOnly};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_apply_shard(void *stream, const rg_mf_tables_t *t, const float *grad_dev, const rg_opt_t *opt,
+                                 int64_t shard_users, int64_t shard_items, int32_t world, int32_t rank,
+                                 float *loss_out_dev) {
+    if (!grad_dev) return fail_arg("rg_mf_apply_shard: null grad");
+    ApplyArgs a;
+    int rc = apply_args(t, nullptr, grad_dev, nullptr, opt, 0, -1, nullptr, loss_out_dev, kApplyDense, a);
+    if (rc || (rc = shard_args(t, shard_users, shard_items, world, rank, a))) return rc;
+    const int64_t u0 = rank * shard_users, i0 = rank * shard_items;
+    const int64_t nu = u0 < t->num_users ? std::min(shard_users, t->num_users - u0) : 0;
+    const int64_t ni = i0 < t->num_items ? std::min(shard_items, t->num_items - i0) : 0;
+    a.row_begin = 0;
+    a.row_end = nu + ni;            // rows of the shard, mapped in mf_apply_kernel
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyDense};
+    return dispatch_dim(t->dim, f);
 }
 
 extern "C" int rg_loss_finalize(void *stream, const float *partials, int64_t n_partials, double inv_a,

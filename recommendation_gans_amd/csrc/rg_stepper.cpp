@@ -439,6 +439,78 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     return RG_OK;
 }
 
+// Replicated data-parallel step (dp_mode 1): every rank holds every row and
+// consumes its column slice of ONE global draw, so R ranks at batch B compute exactly the
+// reference's step at batch R*B (up to fp32 summation order).  First half: pairs of this
+// rank's columns -> the next step's prepare -> every row's data gradient, rank-major.
+int dp_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next, float *loss_out,
+             void *ev0, void *ev1) {
+    const int64_t unit = st.taken;
+    int rc = keep_ahead(st, unit);
+    if (rc) return rc;
+    rg_mf_work_t w = work_for(st, cur);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if ((rc = wait_side(st, s, (int)(unit % 2)))) return rc;
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
+        if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+    }
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) return rc;
+    if ((rc = release(st, s))) return rc;
+    st.prepared = false;
+    if (next) {
+        if ((rc = keep_ahead(st, unit + 1))) return rc;
+        if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        const rg_mf_batch_t nbatch = make_batch(st, *next, unit + 1);
+        const rg_mf_work_t nw = work_for(st, *next);
+        if ((rc = rg_mf_prepare(s, &nbatch, &nw))) return rc;
+        st.prepared = true;
+        st.prep_unit = unit + 1;
+        st.prep_in = *next;
+        st.prep_serial = 0;
+    }
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+    if ((rc = record(ev0, s))) return rc;
+    if ((rc = rg_mf_grads_sharded(s, tb, &w, st.cfg.grad_buf, st.cfg.shard_users, st.cfg.shard_items, st.cfg.world,
+                                  &l)))
+        return rc;
+    return record(ev1, s);
+}
+
+// second half: this rank's rows from its reduce-scattered chunk, then flip the sets
+int dp_end(Stepper &st, hipStream_t s, float *loss_out) {
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    int rc = rg_mf_apply_shard(s, &st.cfg.tables[st.set], st.cfg.grad_buf, &o, st.cfg.shard_users,
+                               st.cfg.shard_items, st.cfg.world, st.cfg.rank, loss_out);
+    if (rc) return rc;
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
+int64_t dp_chunk(const Stepper &st) {
+    return rg_mf_grad_chunk(st.cfg.shard_users, st.cfg.shard_items, st.cfg.tables[0].dim);
+}
+
+// the whole replicated step with the communicator: begin -> RCCL reduce-scatter -> end ->
+// RCCL all-gather of the four tables the step wrote (now the current set)
+int train_dp(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next, float *loss_out,
+             void *ev0, void *ev1) {
+    int rc = dp_begin(st, s, cur, next, loss_out, ev0, ev1);
+    if (rc) return rc;
+    if ((rc = rg::comm_reduce_scatter(st.cfg.comm, s, st.cfg.grad_buf, dp_chunk(st)))) return rc;
+    if ((rc = dp_end(st, s, loss_out))) return rc;
+    const rg_mf_tables_t &t = st.cfg.tables[st.set];
+    float *bufs[4] = {const_cast<float *>(t.user_w), const_cast<float *>(t.item_w), const_cast<float *>(t.user_b),
+                      const_cast<float *>(t.item_b)};
+    const int64_t d = t.dim;
+    const int64_t counts[4] = {st.cfg.shard_users * d, st.cfg.shard_items * d, st.cfg.shard_users,
+                               st.cfg.shard_items};
+    return rg::comm_allgather(st.cfg.comm, s, 4, bufs, counts);
+}
+
 // the touched rows of the hot pass: a stamp scan (RG_HOT_SCAN=1, default) or the owner flags
 const rg_mf_mark_t *hot_mark(const Stepper &st, const rg_mf_mark_t &m) { return st.hot_scan ? &m : nullptr; }
 
@@ -540,6 +612,16 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         rg::set_error("rg_mf_stepper_create: null sampler buffers");
         return nullptr;
     }
+    if (cfg->dp_mode == 1) {
+        const rg_mf_tables_t &t = cfg->tables[0];
+        if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world || !cfg->grad_buf ||
+            cfg->shard_users * cfg->world < t.num_users || cfg->shard_items * cfg->world < t.num_items ||
+            cfg->global_cols != cfg->cols * cfg->world || cfg->col_offset != cfg->rank * cfg->cols || cfg->item_grad ||
+            cfg->loss == RG_LOSS_ADAPTIVE_HINGE) {
+            rg::set_error("rg_mf_stepper_create: inconsistent replicated data-parallel configuration");
+            return nullptr;
+        }
+    }
     Stepper *st = new (std::nothrow) Stepper();
     if (!st) { rg::set_error("rg_mf_stepper_create: out of memory"); return nullptr; }
     st->cfg = *cfg;
@@ -558,7 +640,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         const char *im = getenv("RG_MT_INLINE");
         const int mode = im ? atoi(im) : 1;
         st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
-                         (mode == 2 || walk_us <= 0.85 * dense_us);
+                         cfg->dp_mode != 1 && (mode == 2 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
         st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
         if (st->G < 1) st->G = 1;
@@ -596,7 +678,9 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         return nullptr;
     }
     st->cp_pos = (int32_t)pos;
-    if (env_flag("RG_MT_JUMP", false)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
+    // the jump-ahead walk (parallel segments) by default when every rank walks the global
+    // stream of a multi-rank step: R times the words of one GPU's step
+    if (env_flag("RG_MT_JUMP", cfg->dp_mode == 1 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
     return st;
 }
 
@@ -611,9 +695,29 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !cur) return rg::fail_arg("rg_mf_stepper_train: null handle/input");
     hipStream_t s = (hipStream_t)stream;
+    if (st->cfg.dp_mode == 1) {
+        if (!st->cfg.comm) return rg::fail_arg("rg_mf_stepper_train: replicated DP step needs a communicator "
+                                               "(or rg_mf_stepper_dp_begin / _dp_end around the caller's exchange)");
+        return train_dp(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+    }
     if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
         return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     return train_split(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+}
+
+extern "C" int rg_mf_stepper_dp_begin(void *h, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
+                                      float *loss_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !cur) return rg::fail_arg("rg_mf_stepper_dp_begin: null handle/input");
+    if (st->cfg.dp_mode != 1) return rg::fail_arg("rg_mf_stepper_dp_begin: stepper is not in dp_mode 1");
+    return dp_begin(*st, (hipStream_t)stream, *cur, next, loss_out, nullptr, nullptr);
+}
+
+extern "C" int rg_mf_stepper_dp_end(void *h, void *stream, float *loss_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_dp_end: null handle");
+    if (st->cfg.dp_mode != 1) return rg::fail_arg("rg_mf_stepper_dp_end: stepper is not in dp_mode 1");
+    return dp_end(*st, (hipStream_t)stream, loss_out);
 }
 
 extern "C" int rg_mf_stepper_acquire(void *h, void *stream, const rg_mf_step_in_t *cur, rg_mf_batch_t *batch_out,

@@ -155,12 +155,17 @@ class MFEngine:
                  n_neg=5, batch_size=256, device="cuda", rank=0, world_size=1, prefetch=True,
                  dp=None, comm=None):
         """``dp``: data-parallel layout when world_size > 1 --
-        "user_shard" (default): the tables passed are this rank's user shard plus every
-            item (sharding.py); own MT stream, local draw layout, the item gradient is
-            the only exchange (``comm``: an RcclComm, else ``train_step_sharded``);
-        "global_stream": replicated tables, every rank draws its slice of one global
-            stream (rank r takes columns [r*B, (r+1)*B) of the global batch's draw),
-            the full flat gradient is exchanged (``train_step_dp``)."""
+        "global_stream" (default, reference-exact): every rank holds every row
+            and consumes columns [r*B, (r+1)*B) of ONE global draw of n*B*R indices from
+            the full pool, with loss means over the global batch; the rank-major data
+            gradient is reduce-scattered, each rank updates its row shard, the tables are
+            all-gathered (``comm``: an RcclComm, native in rg_mf_stepper_train; without
+            one, ``train_step_exchange`` takes the two collectives as callables).  R ranks
+            at batch B compute the reference's step at batch R*B;
+        "user_shard" (opt-in, faster, NOT the reference's sampling at R > 1): the tables
+            passed are this rank's user shard plus every item (sharding.py); own MT stream,
+            own sub-pool and positives, the item gradient is the only exchange (``comm``,
+            else ``train_step_sharded``)."""
         _lib.require_gpu()
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
@@ -168,7 +173,7 @@ class MFEngine:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         if not 1 <= n_neg <= RG_MF_MAX_NEG:
             raise ValueError(f"num_negative_samples must be in [1, {RG_MF_MAX_NEG}] for the fused kernel")
-        dp = dp or ("user_shard" if world_size > 1 or comm is not None else None)
+        dp = dp or ("global_stream" if world_size > 1 or comm is not None else None)
         if dp not in (None, "user_shard", "global_stream"):
             raise ValueError(f"unknown data-parallel layout {dp!r}")
         if loss == "adaptive_hinge" and world_size != 1:
@@ -187,12 +192,32 @@ class MFEngine:
         def put(t, shape):
             return torch.as_tensor(t, dtype=torch.float32).reshape(shape).to(dev).contiguous()
 
-        self.tabs = [[put(user_w, (self.U, self.dim)), put(item_w, (self.I, self.dim)),
-                      put(user_b, (self.U,)), put(item_b, (self.I,))]]
-        self.tabs.append([torch.empty_like(t) for t in self.tabs[0]])
+        self.rank, self.world = int(rank), int(world_size)
+        if dp == "global_stream":
+            # row shards of the rank-major exchange; tables allocated with world * shard rows
+            self.shard_users = -(-self.U // self.world)
+            self.shard_items = -(-self.I // self.world)
+            rows = (self.shard_users * self.world, self.shard_items * self.world)
+        else:
+            self.shard_users = self.shard_items = 0
+            rows = (self.U, self.I)
+
+        def padded():
+            bufs = [torch.zeros(rows[0], self.dim, **f32), torch.zeros(rows[1], self.dim, **f32),
+                    torch.zeros(rows[0], **f32), torch.zeros(rows[1], **f32)]
+            return bufs, [bufs[0][:self.U], bufs[1][:self.I], bufs[2][:self.U], bufs[3][:self.I]]
+
+        self._pad, self.tabs = [], []
+        for _ in range(2):
+            b, v = padded()
+            self._pad.append(b)
+            self.tabs.append(v)
+        for dst, src, shape in zip(self.tabs[0], (user_w, item_w, user_b, item_b),
+                                   ((self.U, self.dim), (self.I, self.dim), (self.U,), (self.I,))):
+            dst.copy_(put(src, shape))
         self.opt_kind = optimizer
-        self.m = [torch.zeros_like(t) for t in self.tabs[0]] if optimizer == "adam" else [None] * 4
-        self.v = [torch.zeros_like(t) for t in self.tabs[0]] if optimizer != "sgd" else [None] * 4
+        self.m = padded()[1] if optimizer == "adam" else [None] * 4
+        self.v = padded()[1] if optimizer != "sgd" else [None] * 4
         self.lr, self.wd, self.betas, self.eps, self.alpha = lr, weight_decay, betas, eps, alpha
         pu = np.asarray(pool_u, dtype=np.int64)
         pi = np.asarray(pool_i, dtype=np.int64)
@@ -205,7 +230,6 @@ class MFEngine:
         self.loss = loss
         self.n_neg = int(n_neg)
         self.batch_size = int(batch_size)
-        self.rank, self.world = int(rank), int(world_size)
         self.dp = dp
         self.comm = comm
         if dp == "global_stream":
@@ -231,6 +255,10 @@ class MFEngine:
         self.units_per_block = int(self.lib.rg_mf_plan_units_per_block(self.dim))
         self.grad_buf = None
         self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
+        self.chunk = 0
+        if dp == "global_stream":
+            self.chunk = int(self.lib.rg_mf_grad_chunk(self.shard_users, self.shard_items, self.dim))
+            self.dp_grad = torch.zeros(self.world * self.chunk, **f32)
         self.mt_buf = _as_u32_tensor(mt_state, dev)
         self.pairs = [torch.zeros(int(self.lib.rg_mf_pairs_len(self.batch_size, self.n_neg)), dtype=torch.int32,
                                   device=dev) for _ in range(2)]
@@ -253,6 +281,10 @@ class MFEngine:
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
         cfg.step, cfg.n_partials, cfg.current_set = 0, self.n_partials, 0
+        if dp == "global_stream":
+            cfg.dp_mode, cfg.rank, cfg.world = 1, self.rank, self.world
+            cfg.shard_users, cfg.shard_items = self.shard_users, self.shard_items
+            cfg.grad_buf = ptr(self.dp_grad)
         self._stepper = self.lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + self.lib.rg_last_error().decode())
@@ -354,8 +386,11 @@ class MFEngine:
         (a float32 device tensor of >= 1 element) or to the engine's own slot."""
         if self.dp == "user_shard" and self.world > 1 and self.comm is None:
             raise RuntimeError("user-sharded step over several ranks needs an RcclComm (or train_step_sharded)")
-        if self.dp == "global_stream" and self.world > 1:
-            raise RuntimeError("dp='global_stream' steps go through train_step_dp")
+        if self.dp == "global_stream" and self.comm is None:
+            if self.world > 1:
+                raise RuntimeError("dp='global_stream' over several ranks needs an RcclComm (or train_step_exchange)")
+            return self.train_step_exchange(cur, next_input, lambda buf, chunk: None, lambda bufs, counts: None,
+                                            loss_out=loss_out)
         ev0 = ev1 = None
         if apply_events is not None:
             ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
@@ -436,13 +471,38 @@ class MFEngine:
         self.finish_step()
         return self.loss_out
 
-    def train_step_dp(self, pos_u, pos_i, global_pos, allreduce, plan=None):
-        """Data-parallel step with replicated tables: local pairs -> local flat gradient ->
-        ``allreduce`` (in-place sum across ranks, e.g. torch.distributed.all_reduce over
-        RCCL) -> replicated update."""
-        g = self.grads(pos_u, pos_i, global_pos, plan=plan)
-        allreduce(g)
-        return self.apply_dense(g)
+    # ------------------------------------------------------------------ replicated DP (global_stream)
+    def dp_begin(self, cur, next_input=None, loss_out=None):
+        """First half of the replicated step (rg_mf_stepper_dp_begin): this rank's column
+        slice of the global draw -> pairs -> the rank-major gradient in ``dp_grad``."""
+        out = self.loss_out if loss_out is None else loss_out
+        check(self.lib.rg_mf_stepper_dp_begin(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
+                                              ctypes.byref(next_input) if next_input is not None else None,
+                                              ptr(out)), "rg_mf_stepper_dp_begin")
+        return out
+
+    def dp_end(self, loss_out=None):
+        """Second half: this rank's rows from its (reduce-scattered) chunk, then the sets
+        flip; the caller all-gathers ``dp_gather_buffers()``."""
+        out = self.loss_out if loss_out is None else loss_out
+        check(self.lib.rg_mf_stepper_dp_end(self._stepper, _lib.stream_handle(), ptr(out)), "rg_mf_stepper_dp_end")
+        return out
+
+    def dp_gather_buffers(self):
+        """The current set's four padded tables and this layout's all-gather counts (each
+        rank's shard = rows [rank * count, (rank + 1) * count) of the flat buffer)."""
+        d = self.dim
+        return self._pad[self.cur], [self.shard_users * d, self.shard_items * d, self.shard_users, self.shard_items]
+
+    def train_step_exchange(self, cur, next_input, reduce_scatter, all_gather, loss_out=None):
+        """The replicated step with caller-run collectives: ``reduce_scatter(buf, chunk)``
+        must leave in buf[rank*chunk:(rank+1)*chunk] the sum over ranks of that chunk;
+        ``all_gather(bufs, counts)`` must fill every rank's shard of each buffer."""
+        out = self.dp_begin(cur, next_input, loss_out)
+        reduce_scatter(self.dp_grad, self.chunk)
+        self.dp_end(out)
+        all_gather(*self.dp_gather_buffers())
+        return out
 
     def train_step_sharded(self, pos_u, pos_i, global_pos, allreduce, plan=None):
         """The user-sharded step with the item-gradient exchange done by ``allreduce``

@@ -1,10 +1,16 @@
 """Shared pieces of the data-parallel tests (CPU gloo and GPU).
 
-``global_view`` restates the user-sharded step (recommendation_gans_amd/sharding.py)
-on the GLOBAL tables with the oracle's primitives: every rank's positives and
-draws (its own MT stream over its own sub-pool, mapped back to global user ids)
-contribute gradients with loss means over all ranks; one optimizer step.  The
-sharded runs must reproduce it."""
+Two layouts (recommendation_gans_amd/mf_engine.py):
+
+* replicated / global stream (the default, reference-exact): R ranks at batch B must
+  reproduce ONE process at batch R*B -- ``reference_run`` is the single-process
+  oracle (oracle/mf.py MFOracle, pinned to the reference's goldens) at that batch,
+  and ``rank_columns`` cuts its global batches the way the ranks do;
+* user-sharded (opt-in): ``global_view`` restates the sharded step on the GLOBAL
+  tables with the oracle's primitives: every rank's positives and draws (its own MT
+  stream over its own sub-pool, mapped back to global user ids) contribute
+  gradients with loss means over all ranks; one optimizer step.  This layout is
+  NOT the reference's sampling at R > 1, so it is checked against that restatement."""
 import numpy as np
 import torch
 
@@ -25,6 +31,45 @@ def problem(seed=0):
     return tables, pool_u, pool_i, train_u, train_i, orng.py_seed_state(seed)
 
 
+# ------------------------------------------------------------------ replicated (global stream)
+# a run whose last global batch is partial: 3 full global batches of 2*B + 11 positives
+GS_TRAIN = 3 * 2 * B + 11
+
+
+def global_batches(world, n_train=GS_TRAIN, batch=B):
+    """[lo, hi) of every global batch: contiguous slices of the shuffled order
+    (implicit.py:290 over the order of implicit.py:262), batch*world positives each."""
+    gb = batch * world
+    return [(lo, min(lo + gb, n_train)) for lo in range(0, n_train, gb)]
+
+
+def rank_columns(world, rank, n_train=GS_TRAIN, batch=B):
+    """Per global step: this rank's positives [lo, hi) (columns [rank*B, (rank+1)*B) of the
+    global batch, possibly empty) and the global batch's positive count."""
+    out = []
+    for lo, hi in global_batches(world, n_train, batch):
+        a = min(lo + rank * batch, hi)
+        b = min(a + batch, hi)
+        out.append((a, b, hi - lo))
+    return out
+
+
+def reference_run(tables, pool_u, pool_i, train_u, train_i, state0, world, loss, dtype=torch.float32,
+                  lr=1e-2, wd=1e-5, n_train=GS_TRAIN):
+    """The single process at batch world*B: losses, params and the MT state after each step,
+    and the negative ids of each step as a (n, world*B) array."""
+    o = omf.MFOracle(*[t.clone().to(dtype) for t in tables], pool_u, pool_i, state0.copy(), loss=loss,
+                     optimizer="adam", lr=lr, weight_decay=wd, n_neg=N_NEG, batch_size=B * world)
+    losses, states, negs = [], [], []
+    for lo, hi in global_batches(world, n_train):
+        out = o.step(train_u[lo:hi], train_i[lo:hi], return_all=True)
+        losses.append(out["loss"])
+        states.append(o.state.copy())
+        negs.append((out["neg_u"].numpy().reshape(N_NEG, -1), out["neg_i"].numpy().reshape(N_NEG, -1)))
+    return o, losses, states, negs
+
+
+# ------------------------------------------------------------------ user-sharded (opt-in)
 def rank_batches(train_u, train_i, rank, world, steps=STEPS, batch=B):
     lu, li = sharding.shard_interactions(train_u, train_i, rank, world)
     return [(lu[s * batch:(s + 1) * batch], li[s * batch:(s + 1) * batch]) for s in range(steps)]

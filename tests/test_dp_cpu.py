@@ -1,6 +1,11 @@
-"""User-sharded data parallelism on CPU: partition helpers, and a world_size-2
-gloo run of the sharded step (oracle per rank, item-gradient all-reduce over
-gloo) against the global-view restatement (tests/dp_common.py)."""
+"""Data parallelism on CPU (gloo, world_size 2), at the oracle level.
+
+* replicated / global stream (the default layout): every rank takes its
+  column slice of ONE global draw and the gradients are summed -- must equal the
+  single-process oracle at batch 2B (negative ids and MT state bit-exact, tables and
+  losses within 1e-5), including a partial last global batch;
+* user-sharded (opt-in): partition helpers, and the sharded step (oracle per rank,
+  item-gradient all-reduce) against its global-view restatement (tests/dp_common.py)."""
 import os
 import socket
 
@@ -49,6 +54,60 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _worker_gs(rank, world, port, loss, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+        o = omf.MFOracle(*[t.clone() for t in tables], pool_u, pool_i, state0.copy(), loss=loss, optimizer="adam",
+                         lr=1e-2, weight_decay=1e-5, n_neg=dc.N_NEG, batch_size=dc.B)
+
+        def exchange(grads):
+            for g in grads:
+                dist.all_reduce(g)
+            return grads
+
+        losses, states, negs = [], [], []
+        for a, b, gp in dc.rank_columns(world, rank):
+            lv, nu, ni = omf.step_columns(o, train_u[a:b], train_i[a:b], rank * dc.B, world * dc.B, gp, exchange)
+            t = torch.tensor([lv])
+            dist.all_reduce(t)
+            losses.append(float(t))
+            states.append(o.state.copy())
+            negs.append((nu.numpy().reshape(dc.N_NEG, -1), ni.numpy().reshape(dc.N_NEG, -1)))
+        out[rank] = ([p.clone() for p in o.params], losses, states, negs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge"])
+def test_global_stream_gloo_world2_equals_batch_2B(loss):
+    """R = 2 ranks at batch B == one process at batch 2B (the reference's semantics)."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker_gs, args=(world, _free_port(), loss, out), nprocs=world, join=True)
+    tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+    o, ref_losses, ref_states, ref_negs = dc.reference_run(tables, pool_u, pool_i, train_u, train_i, state0, world,
+                                                           loss)
+    for r in range(world):
+        params, losses, states, negs = out[r]
+        for s in range(len(ref_losses)):
+            assert (states[s] == ref_states[s]).all(), (r, s, "MT state")
+            cols = slice(r * dc.B, (r + 1) * dc.B)
+            assert (negs[s][0] == ref_negs[s][0][:, cols]).all() and (negs[s][1] == ref_negs[s][1][:, cols]).all()
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        for k in range(4):
+            np.testing.assert_allclose(params[k].numpy(), o.params[k].numpy(), rtol=1e-5, atol=1e-7)
+    assert all(torch.equal(a, b) for a, b in zip(out[0][0], out[1][0])), "replicas diverged"
+
+
+def test_rank_columns_partial_batch():
+    cols = dc.rank_columns(2, 1)
+    assert cols[0] == (8, 16, 16) and cols[-1] == (56, 59, 11)
+    assert dc.rank_columns(2, 0)[-1] == (48, 56, 11)
+    assert dc.rank_columns(1, 0)[-1] == (56, 59, 3)
 
 
 def _worker(rank, world, port, loss, out):

@@ -285,8 +285,10 @@ def test_mf_gradients_elementwise(dev, loss, hot, d):
 
 @pytest.mark.parametrize("loss", ["pointwise", "bpr"])
 def test_mf_dense_update_path(dev, loss):
-    """rg_mf_grads -> (identity all-reduce) -> rg_mf_apply_dense, i.e. the data-parallel
-    step at world size 1, tracks the oracle over several steps."""
+    """The replicated data-parallel step at world size 1 without a communicator
+    (rg_mf_stepper_dp_begin: pairs -> rank-major rg_mf_grads_sharded; identity exchange;
+    rg_mf_stepper_dp_end: rg_mf_apply_shard) tracks the oracle over several steps,
+    optimizer state included."""
     from recommendation_gans_amd.mf_engine import MFEngine
     U, I, d, B, n = 300, 200, 64, 128, 5
     tabs, pool_u, pool_i, steps = make_case(U, I, d, B, n, 5000, 4)
@@ -294,10 +296,11 @@ def test_mf_dense_update_path(dev, loss):
     o = omf.MFOracle(*[t.clone() for t in tabs], pool_u, pool_i, st.copy(), loss=loss, optimizer="adam", lr=1e-2,
                      weight_decay=1e-5, n_neg=n, batch_size=B)
     e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), pool_u, pool_i, st.copy(), loss=loss,
-                 optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev)
+                 optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev,
+                 dp="global_stream")
     for s, (pu, pi) in enumerate(steps):
         ref = o.step(pu, pi)
-        got = e.train_step_dp(torch.from_numpy(pu).to(dev), torch.from_numpy(pi).to(dev), len(pu), lambda t: None)
+        got = e.train_step(torch.from_numpy(pu).to(dev), torch.from_numpy(pi).to(dev), len(pu))
         torch.cuda.synchronize()
         close(got[0], np.float32(ref), what=f"dense step {s} loss")
         for k in range(4):
@@ -483,3 +486,32 @@ def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
     for k in range(4):
         ok, msg = omf.tensor_parity(e.params()[k], o.params[k], o64.params[k])
         assert ok, (k, msg)
+
+
+@pytest.mark.parametrize("rank", [0, 5])
+def test_dp_rank_slice_sampler_full_size(dev, rank):
+    """Rank `rank` of 8 in the replicated DP layout at full size (B = 8192 per rank, global
+    draw of 5 * 65,536 indices per step, the jump-ahead walk that layout defaults to at
+    world > 1: 5.2 M words per 8-step slot in parallel segments): its prepared negatives
+    are columns [rank*B, (rank+1)*B) of random.choices' global draw, bit-exact, and the MT
+    state after each step is CPython's.  (Identity exchange: tables are not checked here.)"""
+    from recommendation_gans_amd.mf_engine import MFEngine
+    U, I, d, B, n, world = 300, 200, 16, 8192, 5, 8
+    g = torch.Generator().manual_seed(5)
+    tabs = [torch.randn(U, d, generator=g) / d, torch.randn(I, d, generator=g) / d, torch.zeros(U), torch.zeros(I)]
+    rs = np.random.RandomState(5)
+    pool_u, pool_i = rs.randint(0, U, 30000), rs.randint(0, I, 30000)
+    st = orng.py_seed_state(11)
+    e = MFEngine(*tabs, pool_u, pool_i, st.copy(), loss="bpr", optimizer="adam", lr=1e-2, weight_decay=1e-5,
+                 n_neg=n, batch_size=B, device=dev, rank=rank, world_size=world, dp="global_stream")
+    assert e.words_per_step == 2 * n * B * world
+    ref = st.copy()
+    none = lambda *a: None   # noqa: E731
+    ins = [e.step_input(torch.from_numpy(rs.randint(0, U, B)).to(dev), torch.from_numpy(rs.randint(0, I, B)).to(dev),
+                        B * world) for _ in range(10)]
+    for s in range(9):
+        e.train_step_exchange(ins[s], ins[s + 1], none, none)
+        idx = orng.py_choices_indices(ref, len(pool_u), n * B * world).reshape(n, B * world)[:, rank * B:(rank + 1) * B]
+        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].transpose(0, 1).cpu().numpy() & 0x7FFFFFFF
+        assert (pr[..., 0] == pool_u[idx]).all() and (pr[..., 1] == pool_i[idx]).all(), f"step {s} negatives"
+        assert (e.mt_state() == ref).all(), f"step {s} MT state"
