@@ -1,0 +1,192 @@
+"""BASELINE.json's GPU configurations at their configured sizes, against the oracle.
+
+* C2 / C5 (MF-BPR, ML-20M-shaped: U = 136,677, I = 20,108, 8.1 M train positives,
+  8.1 M pool pairs, B = 8192, n = 5, Adam): three native steps (item plans, the
+  next step's prepare fused into the dense pass, the inline MT walk) at d = 64 and
+  d = 128 against the single-process oracle (oracle/mf.py, fp32 and fp64): negative
+  ids and MT state bit-exact, loss 1e-5 relative, tables by tensor parity;
+* C5's data-parallel shard: rank 3 of 8 in the replicated layout at d = 128 -- its
+  column slice of the global draw of 5 * 65,536 indices (jump-ahead walk) and its
+  rank-major data gradient against the oracle's gradient of the same columns
+  (1e-5 relative per table);
+* C4 (cGAN, N = 20,108, S = 5, H = 256, E = 5, B = 256, histories of the synthetic
+  ML-20M users): one discriminator iteration and one generator iteration with
+  recorded z and dropout masks against the float64 oracle (oracle/gan.py).
+
+The CPU oracle runs at these sizes in a few seconds per step on the box's host cores."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gan as og
+from oracle import mf as omf
+from oracle import rng as orng
+from tests.test_gan_oracle import param_ok
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ml20m():
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    return movielens_like(ML20M, seed=0)
+
+
+def _tables(U, I, d):
+    torch.manual_seed(0)                                  # mf_spotlight.py:37 -> BilinearNet
+    return omf.init_tables(U, I, d)
+
+
+def _rel(got, ref):
+    got = torch.as_tensor(got).double().reshape(-1).cpu()
+    ref = torch.as_tensor(ref).double().reshape(-1)
+    return float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_mf_full_size_steps(ml20m, d):
+    from recommendation_gans_amd.mf_engine import MFEngine
+    dev = torch.device("cuda:0")
+    U, I, B, n = ml20m.num_users, ml20m.num_items, 8192, 5
+    tabs = _tables(U, I, d)
+    st = orng.py_seed_state(0)
+    kw = dict(loss="bpr", optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    o = omf.MFOracle(*[t.clone() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **kw)
+    o64 = omf.MFOracle(*[t.clone().double() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **kw)
+    e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), ml20m.pool_u, ml20m.pool_i, st.copy(),
+                 device=dev, **kw)
+    tu = torch.from_numpy(ml20m.train_u[:4 * B].astype(np.int64)).to(dev)
+    ti = torch.from_numpy(ml20m.train_i[:4 * B].astype(np.int64)).to(dev)
+    ins = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], B, e.make_plan(ti[s * B:(s + 1) * B]))
+           for s in range(4)]
+    for s in range(3):
+        got = e.train_step_in(ins[s], ins[s + 1])
+        out = o.step(ml20m.train_u[s * B:(s + 1) * B], ml20m.train_i[s * B:(s + 1) * B], return_all=True)
+        o64.step(ml20m.train_u[s * B:(s + 1) * B], ml20m.train_i[s * B:(s + 1) * B])
+        torch.cuda.synchronize()
+        assert abs(float(got[0]) - out["loss"]) <= 1e-5 * abs(out["loss"]), (s, float(got[0]), out["loss"])
+        assert (e.mt_state() == o.state).all(), f"d{d} step {s}: MT state"
+        # the consumed pairs (item-plan order): negatives as a multiset per column = random.choices' draw
+        perm = ins[s]._keep[2].perm.cpu().numpy()
+        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].cpu().numpy() & 0x7FFFFFFF      # [position][q]
+        nu = out["neg_u"].numpy().reshape(n, B)[:, perm].T
+        ni = out["neg_i"].numpy().reshape(n, B)[:, perm].T
+        assert (pr[..., 0] == nu).all() and (pr[..., 1] == ni).all(), f"d{d} step {s}: negatives"
+        for k in range(4):
+            ok, msg = omf.tensor_parity(e.params()[k], o.params[k], o64.params[k])
+            assert ok, (d, s, k, msg)
+
+
+def test_mf_dp_rank_gradient_d128(ml20m):
+    """C5's per-rank step: rank 3 of 8, replicated layout, d = 128, full size."""
+    from recommendation_gans_amd.mf_engine import MFEngine
+    dev = torch.device("cuda:0")
+    U, I, d, B, n, world, rank = ml20m.num_users, ml20m.num_items, 128, 8192, 5, 8, 3
+    tabs = _tables(U, I, d)
+    st = orng.py_seed_state(0)
+    kw = dict(loss="bpr", optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), ml20m.pool_u, ml20m.pool_i, st.copy(),
+                 device=dev, rank=rank, world_size=world, dp="global_stream", **kw)
+    o = omf.MFOracle(*[t.clone() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **kw)
+    gb = B * world
+    lo = rank * B
+    pu, pi = ml20m.train_u[lo:lo + B].astype(np.int64), ml20m.train_i[lo:lo + B].astype(np.int64)
+    du, di = torch.from_numpy(pu).to(dev), torch.from_numpy(pi).to(dev)
+    e.dp_begin(e.step_input(du, di, gb, e.make_plan(di)))
+    torch.cuda.synchronize()
+    grads = {}
+
+    def capture(g):
+        grads["g"] = [t.clone() for t in g]
+        return g
+    lv, nu, ni = omf.step_columns(o, pu, pi, rank * B, gb, gb, capture)
+    assert (e.mt_state() == o.state).all(), "MT state"
+    # unpack the rank-major buffer: chunk s = [users s*Us.. | items s*Is.. | biases | loss]
+    Us, Is, C = e.shard_users, e.shard_items, e.chunk
+    buf = e.dp_grad.view(world, C).cpu()
+    gU = torch.cat([buf[s, :Us * d].view(Us, d) for s in range(world)])[:U]
+    gI = torch.cat([buf[s, Us * d:(Us + Is) * d].view(Is, d) for s in range(world)])[:I]
+    nb = (Us + Is) * d
+    gub = torch.cat([buf[s, nb:nb + Us] for s in range(world)])[:U]
+    gib = torch.cat([buf[s, nb + Us:nb + Us + Is] for s in range(world)])[:I]
+    for k, got in enumerate((gU, gI, gub, gib)):
+        ref = grads["g"][k].reshape(got.shape)
+        assert _rel(got, ref) <= 1e-5, (k, _rel(got, ref))
+    for s in range(world):                                   # this rank's loss share in every chunk
+        assert abs(float(buf[s, nb + Us + Is]) - lv) <= 1e-5 * abs(lv)
+
+
+def _gan_batch(ml20m, S, B):
+    order = np.argsort(ml20m.train_u, kind="stable")
+    uu, ii = ml20m.train_u[order], ml20m.train_i[order]
+    starts = np.searchsorted(uu, np.arange(ml20m.num_users + 1))
+    counts = np.diff(starts)
+    users = np.nonzero(counts > S)[0][:B]
+    L = int((counts[users] - S).max())
+    N = ml20m.num_items
+    hist = np.full((B, L), N, np.int64)
+    sl = np.zeros((B, S), np.int64)
+    for r, u in enumerate(users):
+        items = ii[starts[u]:starts[u + 1]]
+        hist[r, :len(items) - S] = items[:-S]
+        sl[r] = items[-S:]
+    return hist, sl
+
+
+def test_gan_full_size_iterations(ml20m):
+    """C4: slate_generation.py's cGAN at S = 5, gan_hidden_layer = 256, batch 256, RMSprop.
+    G keeps the reference's own init (cGAN_models.py:70-73 under torch.manual_seed(0)); every
+    D tensor is rescaled to max |x| = 0.004 (as the cGAN goldens, make_golden.gan_case):
+    with the reference's D init, layers 1-3 (Xavier bound 0.088) are clamped to exactly
+    +-0.01 and their pre-activations cancel to within rounding of the LeakyReLU kink, where
+    the slope -- and so the sign of RMSprop's first, sign-like update -- is decided by
+    summation order in ANY implementation.  Continuous D weights keep the comparison
+    meaningful; lr 1e-4 as the goldens."""
+    from recommendation_gans_amd.gan_engine import GANBatch, GANEngine
+    from recommendation_gans_amd.spotlight.dnn_models.cGAN_models import discriminator, generator
+    N, S, H, E, Z, B, lr = ml20m.num_items, 5, 256, 5, 100, 256, 1e-4
+    hist, sl = _gan_batch(ml20m, S, B)
+    torch.manual_seed(0)
+    G = generator(num_items=N, noise_dim=Z, embedding_dim=E, hidden_layer=[H // 2, H], output_dim=S)
+    D = discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
+    g_sd = {k: v.detach().clone() for k, v in G.state_dict().items()}
+    d_sd = {k: v.detach().clone() * (0.004 / max(float(v.abs().max()), 1e-30)) for k, v in D.state_dict().items()}
+    eng = GANEngine(g_sd, d_sd, N, S, H, E, Z, batch_max=B, optimizer="rms", lr=lr)
+    o = og.GANOracle({k: v.numpy() for k, v in g_sd.items()}, {k: v.numpy() for k, v in d_sd.items()}, N, S, H, E,
+                     Z, opt="rms", lr=lr)
+    rs = np.random.RandomState(7)
+    gd, dd = og.g_hidden(H), og.d_hidden(H)
+
+    def masks(widths, p):
+        return [(rs.rand(B, w) >= p).astype(np.uint8) for w in widths]
+    scales = (float(np.float32(1) / np.float32(0.9)), float(np.float32(1) / np.float32(0.7)))
+    batch = GANBatch(hist, sl, N, S, "cuda")
+    # one discriminator iteration (CGANs.py:410-457)
+    z = rs.rand(B, Z).astype(np.float32)
+    mk = masks(dd, 0.3) + masks(gd, 0.1) + masks(dd, 0.3)
+    out = eng.d_step(batch, z=torch.from_numpy(z), masks=mk).cpu().numpy()
+    loss, d_real, d_fake, fake = o.d_step(hist, sl, z.astype(np.float64), [m.astype(np.float64) for m in mk], scales)
+    dval = eng.last_d_out(2 * B).cpu().numpy()
+    # D outputs: 4 layers over K = S*N + E = 100,545 (fp32 MFMA, split-K): 1e-5 of the outputs' scale
+    scale = np.abs(np.concatenate([d_real.ravel(), d_fake.ravel()])).max()
+    assert np.abs(dval[:B] - d_real.ravel()).max() <= 1e-5 * scale
+    assert np.abs(dval[B:] - d_fake.ravel()).max() <= 1e-5 * scale
+    assert _rel(eng.last_fake(B), fake) <= 1e-5
+    assert abs(out[0] - loss) <= 1e-5 * scale
+    dsd = eng.d_state_dict()
+    for k in o.D:
+        ok, msg = param_ok(dsd[k].numpy(), o.D[k], o.last_grads[k], lr)
+        assert ok, f"D {k}: {msg}"
+    # one generator iteration (CGANs.py:370-408) on the same batch, eval-mode slates after it
+    z = rs.rand(B, Z).astype(np.float32)
+    mk = masks(gd, 0.1) + masks(dd, 0.3)
+    gl, slates = eng.g_step(batch, z=torch.from_numpy(z), masks=mk)
+    gloss, gd_fake, ref_slates = o.g_step(hist, z.astype(np.float64), [m.astype(np.float64) for m in mk], scales)
+    assert abs(float(gl[0]) - gloss) <= 1e-5 * np.abs(gd_fake).max()
+    assert np.abs(eng.last_d_out(B).cpu().numpy() - gd_fake.ravel()).max() <= 1e-5 * np.abs(gd_fake).max()
+    agree = (slates.cpu().numpy() == ref_slates).mean()
+    assert agree >= 0.999, agree                          # argmax ties within fp32 rounding may differ
+    gsd = eng.g_state_dict()
+    for k in o.g_params:
+        ok, msg = param_ok(gsd[k].numpy(), o.G[k], o.last_grads[k], lr, exempt=k in o.pre_bn_biases())
+        assert ok, f"G {k}: {msg}"

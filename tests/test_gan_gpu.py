@@ -41,7 +41,8 @@ def gemm(A, B, a_km, b_km, M, N, K, post=0, splits=1, bias=None, ldc=None):
 
 @pytest.mark.parametrize("a_km,b_km", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K,splits", [(256, 512, 1000, 1), (250, 130, 64, 1), (64, 256, 2048, 7),
-                                          (300, 40, 36, 3)])
+                                          (300, 40, 36, 3),
+                                          (256, 512, 100544, 64)])   # C4's D layer 1 (S*N rounded to 4)
 def test_gemm_matches_float64(a_km, b_km, M, N, K, splits):
     if (a_km or b_km) and K % 4:
         pytest.skip("K-major operands need K % 4 == 0")
