@@ -272,7 +272,7 @@ def load(path=None):
     global _lib, _load_error
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("RG_LIB") or LIB_PATH      # RG_LIB: a same-box A/B variant (scripts)
     if not os.path.exists(p):
         raise RuntimeError(f"librg_hip.so not found at {p}: build it with "
                            "`python -m recommendation_gans_amd.build` (hipcc, gfx950). "

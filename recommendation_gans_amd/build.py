@@ -48,18 +48,23 @@ def up_to_date():
 DIAG_LIB = os.path.join(PKG, "librg_hip_diag.so")
 
 
-def build(force=False, verbose=False, jobs=8, diag=False):
+def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=()):
     """diag=True: librg_hip_diag.so with the RG_DIAG_STAMPS phase stamps (scripts only;
-    the product never loads it)."""
-    lib = DIAG_LIB if diag else LIB
-    if not force and not diag and up_to_date():
+    the product never loads it).  variant=NAME: _variants/librg_hip_NAME.so built with the
+    extra -D defines, for same-box A/B runs (scripts load it through RG_LIB)."""
+    if variant:
+        os.makedirs(os.path.join(PKG, "_variants"), exist_ok=True)
+        lib = os.path.join(PKG, "_variants", f"librg_hip_{variant}.so")
+    else:
+        lib = DIAG_LIB if diag else LIB
+    if not force and not diag and not variant and up_to_date():
         return LIB
     hipcc = _hipcc()
-    objdir = os.path.join(PKG, "_obj_diag" if diag else "_obj")
+    objdir = os.path.join(PKG, f"_obj_{variant}" if variant else "_obj_diag" if diag else "_obj")
     os.makedirs(objdir, exist_ok=True)
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
               "-Wall", "-Wno-unused-function", "-ffp-contract=fast"] + (["-DRG_DIAG_STAMPS"] if diag else []) + \
-        (os.environ.get("RG_EXTRA_CFLAGS", "").split() if diag else [])
+        (os.environ.get("RG_EXTRA_CFLAGS", "").split() if diag else []) + [f"-D{d}" for d in defines]
     procs, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -90,4 +95,7 @@ def build(force=False, verbose=False, jobs=8, diag=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, diag="--diag" in sys.argv))
+    var = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else None
+    defs = [a[2:] for a in sys.argv if a.startswith("-D")]
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, diag="--diag" in sys.argv, variant=var,
+                defines=defs))

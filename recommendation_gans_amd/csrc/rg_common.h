@@ -75,6 +75,18 @@ __device__ __forceinline__ float group_sum(float x) {
 // (lgkmcnt) but leaves its global stores/atomics in flight.  __syncthreads() on
 // gfx9 also emits s_waitcnt vmcnt(0), draining every outstanding global store
 // before the barrier -- needless when no other thread of the block reads them.
+// compute units of the current device (host; cached on first use)
+inline int num_cus() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            return 256;
+        return v;
+    }();
+    return n;
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -31,6 +31,9 @@
 namespace rg {
 
 constexpr int kCap = RG_MF_LIST_CAP;
+#ifndef RG_MF_PULL_GROUP
+#define RG_MF_PULL_GROUP 4
+#endif
 constexpr int kNMax = RG_MF_MAX_NEG;
 constexpr int kBlock = 256;
 
@@ -601,7 +604,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         L::load(g, gbase, gkk, D, sub);
         if (sub == 0) gb = a.grad[gbi];
     } else if (!COLD) {
+#ifdef RG_X_NOPULL   // timing experiments only (wrong results): the pass without the pulls
+        const int c = a.row_count[r] < 0 ? 1 : 0;
+#else
         const int c = a.row_count[r];
+#endif
         // SPEC: the list and the item's partial-slot range are loaded beside the count
         // (entries past the count are stale and never used), so a touched row's partner
         // rows are its only dependent round trip
@@ -626,18 +633,27 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             // MF: the partner row of the other table; NCF: the stored gradient half
             const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
             const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
-            float o[kCap][EPL];
+            // partner rows in groups of PG list entries (RG_MF_PULL_GROUP; most touched rows have
+            // 1-2 entries): a later group's gathers issue only when some row of the wave needs them,
+            // and the smaller register footprint raises occupancy
+            constexpr int PG = RG_MF_PULL_GROUP;
 #pragma unroll
-            for (int e = 0; e < kCap; ++e) {
-                if (e < ne) L::load_strided(o[e], other, ent[e].x, ostride, D, sub); else L::zero(o[e]);
-            }
+            for (int h = 0; h < kCap / PG; ++h) {
+                if (h > 0 && !__any(ne > h * PG)) break;
+                float o[PG][EPL];
 #pragma unroll
-            for (int e = 0; e < kCap; ++e) {
-                if (e < ne) {
-                    const float dz = __int_as_float(ent[e].y);
+                for (int e = 0; e < PG; ++e) {
+                    if (h * PG + e < ne) L::load_strided(o[e], other, ent[h * PG + e].x, ostride, D, sub);
+                    else L::zero(o[e]);
+                }
 #pragma unroll
-                    for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
-                    gb += dz;
+                for (int e = 0; e < PG; ++e) {
+                    if (h * PG + e < ne) {
+                        const float dz = __int_as_float(ent[h * PG + e].y);
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
+                        gb += dz;
+                    }
                 }
             }
             if (c > kCap) {
@@ -758,20 +774,47 @@ struct MtGenArgs {
     int64_t nwords;
 };
 
+// Grid of mf_back_kernel: [MT walk block (optional)] [prepare blocks] [padding] [apply
+// blocks, apply_padded = a multiple of 8 starting at an absolute index that is one].
+// Workgroups go to the 8 XCDs round-robin by absolute index, so with xcd_map the apply
+// block of absolute index B processes row group (B % 8) * apply_padded / 8 + B / 8: each
+// XCD streams one contiguous eighth of the rows, and the per-row small arrays (biases,
+// counts: 4 B per row, 16 B per wave) fill whole lines in ONE XCD's L2 instead of each
+// line being fetched and partially written back by all eight.
+struct BackGrid {
+    int64_t prep_blocks, apply_start, apply_padded;
+    int32_t prep_first, xcd_map;
+};
+
 template <class L, int NT, bool SPEC = false>
 __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
-                                                        int64_t apply_blocks, MtGenArgs gen) {
+                                                        int64_t apply_blocks, MtGenArgs gen, BackGrid bg) {
     static_assert(kBlock == kGenThreads, "the MT walk runs on one full workgroup");
-    int64_t blk = blockIdx.x;
+    const int64_t B = blockIdx.x;
+    int64_t blk = B;
     if (gen.nwords > 0) {
-        if (blk == 0) {
+        if (B == 0) {
             __shared__ uint32_t X[kRing + 2];
             mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
             return;
         }
         --blk;
     }
-    if (blk >= apply_blocks) {
+    // the next step's prepare (latency-bound random pool reads) in the FIRST blocks, so it
+    // overlaps the streaming rows instead of trailing the grid (RG_PREP_FIRST=0: last)
+    if (bg.prep_first) {
+        if (blk < bg.prep_blocks) {
+#ifdef RG_X_NOPREP   // timing experiments only
+            return;
+#endif
+            prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+            return;
+        }
+        if (B < bg.apply_start) return;                         // alignment padding
+        blk = B - bg.apply_start;
+        if (bg.xcd_map) blk = (blk & 7) * (bg.apply_padded >> 3) + (blk >> 3);
+        if (blk >= apply_blocks) return;
+    } else if (blk >= apply_blocks) {
         prepare_one(prep, prep_out, (blk - apply_blocks) * kBlock + threadIdx.x);
         return;
     }
@@ -1297,19 +1340,29 @@ struct BackLaunchF {
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
-        const dim3 grid((unsigned)(nb + prep_blocks + (gen.nwords > 0 ? 1 : 0)));
+        static const int prep_first = [] { const char *e = getenv("RG_PREP_FIRST"); return e ? atoi(e) : 1; }();
+        static const int xcd_map = [] { const char *e = getenv("RG_XCD_MAP"); return e ? atoi(e) : 0; }();   // measured 3 us slower
+        BackGrid bg{prep_blocks, 0, 0, prep_first, prep_first ? xcd_map : 0};
+        const int64_t head = prep_blocks + (gen.nwords > 0 ? 1 : 0);
+        int64_t total = nb + head;
+        if (prep_first) {
+            bg.apply_start = (head + 7) / 8 * 8;
+            bg.apply_padded = (nb + 7) / 8 * 8;
+            total = bg.apply_start + bg.apply_padded;
+        }
+        const dim3 grid((unsigned)total);
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
         // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
         // RG_APPLY_SPEC=0 turns it off)
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
         if (spec)
-            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
+            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
         else if (nt == 1)
-            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
+            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
         else if (nt >= 2)
-            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
+            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
         else
-            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen);
+            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
         return check_launch("rg_mf_apply_prepare");
     }
 };
