@@ -80,12 +80,13 @@ def parse():
     ap.add_argument("--gan-hidden", type=int, default=256)
     ap.add_argument("--gan-slate", type=int, default=5)
     ap.add_argument("--gan-emb", type=int, default=5)
-    ap.add_argument("--dp", default="global_stream", choices=["global_stream", "user_shard"],
-                    help="multi-GPU layout (N > 1): global_stream = reference-exact replicated step "
-                         "(reduce-scatter + all-gather); user_shard = user-sharded opt-in (not the reference's "
-                         "sampling at N > 1)")
+    ap.add_argument("--dp", default="owner", choices=["owner", "global_stream", "user_shard"],
+                    help="multi-GPU layout (N > 1): owner = reference-exact, users sharded by owner, items "
+                         "replicated (score + item-gradient all-reduces); global_stream = reference-exact "
+                         "replicated step (reduce-scatter + all-gather of every row); user_shard = user-sharded "
+                         "opt-in (not the reference's sampling at N > 1)")
     ap.add_argument("--dp-at-1", action="store_true",
-                    help="run the replicated DP code path at N = 1 too (identity exchange; bench-path check)")
+                    help="run the DP code path at N = 1 too (identity exchange; bench-path check)")
     ap.add_argument("--events-every", type=int, default=8,
                     help="record the dominant kernel's timing events on every k-th timed step")
     return ap.parse_args()
@@ -198,7 +199,7 @@ def bench_ncf(args):
     ti = torch.from_numpy(data.train_i).to(dev)
     nb = len(data.train_u) // B
     nplan = min(nb, args.warmup + args.steps)
-    plans = [eng.make_plan(ti[g * B:(g + 1) * B]) for g in range(nplan)]
+    plans = eng.make_plans(ti[:nplan * B])
     for s in range(args.warmup):
         g = s % nplan
         eng.train_step(tu[g * B:(g + 1) * B], ti[g * B:(g + 1) * B], plan=plans[g])
@@ -476,7 +477,19 @@ def main():
         from recommendation_gans_amd.comm import RcclComm
         comm = RcclComm(dev)
     gs = args.dp == "global_stream" and (world > 1 or args.dp_at_1)
-    if gs:
+    own = args.dp == "owner" and (world > 1 or args.dp_at_1)
+    if own:
+        # owner-sharded, reference-exact: this rank's users (u % world == rank) + every item,
+        # the full pool; every global batch of B * world positives, this rank's plan of it
+        eng = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), data.pool_u, data.pool_i, mt, loss=args.loss,
+                       optimizer=args.optim, lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev,
+                       rank=rank, world_size=world, dp="owner", prefetch=not args.no_prefetch, comm=comm)
+        train_u, train_i = data.train_u, data.train_i
+        U_local = eng.U
+        gb = B * world
+        nbatches = len(train_u) // gb
+        batch_lo = [g * gb for g in range(nbatches)]
+    elif gs:
         # replicated, reference-exact: full tables / pool on every rank, global batches of
         # B * world positives, this rank's columns [rank*B, (rank+1)*B) of each
         eng = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), data.pool_u, data.pool_i, mt, loss=args.loss,
@@ -502,18 +515,25 @@ def main():
     ti = torch.from_numpy(train_i).to(dev)
     # per-batch plans: the epoch order is fixed for the whole fit (implicit.py:262), so
     # they are built once per fit, before timing (like the reference's own data
-    # preparation); their cost is measured and reported beside the step
-    nplan = min(nbatches, args.warmup + args.steps)
+    # preparation), for EVERY batch of the epoch in one launch (rg_mf_plans_build); the
+    # cost is measured (second build, warm) and reported beside the step
+    pstride = batch_lo[1] - batch_lo[0] if nbatches > 1 else B
+    pkw = dict(users=tu) if own else {}
+    eng.make_plans(ti[:gb * 4], offset=batch_lo[0], stride=pstride, **({"users": tu[:gb * 4]} if own else {}))
     torch.cuda.synchronize()
     tp0 = time.perf_counter()
-    plans = [eng.make_plan(ti[batch_lo[g]:batch_lo[g] + B]) for g in range(nplan)]
+    plans = eng.make_plans(ti, offset=batch_lo[0], stride=pstride, **pkw)[:nbatches]
     torch.cuda.synchronize()
-    plan_us = (time.perf_counter() - tp0) / nplan * 1e6
+    plan_epoch_s = time.perf_counter() - tp0
+    plan_us = plan_epoch_s / nbatches * 1e6
+    nplan = len(plans)
+
+    span = gb if own else B
 
     def batch(s):
         g = s % nbatches
         lo = batch_lo[g]
-        return tu[lo:lo + B], ti[lo:lo + B], plans[g % nplan]
+        return tu[lo:lo + span], ti[lo:lo + span], plans[g % nplan]
 
     # step inputs (ids + plan pointers) built before timing; each call also hands the
     # NEXT step's input to the native stepper, which generates its words ahead
@@ -553,7 +573,7 @@ def main():
         value = args.steps * B * world / el
         # per rank: its user shard + every item go through the dense optimizer pass
         gather, ids, adam = algorithmic_bytes(U_local, I, d, B, n)
-        user_adam = 6 * U_local * (4 * d + 4) if world > 1 else adam
+        user_adam = 6 * U_local * (4 * d + 4) if (world > 1 or own) else adam
         out = {"metric": METRIC, "value": value, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -563,12 +583,15 @@ def main():
                "config": {"workload": f"MF-{args.loss.upper()} ML-20M-shaped, embedding_dim={d}, "
                                       f"batch {B}/GPU, {n} negatives, {args.optim} (coupled L2 1e-5) over all rows",
                           "global_batch": gb, "embedding_dim": d,
-                          "parallelism": f"dp{world}" + ("" if world == 1 else
+                          "parallelism": f"dp{world}" + (" owner-sharded users, replicated items (score + item-"
+                                                         "gradient all-reduces, reference-exact)" if own else
                                                          " replicated (reduce-scatter + all-gather, reference-exact)"
-                                                         if gs else " user-sharded (opt-in, not reference sampling)")},
-               "plan_build_us_per_batch": plan_us,
-               "plan_build_note": "item-sorted plan of one batch (torch ops), built once per fit for every batch "
-                                  "(the reference shuffles once, implicit.py:262); not in the timed region"}
+                                                         if gs else "" if world == 1 else
+                                                         " user-sharded (opt-in, not reference sampling)")},
+               "plan_build_us_per_batch": plan_us, "plan_build_ms_per_epoch": plan_epoch_s * 1e3,
+               "plan_build_note": f"item-sorted plans of all {nbatches} batches of an epoch in one HIP launch "
+                                  "(rg_mf_plans_build), built once per fit (the reference shuffles once, "
+                                  "implicit.py:262); not in the timed region"}
         step_bytes = gather + ids + adam
         out["step_roofline"] = {"bytes_per_step": step_bytes,
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
@@ -578,7 +601,11 @@ def main():
             from recommendation_gans_amd import _lib
             ms = [_lib.elapsed_ms(a, b) for a, b in (ev for ev in evs if ev is not None)]
             avg = float(np.mean(ms)) * 1e-3
-            if gs:
+            if own:
+                # the events bracket the user rows' update with the next step's owner prepare
+                alg = user_adam
+                kname = "rg_mf_apply (owner: this rank's user rows; next step's owner prepare in the same launch)"
+            elif gs:
                 # rg_mf_grads_sharded: every row's pulled gradient written rank-major (the exchange's input)
                 alg = gather + world * eng.chunk * 4
                 kname = "rg_mf_grads_sharded (mf_apply_kernel<kGradOnly>, rank-major gradient for the reduce-scatter)"

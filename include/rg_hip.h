@@ -183,6 +183,30 @@ int64_t rg_mf_partials_len(int64_t cols, int32_t dim);
 /* Positions per pair-kernel block, the block size a batch plan is built for. */
 int64_t rg_mf_plan_units_per_block(int32_t dim);
 
+/* The plans (rg_mf_work_t plan_*) of many batches in ONE launch, one workgroup per batch
+ * (rg_plan.hip; replaces building them batch by batch on the host).  The reference
+ * shuffles once per fit and revisits the same contiguous batches every epoch
+ * (implicit.py:262, :290), so they are built once per fit.
+ *   batch k = positives [offset + k*stride, offset + k*stride + batch_len) of items / users
+ *             (device int64, n entries in all; clipped at n);
+ *   owner_world > 1: only the positives whose user u has u % owner_world == owner_rank are
+ *             planned (owner-sharded data parallelism; users required), else all;
+ *   per batch k (cols >= batch_len is the output stride):
+ *     perm[k*cols + s]      planned positives' columns (relative to the batch start) sorted
+ *                           by (item, column); then, single rank, the other columns ascending;
+ *                           -1 past the planned positives when owner_world > 1
+ *     pos_slot[k*cols + s]  partial slot (a new slot where the item changes or a block of
+ *                           units_per_block positions starts), -1 past the planned positives
+ *     item_slot_off[k*(num_items+1) + i]   item i's slots [off[i], off[i+1])
+ *     counts[2k], counts[2k+1]             planned positives, slots
+ * scratch: rg_mf_plans_scratch_len(cols, n_batches) uint64 of device memory (0: null is
+ * fine; only batches of more than 16,384 planned positives use it). */
+int64_t rg_mf_plans_scratch_len(int64_t cols, int64_t n_batches);
+int rg_mf_plans_build(void *stream, const int64_t *users, const int64_t *items, int64_t n, int64_t offset,
+                      int64_t stride, int64_t batch_len, int64_t n_batches, int64_t cols, int32_t units_per_block,
+                      int64_t num_items, int32_t owner_world, int32_t owner_rank, int32_t *perm, int32_t *pos_slot,
+                      int32_t *item_slot_off, int32_t *counts, uint64_t *scratch);
+
 /* Resolve the step's pairs: positives permuted to processing order and every
  * negative draw -> pool index (CPython random.choices arithmetic) -> (user, item).
  * Fully parallel; depends only on the words, the pool, the plan and the ids, so it
@@ -288,6 +312,56 @@ int rg_mf_grads_sharded(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t
 int rg_mf_apply_shard(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
                       int64_t shard_users, int64_t shard_items, int32_t world, int32_t rank, float *loss_out_dev);
 
+/* ------------------------------------------------------------------------------
+ * Owner-sharded data-parallel step (dp_mode 2; rg_owner.hip), reference-exact: R ranks
+ * at batch B compute the reference's step at batch R*B (one global CPython stream of
+ * n*R*B draws over the FULL pool, contiguous global batches, global loss means;
+ * implicit.py:262, :290, :351-354), with only the items replicated:
+ *   rank r owns the users u with u % R == r (its tables hold them as local rows u / R,
+ *   then every item); every rank walks the global draw and keeps the pairs whose user
+ *   it owns (rg_mf_owner_prepare);
+ *   rg_mf_owner_scores: the scores of its pairs into a zeroed global score vector
+ *   [(1 + n) * GC] (pair gp = c: positive of column c, (1 + k) * GC + c: its negative k);
+ *   -> all-reduce (sum; every slot has exactly one writer, so the sum is exact) ->
+ *   rg_mf_owner_back: dL/dz of its pairs from the column's scores (the BPR / hinge
+ *   pairing couples a column's positive with its negatives), contribution lists, planned
+ *   item partials, loss partials (this rank's share);
+ *   -> rg_mf_grads over the item rows (+ loss) -> all-reduce -> rg_mf_apply_dense of the
+ *   items beside rg_mf_apply of the user rows.
+ * Per step a rank exchanges 4 (1 + n) GC bytes of scores and the (I (d + 1) + 1)-float
+ * item gradient, instead of the (U + I)(d + 1) floats of the replicated layout.
+ * Not for adaptive hinge (global max over all negatives).
+ * ---------------------------------------------------------------------------- */
+typedef struct rg_mf_owner_batch {
+    const int64_t *pos_user, *pos_item;  /* the GLOBAL batch's positives (global ids), column order */
+    int64_t n_pos;                       /* positives in the global batch (<= global_cols) */
+    int64_t global_cols;                 /* GC = batch_size * world */
+    const int32_t *plan_perm, *plan_pos_slot;   /* this rank's planned positives (rg_mf_plans_build
+                                                   with the owner filter); plan_item_slot_off in work */
+    int64_t n_planned;
+    const uint32_t *words;               /* 2 * n_neg * GC raw MT19937 words of the step */
+    const int32_t *pool;                 /* the FULL negative pool, int32 (user, item) global ids */
+    int64_t pool_len;
+    int32_t n_neg, loss;
+    int32_t world, rank;
+    int32_t *neg_rec;                    /* [4 * rg_mf_owner_rec_len(GC, n_neg)] prepared records */
+    int32_t *seg_count;                  /* [rg_mf_owner_segments(GC, n_neg)] */
+    float *scores;                       /* [(1 + n_neg) * GC] */
+} rg_mf_owner_batch_t;
+
+int64_t rg_mf_owner_segments(int64_t global_cols, int32_t n_neg);
+int64_t rg_mf_owner_rec_len(int64_t global_cols, int32_t n_neg);
+/* float loss partials rg_mf_owner_back writes (upper bound over any n_planned <= GC) */
+int64_t rg_mf_owner_partials_len(int64_t global_cols, int32_t n_neg, int32_t dim, int32_t world);
+/* the partials a step with n_planned planned positives actually writes */
+int64_t rg_mf_owner_partials_used(int64_t global_cols, int32_t n_neg, int32_t dim, int32_t world,
+                                  int64_t n_planned);
+int rg_mf_owner_prepare(void *stream, const rg_mf_owner_batch_t *batch);
+/* tables: this rank's (num_users = its local users) */
+int rg_mf_owner_scores(void *stream, const rg_mf_tables_t *tables, const rg_mf_owner_batch_t *batch);
+int rg_mf_owner_back(void *stream, const rg_mf_tables_t *tables, const rg_mf_owner_batch_t *batch,
+                     rg_mf_work_t *work);
+
 /* Optimizer update of the rows in range from a (summed) flat gradient
  * (+ weight_decay * p).  loss_out_dev (optional) receives grad_dev's loss slot. */
 int rg_mf_apply_dense(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
@@ -359,12 +433,22 @@ typedef struct rg_mf_stepper_config {
     int32_t dp_mode, rank, world, pad2_;
     int64_t shard_users, shard_items;
     float *grad_buf;
+    /* dp_mode 2: the owner-sharded step (rg_mf_owner_*, reference-exact): tables[k] hold this
+     * rank's users (local rows u / world) and every item; cols = global_cols = GC and
+     * col_offset = 0 (every rank walks the whole global draw); item_grad is the exchanged
+     * item gradient; per-unit buffers (unit parity) of the prepared records, their segment
+     * counts and the score vector the first exchange sums. */
+    int32_t *owner_rec[2];          /* [4 * rg_mf_owner_rec_len(GC, n_neg)] each */
+    int32_t *owner_seg[2];          /* [rg_mf_owner_segments(GC, n_neg)] each */
+    float *owner_scores[2];         /* [(1 + n_neg) * GC] each */
 } rg_mf_stepper_config_t;
 
 typedef struct rg_mf_step_in {
     const int64_t *pos_user, *pos_item;
     int64_t n_pos, global_pos;
     const int32_t *plan_perm, *plan_pos_slot, *plan_item_slot_off;   /* optional plan */
+    int64_t n_planned;              /* dp_mode 2: this rank's planned positives (plan required);
+                                       pos_user / pos_item / n_pos are then the GLOBAL batch */
 } rg_mf_step_in_t;
 
 void *rg_mf_stepper_create(const rg_mf_stepper_config_t *config);
@@ -393,6 +477,21 @@ int rg_mf_stepper_prefetch(void *stepper, void *stream, const rg_mf_step_in_t *n
 int rg_mf_stepper_dp_begin(void *stepper, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
                            float *loss_out_dev);
 int rg_mf_stepper_dp_end(void *stepper, void *stream, float *loss_out_dev);
+/* The owner-sharded step (dp_mode 2) in three parts around caller-run all-reduces (sum)
+ * (comm == NULL; tests, gloo); with a communicator rg_mf_stepper_train runs all of it:
+ *   owner_begin: prepare (unless prefetched) + rg_mf_owner_scores of `cur` -> the caller
+ *     all-reduces rg_mf_stepper_owner_buffers' scores (pointwise: no exchange needed);
+ *   owner_mid: rg_mf_owner_back + rg_mf_grads of the item rows into item_grad -> the caller
+ *     all-reduces item_grad;
+ *   owner_end: the user rows' update with `next`'s owner prepare in the same launch, then
+ *     the items from item_grad; flips the sets. */
+int rg_mf_stepper_owner_begin(void *stepper, void *stream, const rg_mf_step_in_t *cur);
+int rg_mf_stepper_owner_mid(void *stepper, void *stream, float *loss_out_dev);
+/* (ev_begin / ev_end optional hipEvent_t recorded around the user rows' update launch) */
+int rg_mf_stepper_owner_end(void *stepper, void *stream, const rg_mf_step_in_t *next, float *loss_out_dev,
+                            void *ev_begin, void *ev_end);
+/* the current unit's score vector and its length (floats) */
+int rg_mf_stepper_owner_scores(void *stepper, float **scores_out, int64_t *len_out);
 /* Optimizer scalars for optimizer step `step` (1-based). */
 int rg_mf_stepper_opt(void *stepper, int64_t step, rg_opt_t *opt_out);
 int rg_mf_stepper_state(void *stepper, int32_t *current_set, int64_t *step);

@@ -239,6 +239,48 @@ def step_columns(oracle, pos_u, pos_i, col_offset, global_cols, global_pos, exch
     return float(loss), nu, ni
 
 
+def step_owner(oracle, pos_u, pos_i, world, rank, allreduce):
+    """One rank's share of the owner-sharded data-parallel step (the layout of
+    recommendation_gans_amd/csrc/rg_owner.hip): the step of a single process at batch
+    ``oracle.batch_size`` = GC global columns (implicit.py:347-364), split by user owner.
+
+    ``oracle.params`` hold this rank's users (global u with u % world == rank, local row
+    u // world) and every item; the draw is the global one over the full pool
+    (implicit.py:351-354).  The rank scores the pairs whose user it owns into a zeroed
+    global score vector, ``allreduce`` sums it (one writer per slot), every rank then has
+    the loss and the pairing's dL/dp (spotlight/losses.py), keeps dL/dz of its own pairs,
+    and ``allreduce`` sums the item-table gradients before the optimizer step.
+    Returns (loss, negative users (n, GC), negative items (n, GC), own-negative mask)."""
+    U, I, ub, ib = oracle.params
+    n, GC = oracle.n, oracle.batch_size
+    pos_u = torch.as_tensor(pos_u).long()
+    pos_i = torch.as_tensor(pos_i).long()
+    Bp = len(pos_u)
+    idx, nu, ni = oracle.draw(n * GC)
+    nu, ni = nu.view(n, GC), ni.view(n, GC)
+    valid = torch.ones(n, GC, dtype=torch.bool)
+    if oracle.loss_kind in ("bpr", "hinge"):
+        valid[:, Bp:] = False
+    own_p = pos_u % world == rank
+    own_n = (nu % world == rank) & valid
+    S = torch.zeros((1 + n) * GC, dtype=U.dtype)
+    S[:Bp][own_p] = scores(U, I, ub, ib, pos_u[own_p] // world, pos_i[own_p])
+    Sn = S[GC:].view(n, GC)
+    Sn[own_n] = scores(U, I, ub, ib, nu[own_n] // world, ni[own_n])
+    allreduce(S)
+    p_pos, p_neg = S[:Bp], S[GC:]
+    loss, dpp, dpn = loss_and_dp(oracle.loss_kind, p_pos, p_neg, n, GC)
+    dzp = (dpp * (1.0 - p_pos) * p_pos)[own_p]
+    dzn = (dpn * (1.0 - p_neg) * p_neg).view(n, GC)[own_n]
+    u = torch.cat([pos_u[own_p], nu[own_n]]) // world
+    i = torch.cat([pos_i[own_p], ni[own_n]])
+    grads = dense_grads(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
+    allreduce(grads[1])
+    allreduce(grads[3])
+    oracle.opt.step(oracle.params, grads)
+    return float(loss), nu, ni, own_n
+
+
 def val_loss(oracle, pos_u, pos_i):
     """run_val_iteration (implicit.py:366-379): same draw, loss only, no update."""
     U, I, ub, ib = oracle.params

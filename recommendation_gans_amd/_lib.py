@@ -89,7 +89,8 @@ class MFStepperConfig(ctypes.Structure):
                 ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32),
                 ("dp_mode", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("pad2_", ctypes.c_int32), ("shard_users", ctypes.c_int64), ("shard_items", ctypes.c_int64),
-                ("grad_buf", ctypes.c_void_p)]
+                ("grad_buf", ctypes.c_void_p), ("owner_rec", ctypes.c_void_p * 2), ("owner_seg", ctypes.c_void_p * 2),
+                ("owner_scores", ctypes.c_void_p * 2)]
 
 
 class NCFModel(ctypes.Structure):
@@ -140,7 +141,16 @@ GAN_WS_FAKE, GAN_WS_DOUT = 0, 1
 class MFStepIn(ctypes.Structure):
     _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
                 ("global_pos", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
-                ("plan_item_slot_off", ctypes.c_void_p)]
+                ("plan_item_slot_off", ctypes.c_void_p), ("n_planned", ctypes.c_int64)]
+
+
+class MFOwnerBatch(ctypes.Structure):
+    _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
+                ("global_cols", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
+                ("n_planned", ctypes.c_int64), ("words", ctypes.c_void_p), ("pool", ctypes.c_void_p),
+                ("pool_len", ctypes.c_int64), ("n_neg", ctypes.c_int32), ("loss", ctypes.c_int32),
+                ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("neg_rec", ctypes.c_void_p),
+                ("seg_count", ctypes.c_void_p), ("scores", ctypes.c_void_p)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/rg_hip.h
@@ -199,6 +209,12 @@ SIGNATURES = [
                                       ctypes.c_void_p]),
     ("rg_mf_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     ("rg_mf_plan_units_per_block", ctypes.c_int64, [ctypes.c_int32]),
+    ("rg_mf_plans_scratch_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+    ("rg_mf_plans_build", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_mf_pairs_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     ("rg_mf_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
     ("rg_mf_prepare_marked", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
@@ -235,6 +251,20 @@ SIGNATURES = [
     ("rg_mf_stepper_dp_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                               ctypes.POINTER(MFStepIn), ctypes.c_void_p]),
     ("rg_mf_stepper_dp_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_owner_segments", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_mf_owner_rec_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_mf_owner_partials_len", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rg_mf_owner_partials_used", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_int64]),
+    ("rg_mf_owner_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFOwnerBatch)]),
+    ("rg_mf_owner_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFOwnerBatch)]),
+    ("rg_mf_owner_back", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFOwnerBatch),
+                                        ctypes.POINTER(MFWork)]),
+    ("rg_mf_stepper_owner_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn)]),
+    ("rg_mf_stepper_owner_mid", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_owner_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_owner_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_comm_reduce_scatter_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_int64]),
     ("rg_comm_allgather_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,

@@ -27,6 +27,7 @@
 
 #include "rg_common.h"
 #include "rg_mt.h"
+#include "rg_owner.h"
 
 namespace rg {
 
@@ -786,9 +787,11 @@ struct BackGrid {
     int32_t prep_first, xcd_map;
 };
 
-template <class L, int NT, bool SPEC = false>
+template <class L, int NT, bool SPEC = false, bool OWN = false>
 __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
-                                                        int64_t apply_blocks, MtGenArgs gen, BackGrid bg) {
+                                                        int64_t apply_blocks, MtGenArgs gen, BackGrid bg,
+                                                        OwnerArgs own) {
+    static_assert(kBlock == kOwnSeg, "an owner prepare segment is one workgroup");
     static_assert(kBlock == kGenThreads, "the MT walk runs on one full workgroup");
     const int64_t B = blockIdx.x;
     int64_t blk = B;
@@ -807,7 +810,8 @@ __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs 
 #ifdef RG_X_NOPREP   // timing experiments only
             return;
 #endif
-            prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+            if (OWN) owner_prepare_block(own, blk);
+            else prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
             return;
         }
         if (B < bg.apply_start) return;                         // alignment padding
@@ -815,7 +819,8 @@ __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs 
         if (bg.xcd_map) blk = (blk & 7) * (bg.apply_padded >> 3) + (blk >> 3);
         if (blk >= apply_blocks) return;
     } else if (blk >= apply_blocks) {
-        prepare_one(prep, prep_out, (blk - apply_blocks) * kBlock + threadIdx.x);
+        if (OWN) owner_prepare_block(own, blk - apply_blocks);
+        else prepare_one(prep, prep_out, (blk - apply_blocks) * kBlock + threadIdx.x);
         return;
     }
     constexpr int LPU = L::LPU, UPW = L::UPW;
@@ -1334,6 +1339,7 @@ struct BackLaunchF {
     int64_t prep_blocks;
     MtGenArgs gen;
     hipStream_t s;
+    const OwnerArgs *own = nullptr;   // owner-sharded DP: the next step's owner prepare
     template <class L>
     int operator()() {
         const int64_t rows = a->row_end - a->row_begin;
@@ -1355,14 +1361,19 @@ struct BackLaunchF {
         // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
         // RG_APPLY_SPEC=0 turns it off)
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
-        if (spec)
-            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
+        const OwnerArgs oa = own ? *own : OwnerArgs{};
+        if (own)
+            hipLaunchKernelGGL((mf_back_kernel<L, 0, true, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen,
+                               bg, oa);
+        else if (spec)
+            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
+                               oa);
         else if (nt == 1)
-            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
+            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         else if (nt >= 2)
-            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
+            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         else
-            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg);
+            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         return check_launch("rg_mf_apply_prepare");
     }
 };
@@ -1397,6 +1408,25 @@ extern "C" int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *t, rg
     BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
+
+namespace rg {
+int apply_prepare_owner(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                        int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
+                        const rg_mf_owner_batch_t *next) {
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, loss, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    PairsArgs prep{};
+    OwnerArgs oa{};
+    int64_t prep_blocks = 0;
+    if (next) {
+        if ((rc = owner_args(next, oa))) return rc;
+        prep_blocks = oa.segs;
+    }
+    BackLaunchF f{&a, &prep, nullptr, prep_blocks, MtGenArgs{}, (hipStream_t)stream, next ? &oa : nullptr};
+    return dispatch_dim(t->dim, f);
+}
+}  // namespace rg
 
 extern "C" int rg_mf_step_front(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *cur, rg_mf_work_t *w,
                                 const rg_mf_mark_t *cur_mark, const rg_opt_t *opt, int64_t cold_begin,

@@ -47,6 +47,7 @@
 #include <new>
 
 #include "rg_common.h"
+#include "rg_owner.h"
 
 namespace {
 
@@ -99,6 +100,10 @@ struct Stepper {
     int32_t cp_pos = 624;
     bool win_at[kSlots] = {false, false, false};   // form / position at each slot's start
     int32_t pos_at[kSlots] = {624, 624, 624};
+    // owner-sharded step (dp_mode 2) between its parts
+    rg_mf_step_in_t own_in{};
+    int64_t own_unit = -1;
+    int own_stage = 0;                    // 0 idle, 1 after begin, 2 after mid
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -511,6 +516,135 @@ int train_dp(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf
     return rg::comm_allgather(st.cfg.comm, s, 4, bufs, counts);
 }
 
+// ---------------------------------------------------------------- owner-sharded step (dp_mode 2)
+rg_mf_owner_batch_t owner_batch(const Stepper &st, const rg_mf_step_in_t &in, int64_t unit) {
+    rg_mf_owner_batch_t b{};
+    b.pos_user = in.pos_user;
+    b.pos_item = in.pos_item;
+    b.n_pos = in.n_pos;
+    b.global_cols = st.cfg.global_cols;
+    b.plan_perm = in.plan_perm;
+    b.plan_pos_slot = in.plan_pos_slot;
+    b.n_planned = in.n_planned;
+    b.words = unit_words(st, unit);
+    b.pool = st.cfg.pool;
+    b.pool_len = st.cfg.pool_len;
+    b.n_neg = st.cfg.n_neg;
+    b.loss = st.cfg.loss;
+    b.world = st.cfg.world;
+    b.rank = st.cfg.rank;
+    b.neg_rec = st.cfg.owner_rec[unit % 2];
+    b.seg_count = st.cfg.owner_seg[unit % 2];
+    b.scores = st.cfg.owner_scores[unit % 2];
+    return b;
+}
+
+int owner_check_in(const Stepper &st, const rg_mf_step_in_t &in) {
+    if (!in.plan_perm || !in.plan_pos_slot || !in.plan_item_slot_off)
+        return rg::fail_arg("owner-sharded step: every step input needs this rank's plan (rg_mf_plans_build, owner filter)");
+    if (in.n_pos > st.cfg.global_cols || in.n_planned < 0 || in.n_planned > in.n_pos || in.global_pos != in.n_pos)
+        return rg::fail_arg("owner-sharded step: n_pos / n_planned / global_pos inconsistent with the global batch");
+    return RG_OK;
+}
+
+// part 1: this unit's owner prepare (unless the previous dense pass prepared it) and the
+// scores of this rank's pairs into the zeroed global score vector
+int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
+    int rc = owner_check_in(st, cur);
+    if (rc) return rc;
+    const int64_t unit = st.taken;
+    if ((rc = keep_ahead(st, unit))) return rc;
+    const rg_mf_owner_batch_t b = owner_batch(st, cur, unit);
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
+        if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_owner_prepare(s, &b))) return rc;
+    }
+    st.prepared = false;
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if ((rc = rg_mf_owner_scores(s, tb, &b))) return rc;
+    if ((rc = release(st, s))) return rc;               // the unit's words were read by its prepare
+    st.own_in = cur;
+    st.own_unit = unit;
+    st.own_stage = 1;
+    return RG_OK;
+}
+
+// part 2 (after the score exchange): dL/dz, contribution lists, the item rows' data gradient
+int owner_mid(Stepper &st, hipStream_t s, float *loss_out) {
+    if (st.own_stage != 1) return rg::fail_arg("rg_mf_stepper_owner_mid: owner_begin must come first");
+    const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
+    rg_mf_work_t w = work_for(st, st.own_in);
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    int rc = rg_mf_owner_back(s, tb, &b, &w);
+    if (rc) return rc;
+    rg_mf_loss_t l = loss_of(st, st.own_in.global_pos, loss_out);
+    l.n_partials = rg_mf_owner_partials_used(st.cfg.global_cols, st.cfg.n_neg, tb->dim, st.cfg.world,
+                                             st.own_in.n_planned) / 2;
+    const int64_t U = tb->num_users, R = U + tb->num_items;
+    if ((rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l))) return rc;
+    st.own_stage = 2;
+    return RG_OK;
+}
+
+// part 3 (after the item-gradient exchange, or beside it on the communicator stream): the
+// user rows' update with the next unit's owner prepare in the same launch, the items
+int owner_user_update(Stepper &st, hipStream_t s, const rg_mf_step_in_t *next, const rg_opt_t &o) {
+    int rc = RG_OK;
+    rg_mf_owner_batch_t nb{};
+    const int64_t unit = st.own_unit;
+    if (next) {
+        if ((rc = owner_check_in(st, *next))) return rc;
+        if ((rc = keep_ahead(st, unit + 1))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        nb = owner_batch(st, *next, unit + 1);
+    }
+    rg_mf_work_t w = work_for(st, st.own_in);
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if ((rc = rg::apply_prepare_owner(s, tb, &w, &o, 0, tb->num_users, nullptr, next ? &nb : nullptr))) return rc;
+    if (next) {
+        st.prepared = true;
+        st.prep_unit = unit + 1;
+        st.prep_in = *next;
+        st.prep_serial = 0;
+    }
+    return RG_OK;
+}
+
+int owner_item_update(Stepper &st, hipStream_t s, const rg_opt_t &o, float *loss_out) {
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    const int64_t U = tb->num_users, R = U + tb->num_items;
+    int rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out);
+    if (rc) return rc;
+    st.set = 1 - st.set;
+    st.own_stage = 0;
+    return RG_OK;
+}
+
+// the whole owner-sharded step with the communicator: begin -> score all-reduce (not for
+// pointwise: no pairing) -> mid -> item-gradient all-reduce on the communicator stream
+// beside the user update (+ next prepare) -> item update
+int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next, float *loss_out,
+                void *ev0, void *ev1) {
+    int rc = owner_begin(st, s, cur);
+    if (rc) return rc;
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if (st.cfg.loss != RG_LOSS_POINTWISE) {
+        const int64_t len = (int64_t)(1 + st.cfg.n_neg) * st.cfg.global_cols;
+        if ((rc = rg::comm_begin(st.cfg.comm, s, st.cfg.owner_scores[st.own_unit % 2], len))) return rc;
+        if ((rc = rg::comm_end(st.cfg.comm, s))) return rc;
+    }
+    if ((rc = owner_mid(st, s, loss_out))) return rc;
+    if ((rc = rg::comm_begin(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+        return rc;
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    if ((rc = record(ev0, s))) return rc;
+    if ((rc = owner_user_update(st, s, next, o))) return rc;
+    if ((rc = record(ev1, s))) return rc;
+    if ((rc = rg::comm_end(st.cfg.comm, s))) return rc;
+    return owner_item_update(st, s, o, loss_out);
+}
+
 // the touched rows of the hot pass: a stamp scan (RG_HOT_SCAN=1, default) or the owner flags
 const rg_mf_mark_t *hot_mark(const Stepper &st, const rg_mf_mark_t &m) { return st.hot_scan ? &m : nullptr; }
 
@@ -612,6 +746,16 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         rg::set_error("rg_mf_stepper_create: null sampler buffers");
         return nullptr;
     }
+    if (cfg->dp_mode == 2) {
+        const int64_t segs = rg_mf_owner_segments(cfg->global_cols, cfg->n_neg);
+        if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world || !cfg->item_grad ||
+            cfg->cols != cfg->global_cols || cfg->col_offset != 0 || segs <= 0 ||
+            cfg->loss == RG_LOSS_ADAPTIVE_HINGE || !cfg->owner_rec[0] || !cfg->owner_rec[1] ||
+            !cfg->owner_seg[0] || !cfg->owner_seg[1] || !cfg->owner_scores[0] || !cfg->owner_scores[1]) {
+            rg::set_error("rg_mf_stepper_create: inconsistent owner-sharded data-parallel configuration");
+            return nullptr;
+        }
+    }
     if (cfg->dp_mode == 1) {
         const rg_mf_tables_t &t = cfg->tables[0];
         if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world || !cfg->grad_buf ||
@@ -640,7 +784,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         const char *im = getenv("RG_MT_INLINE");
         const int mode = im ? atoi(im) : 1;
         st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
-                         cfg->dp_mode != 1 && (mode == 2 || walk_us <= 0.85 * dense_us);
+                         cfg->dp_mode == 0 && (mode == 2 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
         st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
         if (st->G < 1) st->G = 1;
@@ -680,7 +824,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->cp_pos = (int32_t)pos;
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
-    if (env_flag("RG_MT_JUMP", cfg->dp_mode == 1 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
+    if (env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
     return st;
 }
 
@@ -700,6 +844,11 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
                                                "(or rg_mf_stepper_dp_begin / _dp_end around the caller's exchange)");
         return train_dp(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     }
+    if (st->cfg.dp_mode == 2) {
+        if (!st->cfg.comm) return rg::fail_arg("rg_mf_stepper_train: owner-sharded DP step needs a communicator "
+                                               "(or rg_mf_stepper_owner_begin / _mid / _end around the exchanges)");
+        return train_owner(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+    }
     if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
         return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     return train_split(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
@@ -718,6 +867,44 @@ extern "C" int rg_mf_stepper_dp_end(void *h, void *stream, float *loss_out) {
     if (!st) return rg::fail_arg("rg_mf_stepper_dp_end: null handle");
     if (st->cfg.dp_mode != 1) return rg::fail_arg("rg_mf_stepper_dp_end: stepper is not in dp_mode 1");
     return dp_end(*st, (hipStream_t)stream, loss_out);
+}
+
+extern "C" int rg_mf_stepper_owner_begin(void *h, void *stream, const rg_mf_step_in_t *cur) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !cur) return rg::fail_arg("rg_mf_stepper_owner_begin: null handle/input");
+    if (st->cfg.dp_mode != 2) return rg::fail_arg("rg_mf_stepper_owner_begin: stepper is not in dp_mode 2");
+    if (st->own_stage != 0) return rg::fail_arg("rg_mf_stepper_owner_begin: the previous step is not finished");
+    return owner_begin(*st, (hipStream_t)stream, *cur);
+}
+
+extern "C" int rg_mf_stepper_owner_mid(void *h, void *stream, float *loss_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_owner_mid: null handle");
+    if (st->cfg.dp_mode != 2) return rg::fail_arg("rg_mf_stepper_owner_mid: stepper is not in dp_mode 2");
+    return owner_mid(*st, (hipStream_t)stream, loss_out);
+}
+
+extern "C" int rg_mf_stepper_owner_end(void *h, void *stream, const rg_mf_step_in_t *next, float *loss_out,
+                                       void *ev0, void *ev1) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_owner_end: null handle");
+    if (st->cfg.dp_mode != 2 || st->own_stage != 2)
+        return rg::fail_arg("rg_mf_stepper_owner_end: needs dp_mode 2 after owner_mid");
+    hipStream_t s = (hipStream_t)stream;
+    st->cfg.step += 1;
+    const rg_opt_t o = opt_at(*st, st->cfg.step);
+    int rc = record(ev0, s);
+    if (rc || (rc = owner_user_update(*st, s, next, o)) || (rc = record(ev1, s))) return rc;
+    return owner_item_update(*st, s, o, loss_out);
+}
+
+extern "C" int rg_mf_stepper_owner_scores(void *h, float **scores_out, int64_t *len_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !scores_out || !len_out) return rg::fail_arg("rg_mf_stepper_owner_scores: null argument");
+    if (st->cfg.dp_mode != 2 || st->own_unit < 0) return rg::fail_arg("rg_mf_stepper_owner_scores: no owner step yet");
+    *scores_out = st->cfg.owner_scores[st->own_unit % 2];
+    *len_out = (int64_t)(1 + st->cfg.n_neg) * st->cfg.global_cols;
+    return RG_OK;
 }
 
 extern "C" int rg_mf_stepper_acquire(void *h, void *stream, const rg_mf_step_in_t *cur, rg_mf_batch_t *batch_out,

@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from . import _mtstate
-from .mf_engine import MFEngine, build_plan
+from .mf_engine import MFEngine
 from .ncf_engine import NCFEngine
 from .spotlight.factorization.representations import BilinearNet
 from .spotlight.optimizers import describe
@@ -178,11 +178,10 @@ class ImplicitFactorizationModel:
         losses = torch.zeros(nb, dtype=torch.float32, device=dev)
         total = {"train_loss": [], "validation_loss": [], "curr_epoch": []}
         # the batches repeat every epoch (one shuffle): plans (and MF step inputs) are built once
+        # (one launch builds every batch's plan, rg_mf_plans_build)
+        plans = e.make_plans(ti)
         if self._kind == "mf":
-            plans = [build_plan(ti[s * B:(s + 1) * B], B, e.units_per_block, e.I) for s in range(nb)]
             inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
-        else:
-            plans = [e.make_plan(ti[s * B:(s + 1) * B]) for s in range(nb)]
         for epoch in range(self._n_iter):
             for s in range(nb):
                 if self._kind == "mf":

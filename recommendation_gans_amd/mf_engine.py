@@ -106,44 +106,57 @@ class DeviceSampler:
         self.state.copy_(_as_u32_tensor(mt_state, self.device))
 
 
-MFPlan = namedtuple("MFPlan", "perm pos_slot item_slot_off")
+MFPlan = namedtuple("MFPlan", "perm pos_slot item_slot_off n_planned", defaults=(None,))
+
+
+def build_plans(items, batch_size, units_per_block, num_items, *, offset=0, stride=None, n_batches=None,
+                users=None, world=1, rank=0, cols=None):
+    """Per-batch plans (include/rg_hip.h rg_mf_work_t): positives processed in
+    item-sorted column order, one partial slot per (item, pair-kernel block), built on
+    the device for every batch in ONE launch (rg_mf_plans_build, rg_plan.hip).
+
+    Batch k covers positives [offset + k*stride, offset + k*stride + batch_size) of
+    ``items`` (device int64).  ``world`` > 1: only the positives whose user (``users``)
+    this ``rank`` owns (u % world == rank) are planned -- the owner-sharded data-parallel
+    step.  The reference shuffles the training set once per fit (implicit.py:262), so
+    every epoch revisits the same batches: plans are built once per fit.  Returns a list
+    of MFPlan (views into three shared tensors; ``n_planned`` = planned positives)."""
+    lib = _lib.load()
+    dev = items.device
+    stride = stride or batch_size
+    n = items.numel()
+    if n_batches is None:
+        n_batches = max(0, -(-(n - offset) // stride))
+    cols = cols or batch_size
+    if n_batches == 0:
+        return []
+    perm = torch.empty(n_batches * cols, dtype=torch.int32, device=dev)
+    pos_slot = torch.empty(n_batches * cols, dtype=torch.int32, device=dev)
+    off = torch.empty(n_batches * (num_items + 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(2 * n_batches, dtype=torch.int32, device=dev)
+    sl = int(lib.rg_mf_plans_scratch_len(cols, n_batches))
+    scratch = torch.empty(max(sl, 1), dtype=torch.int64, device=dev) if sl > 0 else None
+    for t in (items, users):
+        if t is not None and (t.dtype != torch.int64 or not t.is_contiguous() or t.device != dev):
+            raise ValueError("plan inputs must be contiguous int64 tensors on one device")
+    check(lib.rg_mf_plans_build(_lib.stream_handle(), ptr(users) if world > 1 else None, ptr(items), n, offset,
+                                stride, batch_size, n_batches, cols, units_per_block, num_items, world, rank,
+                                ptr(perm), ptr(pos_slot), ptr(off), ptr(counts), ptr(scratch)), "rg_mf_plans_build")
+    planned = counts.cpu().numpy()[0::2]
+    return [MFPlan(perm[k * cols:(k + 1) * cols], pos_slot[k * cols:(k + 1) * cols],
+                   off[k * (num_items + 1):(k + 1) * (num_items + 1)], int(planned[k])) for k in range(n_batches)]
 
 
 def build_plan(pos_i, cols, units_per_block, num_items):
-    """Per-batch plan (include/rg_hip.h, rg_mf_work_t): process positives in
-    item-sorted column order; one partial slot per (item, pair-kernel block).
-
-    The reference shuffles the training set once per fit (implicit.py:262), so
-    every epoch revisits the same batches: plans are loop-invariant and are
-    built once per fit (``build_epoch_plans``)."""
-    dev = pos_i.device
-    n_pos = pos_i.numel()
-    items_sorted, order = torch.sort(pos_i, stable=True)
-    perm = torch.cat([order, torch.arange(n_pos, cols, device=dev)]).to(torch.int32)
-    blk = torch.arange(n_pos, device=dev) // units_per_block
-    new = torch.ones(n_pos, dtype=torch.bool, device=dev)
-    if n_pos > 1:
-        new[1:] = (items_sorted[1:] != items_sorted[:-1]) | (blk[1:] != blk[:-1])
-    slot = torch.cumsum(new.to(torch.int32), 0) - 1
-    pos_slot = torch.full((cols,), -1, dtype=torch.int32, device=dev)
-    pos_slot[:n_pos] = slot.to(torch.int32)
-    seg_items = items_sorted[new]
-    off = torch.searchsorted(seg_items, torch.arange(num_items + 1, device=dev)).to(torch.int32)
-    return MFPlan(perm.contiguous(), pos_slot.contiguous(), off.contiguous())
+    """The plan of one batch (see build_plans); ``pos_i``: its positives' items."""
+    return build_plans(pos_i.contiguous(), max(1, pos_i.numel()), units_per_block, num_items, n_batches=1,
+                       cols=cols)[0]
 
 
 def build_epoch_plans(items, batch_size, units_per_block, num_items, offset=0, stride=None):
     """Plans of every batch of an epoch: batch k covers positives
     [offset + k*stride, offset + k*stride + batch_size) of ``items`` (device int64)."""
-    stride = stride or batch_size
-    plans = []
-    n = items.numel()
-    k = 0
-    while offset + k * stride < n:
-        lo = offset + k * stride
-        plans.append(build_plan(items[lo:min(lo + batch_size, n)], batch_size, units_per_block, num_items))
-        k += 1
-    return plans
+    return build_plans(items, batch_size, units_per_block, num_items, offset=offset, stride=stride)
 
 
 class MFEngine:
@@ -165,7 +178,14 @@ class MFEngine:
         "user_shard" (opt-in, faster, NOT the reference's sampling at R > 1): the tables
             passed are this rank's user shard plus every item (sharding.py); own MT stream,
             own sub-pool and positives, the item gradient is the only exchange (``comm``,
-            else ``train_step_sharded``)."""
+            else ``train_step_sharded``);
+        "owner" (default when world_size > 1, reference-exact like "global_stream"): the
+            FULL tables are passed and this rank keeps the users u % R == rank (local rows
+            u // R) and every item; every rank walks the one global draw over the full pool
+            and keeps the pairs whose user it owns; the step exchanges the pairs' scores and
+            the item gradient only (rg_mf_owner_*, ``comm`` or ``train_step_owner_exchange``).
+            ``batch_size`` is per rank; a step's input is the GLOBAL batch of R*B positives
+            with this rank's plan (``make_plans(items, users=...)``)."""
         _lib.require_gpu()
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
@@ -173,11 +193,15 @@ class MFEngine:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         if not 1 <= n_neg <= RG_MF_MAX_NEG:
             raise ValueError(f"num_negative_samples must be in [1, {RG_MF_MAX_NEG}] for the fused kernel")
-        dp = dp or ("global_stream" if world_size > 1 or comm is not None else None)
-        if dp not in (None, "user_shard", "global_stream"):
+        dp = dp or ("owner" if world_size > 1 or comm is not None else None)
+        if dp not in (None, "user_shard", "global_stream", "owner"):
             raise ValueError(f"unknown data-parallel layout {dp!r}")
-        if loss == "adaptive_hinge" and world_size != 1:
-            raise NotImplementedError("adaptive_hinge is implemented for world_size 1")
+        if loss == "adaptive_hinge" and (world_size != 1 or dp is not None):
+            raise NotImplementedError("adaptive_hinge is implemented for the single-rank step")
+        self.U_global = int(user_w.shape[0])
+        if dp == "owner":
+            user_w = user_w[rank::world_size]
+            user_b = torch.as_tensor(user_b).reshape(-1)[rank::world_size]
         self.lib = _lib.load()
         self.device = torch.device(device)
         dev = self.device
@@ -223,7 +247,8 @@ class MFEngine:
         pi = np.asarray(pool_i, dtype=np.int64)
         if len(pu) == 0 or len(pu) != len(pi):
             raise ValueError("negative pool must be non-empty with matching user/item arrays")
-        if pu.min() < 0 or pu.max() >= self.U or pi.min() < 0 or pi.max() >= self.I:
+        if pu.min() < 0 or pu.max() >= (self.U_global if dp == "owner" else self.U) or pi.min() < 0 or \
+                pi.max() >= self.I:
             raise ValueError("negative pool contains ids outside the model's tables")
         self.pool = torch.from_numpy(np.stack([pu, pi], 1).astype(np.int32)).to(dev).contiguous()
         self.pool_len = len(pu)
@@ -234,8 +259,11 @@ class MFEngine:
         self.comm = comm
         if dp == "global_stream":
             self.col_offset, self.global_cols = self.rank * self.batch_size, self.batch_size * self.world
+        elif dp == "owner":
+            self.col_offset, self.global_cols = 0, self.batch_size * self.world
         else:
             self.col_offset, self.global_cols = 0, self.batch_size
+        self.cols = self.global_cols if dp == "owner" else self.batch_size
         self.neg_cols = self.batch_size * self.world
         self.words_per_step = 2 * self.n_neg * self.global_cols
         self.prefetch = prefetch
@@ -244,17 +272,27 @@ class MFEngine:
         self.row_list = torch.empty(rows * RG_MF_LIST_CAP * 2, dtype=torch.int32, device=dev)
         self.hot_grad = torch.zeros(rows * self.dim, **f32)
         self.hot_bias = torch.zeros(rows, **f32)
-        self.n_partials = self.lib.rg_mf_partials_len(self.batch_size, self.dim) // 2
+        if dp == "owner":
+            self.n_partials = self.lib.rg_mf_owner_partials_len(self.global_cols, self.n_neg, self.dim,
+                                                                self.world) // 2
+        else:
+            self.n_partials = self.lib.rg_mf_partials_len(self.batch_size, self.dim) // 2
         self.partials = torch.zeros(2 * self.n_partials, **f32)
         self.scores_buf = torch.empty(self.batch_size, **f32) if loss == "adaptive_hinge" else None
         self.max_key = torch.zeros(1, dtype=torch.int64, device=dev) if loss == "adaptive_hinge" else None
         self.active_count = torch.zeros(1, dtype=torch.int32, device=dev) if loss == "adaptive_hinge" else None
         self.loss_out = torch.zeros(1, **f32)
-        self.part_row = torch.zeros(self.batch_size * self.dim, **f32)
-        self.part_bias = torch.zeros(self.batch_size, **f32)
+        self.part_row = torch.zeros(self.cols * self.dim, **f32)
+        self.part_bias = torch.zeros(self.cols, **f32)
         self.units_per_block = int(self.lib.rg_mf_plan_units_per_block(self.dim))
         self.grad_buf = None
-        self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp == "user_shard" else None
+        self.item_grad = torch.zeros(self.I * (self.dim + 1) + 1, **f32) if dp in ("user_shard", "owner") else None
+        if dp == "owner":
+            rl = int(self.lib.rg_mf_owner_rec_len(self.global_cols, self.n_neg))
+            ns = int(self.lib.rg_mf_owner_segments(self.global_cols, self.n_neg))
+            self.owner_rec = [torch.zeros(4 * rl, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.owner_seg = [torch.zeros(ns, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.owner_scores = [torch.zeros((1 + self.n_neg) * self.global_cols, **f32) for _ in range(2)]
         self.chunk = 0
         if dp == "global_stream":
             self.chunk = int(self.lib.rg_mf_grad_chunk(self.shard_users, self.shard_items, self.dim))
@@ -274,7 +312,7 @@ class MFEngine:
         cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
         cfg.pool, cfg.pool_len = ptr(self.pool), self.pool_len
         cfg.n_neg, cfg.loss = self.n_neg, LOSS_KINDS[loss]
-        cfg.cols, cfg.col_offset, cfg.global_cols = self.batch_size, self.col_offset, self.global_cols
+        cfg.cols, cfg.col_offset, cfg.global_cols = self.cols, self.col_offset, self.global_cols
         cfg.neg_cols = self.neg_cols
         cfg.item_grad = ptr(self.item_grad)
         cfg.comm = comm.handle if comm is not None else None
@@ -285,6 +323,12 @@ class MFEngine:
             cfg.dp_mode, cfg.rank, cfg.world = 1, self.rank, self.world
             cfg.shard_users, cfg.shard_items = self.shard_users, self.shard_items
             cfg.grad_buf = ptr(self.dp_grad)
+        elif dp == "owner":
+            cfg.dp_mode, cfg.rank, cfg.world = 2, self.rank, self.world
+            for k in range(2):
+                cfg.owner_rec[k] = ptr(self.owner_rec[k])
+                cfg.owner_seg[k] = ptr(self.owner_seg[k])
+                cfg.owner_scores[k] = ptr(self.owner_scores[k])
         self._stepper = self.lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + self.lib.rg_last_error().decode())
@@ -348,6 +392,18 @@ class MFEngine:
     def make_plan(self, pos_i):
         return build_plan(pos_i, self.batch_size, self.units_per_block, self.I)
 
+    def make_plans(self, items, offset=0, stride=None, users=None):
+        """Plans of every batch [offset + k*stride, +batch_size) of ``items`` in one launch;
+        owner layout: of every GLOBAL batch [k*R*B, (k+1)*R*B), this rank's positives
+        (``users`` required)."""
+        if self.dp == "owner":
+            if users is None:
+                raise ValueError("the owner-sharded layout plans this rank's positives: pass users=")
+            return build_plans(items, self.global_cols, self.units_per_block, self.I, offset=offset,
+                               stride=stride or self.global_cols, users=users, world=self.world, rank=self.rank,
+                               cols=self.global_cols)
+        return build_plans(items, self.batch_size, self.units_per_block, self.I, offset=offset, stride=stride)
+
     def _loss(self, global_pos, out):
         ia, ib = self.loss_scales(global_pos)
         return _lib.MFLoss(self.n_partials, ia, ib, ptr(out))
@@ -356,18 +412,24 @@ class MFEngine:
         for t in (pos_u, pos_i):
             if t.dtype != torch.int64 or t.device != self.device or not t.is_contiguous():
                 raise ValueError("positive ids must be contiguous int64 tensors on the engine's device")
-        if pos_u.numel() != pos_i.numel() or pos_u.numel() > self.batch_size:
-            raise ValueError("positive id batch larger than batch_size or mismatched")
+        if pos_u.numel() != pos_i.numel() or pos_u.numel() > self.cols:
+            raise ValueError("positive id batch larger than batch_size (owner layout: world * batch_size) "
+                             "or mismatched")
 
     def step_input(self, pos_u, pos_i, global_pos=None, plan=None):
         self._check_ids(pos_u, pos_i)
         n_pos = int(pos_u.numel())
+        if self.dp == "owner":
+            if plan is None or plan.n_planned is None:
+                raise ValueError("the owner-sharded step needs this rank's plan of the global batch (make_plans)")
+            global_pos = n_pos
         global_pos = n_pos * self.world if global_pos is None else int(global_pos)
         x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos, global_pos,
-                          None, None, None)
+                          None, None, None, 0)
         if plan is not None:
             x.plan_perm, x.plan_pos_slot, x.plan_item_slot_off = ptr(plan.perm), ptr(plan.pos_slot), \
                 ptr(plan.item_slot_off)
+            x.n_planned = plan.n_planned or 0
         x._keep = (pos_u, pos_i, plan)
         return x
 
@@ -391,6 +453,11 @@ class MFEngine:
                 raise RuntimeError("dp='global_stream' over several ranks needs an RcclComm (or train_step_exchange)")
             return self.train_step_exchange(cur, next_input, lambda buf, chunk: None, lambda bufs, counts: None,
                                             loss_out=loss_out)
+        if self.dp == "owner" and self.comm is None:
+            if self.world > 1:
+                raise RuntimeError("dp='owner' over several ranks needs an RcclComm (or train_step_owner_exchange)")
+            return self.train_step_owner_exchange(cur, next_input, lambda buf: None, loss_out=loss_out,
+                                                  apply_events=apply_events)
         ev0 = ev1 = None
         if apply_events is not None:
             ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
@@ -503,6 +570,37 @@ class MFEngine:
         self.dp_end(out)
         all_gather(*self.dp_gather_buffers())
         return out
+
+    # ------------------------------------------------------------------ owner-sharded DP
+    def train_step_owner_exchange(self, cur, next_input, allreduce, loss_out=None, apply_events=None):
+        """The owner-sharded step with caller-run exchanges: ``allreduce(buf)`` must sum
+        ``buf`` over the ranks in place (the score vector, then the item gradient) -- what
+        rg_mf_stepper_train does natively over RCCL."""
+        out = self.loss_out if loss_out is None else loss_out
+        st = _lib.stream_handle()
+        check(self.lib.rg_mf_stepper_owner_begin(self._stepper, st, ctypes.byref(cur)), "rg_mf_stepper_owner_begin")
+        if self.loss != "pointwise":
+            allreduce(self.current_scores())
+        check(self.lib.rg_mf_stepper_owner_mid(self._stepper, st, ptr(out)), "rg_mf_stepper_owner_mid")
+        allreduce(self.item_grad)
+        ev0 = ev1 = None
+        if apply_events is not None:
+            ev0, ev1 = (ctypes.c_void_p(e.cuda_event) for e in apply_events)
+        check(self.lib.rg_mf_stepper_owner_end(self._stepper, st, ctypes.byref(next_input)
+                                               if next_input is not None else None, ptr(out), ev0, ev1),
+              "rg_mf_stepper_owner_end")
+        return out
+
+    def current_scores(self):
+        """The score vector of the owner step in flight ((1 + n) * R * B floats)."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(self.lib.rg_mf_stepper_owner_scores(self._stepper, ctypes.byref(p), ctypes.byref(n)),
+              "rg_mf_stepper_owner_scores")
+        for t in self.owner_scores:
+            if t.data_ptr() == p.value:
+                return t[:n.value]
+        raise RuntimeError("owner score buffer not found")
 
     def train_step_sharded(self, pos_u, pos_i, global_pos, allreduce, plan=None):
         """The user-sharded step with the item-gradient exchange done by ``allreduce``

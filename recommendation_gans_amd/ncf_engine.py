@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 from ._lib import LOSS_KINDS, OPT_KINDS, RG_MF_LIST_CAP, RG_MF_MAX_NEG, check, ptr
-from .mf_engine import build_plan
+from .mf_engine import build_plan, build_plans
 
 
 class NCFEngine:
@@ -151,6 +151,10 @@ class NCFEngine:
 
     def make_plan(self, pos_i):
         return build_plan(pos_i, self.batch_size, self.tc, self.I)
+
+    def make_plans(self, items, offset=0, stride=None):
+        """Plans of every batch [offset + k*stride, +batch_size) of ``items`` in one launch."""
+        return build_plans(items, self.batch_size, self.tc, self.I, offset=offset, stride=stride)
 
     def mlp_params(self):
         """The MLP parameters as tensors of their reference shapes (views of the flat buffer)."""

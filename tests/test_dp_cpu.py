@@ -103,6 +103,54 @@ def test_global_stream_gloo_world2_equals_batch_2B(loss):
     assert all(torch.equal(a, b) for a, b in zip(out[0][0], out[1][0])), "replicas diverged"
 
 
+def _worker_owner(rank, world, port, loss, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+        local = [sharding.shard_rows(tables[0], rank, world).clone(), tables[1].clone(),
+                 sharding.shard_rows(tables[2], rank, world).clone(), tables[3].clone()]
+        o = omf.MFOracle(*local, pool_u, pool_i, state0.copy(), loss=loss, optimizer="adam", lr=1e-2,
+                         weight_decay=1e-5, n_neg=dc.N_NEG, batch_size=dc.B * world)
+        losses, states, negs = [], [], []
+        for lo, hi in dc.global_batches(world):
+            lv, nu, ni, own = omf.step_owner(o, train_u[lo:hi], train_i[lo:hi], world, rank, dist.all_reduce)
+            losses.append(lv)
+            states.append(o.state.copy())
+            negs.append((nu.numpy(), ni.numpy(), own.numpy()))
+        out[rank] = ([p.clone() for p in o.params], losses, states, negs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge"])
+def test_owner_gloo_world2_equals_batch_2B(loss):
+    """The owner-sharded layout (the default at R > 1, rg_owner.hip) at the oracle level: two
+    ranks owning users u % 2, exchanging the pairs' scores and the item gradient, == one
+    process at batch 2B; each valid draw is owned by exactly one rank."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker_owner, args=(world, _free_port(), loss, out), nprocs=world, join=True)
+    tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+    o, ref_losses, ref_states, ref_negs = dc.reference_run(tables, pool_u, pool_i, train_u, train_i, state0, world,
+                                                           loss)
+    for s, (lo, hi) in enumerate(dc.global_batches(world)):
+        owners = sum(out[r][3][s][2].astype(int) for r in range(world))
+        valid = world * dc.B if loss == "pointwise" else hi - lo
+        assert (owners[:, :valid] == 1).all() and (owners[:, valid:] == 0).all()
+    for r in range(world):
+        params, losses, states, negs = out[r]
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        for s in range(len(ref_losses)):
+            assert (states[s] == ref_states[s]).all(), (r, s, "MT state")
+            assert (negs[s][0] == ref_negs[s][0]).all() and (negs[s][1] == ref_negs[s][1]).all()
+        for k in (1, 3):
+            np.testing.assert_allclose(params[k].numpy(), o.params[k].numpy(), rtol=1e-5, atol=1e-7)
+    for k in (0, 2):
+        full = sharding.unshard_rows([out[r][0][k].numpy() for r in range(world)], dc.U)
+        np.testing.assert_allclose(full, o.params[k].numpy(), rtol=1e-5, atol=1e-7)
+
+
 def test_rank_columns_partial_batch():
     cols = dc.rank_columns(2, 1)
     assert cols[0] == (8, 16, 16) and cols[-1] == (56, 59, 11)

@@ -231,3 +231,112 @@ def test_native_rccl_step_world1():
     mp.spawn(_worker_rccl, args=(1, _free_port(), "bpr", out), nprocs=1, join=True)
     assert torch.equal(out[0][3], torch.arange(5, dtype=torch.float32))
     _check(out, 1, "bpr")
+
+
+# ------------------------------------------------------------------ owner-sharded (default at R > 1)
+def _own_engine(rank, world, loss, comm=None):
+    from recommendation_gans_amd.mf_engine import MFEngine
+    tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+    e = MFEngine(tables[0], tables[1], tables[2].reshape(-1), tables[3].reshape(-1), pool_u, pool_i, state0.copy(),
+                 loss=loss, optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=dc.N_NEG, batch_size=dc.B,
+                 device="cuda:0", rank=rank, world_size=world, dp="owner", comm=comm)
+    tu = torch.from_numpy(train_u[:dc.GS_TRAIN].astype(np.int64)).cuda()
+    ti = torch.from_numpy(train_i[:dc.GS_TRAIN].astype(np.int64)).cuda()
+    plans = e.make_plans(ti, users=tu)
+    inputs = [e.step_input(tu[lo:hi], ti[lo:hi], hi - lo, plans[g])
+              for g, (lo, hi) in enumerate(dc.global_batches(world))]
+    return e, inputs
+
+
+def _own_collect(e, inputs, step_fn):
+    losses, states, recs = [], [], []
+    for k, cur in enumerate(inputs):
+        nxt = inputs[k + 1] if k + 1 < len(inputs) else None
+        lv = step_fn(cur, nxt)
+        losses.append(float(lv[0]))
+        states.append(e.mt_state())
+        counts = e.owner_seg[k % 2].cpu().numpy()
+        rec = e.owner_rec[k % 2].view(-1, 256, 4).cpu().numpy()
+        recs.append(np.concatenate([rec[s, :counts[s], :3] for s in range(len(counts))]))
+    torch.cuda.synchronize()
+    return [p.cpu().clone() for p in e.params()], losses, states, recs
+
+
+def _worker_own_gloo(rank, world, port, loss, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        e, inputs = _own_engine(rank, world, loss)
+        out[rank] = _own_collect(e, inputs, lambda cur, nxt: e.train_step_owner_exchange(cur, nxt, dist.all_reduce))
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_own_rccl(rank, world, port, loss, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommendation_gans_amd.comm import RcclComm
+        comm = RcclComm("cuda:0")
+        e, inputs = _own_engine(rank, world, loss, comm=comm)
+        out[rank] = _own_collect(e, inputs, lambda cur, nxt: e.train_step_in(cur, nxt))
+        del e
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _own_check(out, world, loss):
+    """R owner-sharded ranks at batch B == one process at batch R*B (the oracle): losses 1e-5,
+    MT state and every negative's ids bit-exact (each valid draw kept by exactly the rank
+    owning its user), tables by tensor parity after unsharding the user rows."""
+    tables, pool_u, pool_i, train_u, train_i, state0 = dc.problem()
+    o, ref_losses, ref_states, ref_negs = dc.reference_run(tables, pool_u, pool_i, train_u, train_i, state0, world,
+                                                           loss)
+    o64, _, _, _ = dc.reference_run(tables, pool_u, pool_i, train_u, train_i, state0, world, loss,
+                                    dtype=torch.float64)
+    GC = dc.B * world
+    batches = dc.global_batches(world)
+    for s, (lo, hi) in enumerate(batches):
+        seen = np.zeros((dc.N_NEG, GC), np.int64)
+        for r in range(world):
+            rec = out[r][3][s]
+            k1, c = rec[:, 0] // GC, rec[:, 0] % GC
+            assert (k1 >= 1).all()
+            users = rec[:, 1].astype(np.int64) * world + r
+            assert (users == ref_negs[s][0][k1 - 1, c]).all(), (r, s, "negative users")
+            assert (rec[:, 2] == ref_negs[s][1][k1 - 1, c]).all(), (r, s, "negative items")
+            np.add.at(seen, (k1 - 1, c), 1)
+        valid_cols = GC if loss == "pointwise" else hi - lo
+        assert (seen[:, :valid_cols] == 1).all() and (seen[:, valid_cols:] == 0).all(), (s, "draw ownership")
+    for r in range(world):
+        params, losses, states, _ = out[r]
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        for s in range(len(ref_losses)):
+            assert (states[s] == ref_states[s]).all(), (r, s, "MT state")
+        for k in (1, 3):
+            ok, msg = omf.tensor_parity(params[k].reshape(o.params[k].shape), o.params[k], o64.params[k])
+            assert ok, (r, k, msg)
+    for k in (0, 2):
+        full = torch.from_numpy(sharding.unshard_rows([out[r][0][k].numpy() for r in range(world)], dc.U))
+        ok, msg = omf.tensor_parity(full.reshape(o.params[k].shape), o.params[k], o64.params[k])
+        assert ok, (k, msg)
+    if world > 1:
+        assert torch.equal(out[0][0][1], out[1][0][1]), "replicated items diverged"
+
+
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge"])
+def test_owner_engine_gloo_world2(loss):
+    """Two owner-sharded ranks at batch B (native parts, gloo all-reduces) == one process at 2B."""
+    out = mp.Manager().dict()
+    mp.spawn(_worker_own_gloo, args=(2, _free_port(), loss, out), nprocs=2, join=True)
+    _own_check(out, 2, loss)
+
+
+def test_owner_native_rccl_world1():
+    """The whole native owner-sharded step with its two RCCL all-reduces."""
+    out = mp.Manager().dict()
+    mp.spawn(_worker_own_rccl, args=(1, _free_port(), "bpr", out), nprocs=1, join=True)
+    _own_check(out, 1, "bpr")
