@@ -30,6 +30,7 @@ with HIP events on the stream it is launched on; `cpu_baseline` times the CPU re
 reference's algorithm incl. its random.choices sampler) on a bounded sample.
 """
 import argparse
+import contextlib
 import json
 import os
 import random
@@ -45,6 +46,20 @@ sys.path.insert(0, ROOT)
 
 METRIC = "train interactions/sec, MF-BPR dim=64 MovieLens-20M, 1→8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route file descriptor 1 to 2 (RCCL / gloo print init banners on stdout)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def algorithmic_bytes(U, I, d, B, n):
@@ -87,6 +102,8 @@ def parse():
                          "opt-in (not the reference's sampling at N > 1)")
     ap.add_argument("--dp-at-1", action="store_true",
                     help="run the DP code path at N = 1 too (identity exchange; bench-path check)")
+    ap.add_argument("--comm-at-1", action="store_true",
+                    help="with --dp-at-1 --dp owner: the native step with a one-rank RCCL communicator")
     ap.add_argument("--events-every", type=int, default=8,
                     help="record the dominant kernel's timing events on every k-th timed step")
     return ap.parse_args()
@@ -451,7 +468,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        with stdout_to_stderr():          # stdout carries only the JSON line
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
 
@@ -475,9 +493,25 @@ def main():
     comm = None
     if world > 1:
         from recommendation_gans_amd.comm import RcclComm
-        comm = RcclComm(dev)
+        with stdout_to_stderr():          # RCCL's init banner
+            comm = RcclComm(dev)
     gs = args.dp == "global_stream" and (world > 1 or args.dp_at_1)
     own = args.dp == "owner" and (world > 1 or args.dp_at_1)
+    solo_pg = False
+    if own and comm is None and args.comm_at_1:
+        # N = 1 on the DP code path: a one-rank gloo group carries the RCCL id, so the native
+        # owner step runs with its two RCCL all-reduces (and the item gradient on the
+        # communicator stream) exactly as at N > 1
+        import socket
+        from recommendation_gans_amd.comm import RcclComm
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            os.environ.setdefault("MASTER_PORT", str(sk.getsockname()[1]))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        with stdout_to_stderr():
+            dist.init_process_group("gloo", rank=0, world_size=1)
+            comm = RcclComm(dev)
+        solo_pg = True
     if own:
         # owner-sharded, reference-exact: this rank's users (u % world == rank) + every item,
         # the full pool; every global batch of B * world positives, this rank's plan of it
@@ -634,7 +668,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or solo_pg:
         del eng
         comm.close()
         dist.destroy_process_group()

@@ -45,6 +45,8 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
     return RG_OK;
 }
 
+hipStream_t comm_stream(void *h) { return h ? static_cast<Comm *>(h)->stream : nullptr; }
+
 int comm_end(void *h, hipStream_t stream) {
     Comm *c = static_cast<Comm *>(h);
     if (!c) return fail_arg("rg_comm_allreduce_end: null communicator");

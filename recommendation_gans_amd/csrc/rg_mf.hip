@@ -1046,6 +1046,7 @@ struct ApplyLaunchF {
         if (nb < 1) nb = 1;
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 0; }();
+        static const int grad_spec = [] { const char *e = getenv("RG_GRAD_SPEC"); return e ? atoi(e) : 1; }();
         if (mode == kApplyPull && spec && nt == 1)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1, true>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kApplyPull && spec)
@@ -1056,6 +1057,8 @@ struct ApplyLaunchF {
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 2>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kApplyPull)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull>), dim3(nb), dim3(kBlock), 0, s, *a);
+        else if (mode == kGradOnly && grad_spec)   // list and slot range loaded beside the count
+            hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly, 0, true>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kGradOnly)
             hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly>), dim3(nb), dim3(kBlock), 0, s, *a);
         else

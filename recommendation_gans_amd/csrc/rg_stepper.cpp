@@ -104,6 +104,7 @@ struct Stepper {
     rg_mf_step_in_t own_in{};
     int64_t own_unit = -1;
     int own_stage = 0;                    // 0 idle, 1 after begin, 2 after mid
+    hipEvent_t own_back = nullptr;        // after the owner backward (the item gradient may start)
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -570,13 +571,22 @@ int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
 }
 
 // part 2 (after the score exchange): dL/dz, contribution lists, the item rows' data gradient
-int owner_mid(Stepper &st, hipStream_t s, float *loss_out) {
+// (grad_stream: where the item gradient runs, ordered after the backward on s)
+int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr) {
     if (st.own_stage != 1) return rg::fail_arg("rg_mf_stepper_owner_mid: owner_begin must come first");
     const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
     rg_mf_work_t w = work_for(st, st.own_in);
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     int rc = rg_mf_owner_back(s, tb, &b, &w);
     if (rc) return rc;
+    if (grad_stream && grad_stream != s) {
+        hipError_t e = hipSuccess;
+        if (!st.own_back) e = hipEventCreateWithFlags(&st.own_back, hipEventDisableTiming | hipEventDisableSystemFence);
+        if (e == hipSuccess) e = hipEventRecord(st.own_back, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(grad_stream, st.own_back, 0);
+        if (e != hipSuccess) return hip_fail("stepper: order the item gradient", e);
+        s = grad_stream;
+    }
     rg_mf_loss_t l = loss_of(st, st.own_in.global_pos, loss_out);
     l.n_partials = rg_mf_owner_partials_used(st.cfg.global_cols, st.cfg.n_neg, tb->dim, st.cfg.world,
                                              st.own_in.n_planned) / 2;
@@ -621,8 +631,8 @@ int owner_item_update(Stepper &st, hipStream_t s, const rg_opt_t &o, float *loss
 }
 
 // the whole owner-sharded step with the communicator: begin -> score all-reduce (not for
-// pointwise: no pairing) -> mid -> item-gradient all-reduce on the communicator stream
-// beside the user update (+ next prepare) -> item update
+// pointwise: no pairing) -> backward; then the item gradient and its all-reduce on the
+// communicator stream beside the user update (+ next prepare) -> item update
 int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next, float *loss_out,
                 void *ev0, void *ev1) {
     int rc = owner_begin(st, s, cur);
@@ -633,8 +643,9 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         if ((rc = rg::comm_begin(st.cfg.comm, s, st.cfg.owner_scores[st.own_unit % 2], len))) return rc;
         if ((rc = rg::comm_end(st.cfg.comm, s))) return rc;
     }
-    if ((rc = owner_mid(st, s, loss_out))) return rc;
-    if ((rc = rg::comm_begin(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+    hipStream_t cs = rg::comm_stream(st.cfg.comm);
+    if ((rc = owner_mid(st, s, loss_out, cs))) return rc;
+    if ((rc = rg::comm_begin(st.cfg.comm, cs, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
         return rc;
     st.cfg.step += 1;
     const rg_opt_t o = opt_at(st, st.cfg.step);
@@ -732,6 +743,7 @@ void destroy(Stepper *st) {
         if (st->stamp[i]) hipFree(st->stamp[i]);
     }
     if (st->mark) hipEventDestroy(st->mark);
+    if (st->own_back) hipEventDestroy(st->own_back);
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
     rg::mt_jump_plan_destroy(st->jump);
