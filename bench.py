@@ -659,11 +659,19 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                                "traffic": None, "algorithmic_bytes_per_launch": alg,
                                "avg_launch_us": avg * 1e6}
+            # PMC traffic (scripts/pmc_apply.sh: FETCH_SIZE / WRITE_SIZE passes) of THIS build only:
+            # the profile is stamped with the library's hash, a profile of another build is refused
             pmc = os.path.join(ROOT, "profiles", "pmc_step.json" if fused else "pmc_back.json")
-            if world == 1 and os.path.exists(pmc):
+            if world == 1 and not own and not gs and os.path.exists(pmc):
+                import hashlib
                 p = json.load(open(pmc))
-                if p.get("dim") == d and p.get("batch") == B:
+                sha = hashlib.sha256(open(os.environ.get("RG_LIB") or rg_build.LIB, "rb").read()).hexdigest()[:16]
+                if p.get("dim") == d and p.get("batch") == B and p.get("lib_sha16") == sha:
                     out["roofline"]["traffic"] = p.get("hbm_bytes_per_step" if fused else "hbm_bytes_per_launch")
+                    out["roofline"]["traffic_source"] = f"profiles/{os.path.basename(pmc)} (lib {sha})"
+                else:
+                    out["roofline"]["traffic_source"] = (f"profiles/{os.path.basename(pmc)} is of another build "
+                                                         f"(lib {p.get('lib_sha16')} vs {sha}): not used")
         out["final_loss"] = loss_last
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)

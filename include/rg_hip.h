@@ -361,6 +361,9 @@ int rg_mf_owner_prepare(void *stream, const rg_mf_owner_batch_t *batch);
 int rg_mf_owner_scores(void *stream, const rg_mf_tables_t *tables, const rg_mf_owner_batch_t *batch);
 int rg_mf_owner_back(void *stream, const rg_mf_tables_t *tables, const rg_mf_owner_batch_t *batch,
                      rg_mf_work_t *work);
+/* run_val_iteration's loss (implicit.py:366-379) of the step from its EXCHANGED score vector
+ * (every rank computes the same value; one workgroup, fixed order) */
+int rg_mf_owner_loss(void *stream, const rg_mf_owner_batch_t *batch, float *loss_out_dev);
 
 /* Optimizer update of the rows in range from a (summed) flat gradient
  * (+ weight_decay * p).  loss_out_dev (optional) receives grad_dev's loss slot. */
@@ -492,6 +495,11 @@ int rg_mf_stepper_owner_end(void *stepper, void *stream, const rg_mf_step_in_t *
                             void *ev_begin, void *ev_end);
 /* the current unit's score vector and its length (floats) */
 int rg_mf_stepper_owner_scores(void *stepper, float **scores_out, int64_t *len_out);
+/* Validation (run_val_iteration) in the owner layout: owner_begin of `cur` (same draw stream),
+ * the caller all-reduces the scores, owner_val_end writes the batch's loss; with a
+ * communicator rg_mf_stepper_owner_val does all three. */
+int rg_mf_stepper_owner_val_end(void *stepper, void *stream, float *loss_out_dev);
+int rg_mf_stepper_owner_val(void *stepper, void *stream, const rg_mf_step_in_t *cur, float *loss_out_dev);
 /* Optimizer scalars for optimizer step `step` (1-based). */
 int rg_mf_stepper_opt(void *stepper, int64_t step, rg_opt_t *opt_out);
 int rg_mf_stepper_state(void *stepper, int32_t *current_set, int64_t *step);

@@ -265,6 +265,10 @@ SIGNATURES = [
     ("rg_mf_stepper_owner_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_mf_stepper_owner_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_owner_loss", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFOwnerBatch), ctypes.c_void_p]),
+    ("rg_mf_stepper_owner_val_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_owner_val", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                               ctypes.c_void_p]),
     ("rg_comm_reduce_scatter_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_int64]),
     ("rg_comm_allgather_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,

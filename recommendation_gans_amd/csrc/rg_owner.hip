@@ -227,6 +227,44 @@ __global__ __launch_bounds__(kBlk) void owner_back_kernel(OwnerArgs a, OwnTables
 
 __global__ __launch_bounds__(kBlk) void owner_prepare_kernel(OwnerArgs a) { owner_prepare_block(a, blockIdx.x); }
 
+// run_val_iteration's loss (implicit.py:366-379) from the exchanged score vector: every
+// rank holds every score, so each computes the whole loss (one workgroup, fixed order,
+// double accumulators) -- identical on every rank
+__global__ __launch_bounds__(1024) void owner_loss_kernel(OwnerArgs a, double inv_a, double inv_b, float *out) {
+    __shared__ double red[2][1024 / kWave];
+    const int64_t gc = a.gc;
+    const int n = a.n_neg;
+    const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
+    double sa = 0.0, sb = 0.0;
+    for (int64_t c = threadIdx.x; c < gc; c += 1024) {
+        const bool has = c < a.n_pos;
+        const float p0 = a.scores[c];
+        if (pairwise) {
+            if (!has) continue;
+            for (int k = 0; k < n; ++k) {
+                const float pk = a.scores[(1 + k) * gc + c];
+                if (a.loss == RG_LOSS_BPR) sa += (double)(1.0f - sigmoidf_ref(p0 - pk));
+                else sa += (double)fmaxf((pk - p0) + 1.0f, 0.0f);
+            }
+        } else {
+            if (has) sa += (double)(-fmaxf(logf(p0), -100.0f));
+            for (int k = 0; k < n; ++k) sb += (double)(-fmaxf(logf(1.0f - a.scores[(1 + k) * gc + c]), -100.0f));
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sa += __shfl_xor(sa, off);
+        sb += __shfl_xor(sb, off);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & (kWave - 1)) == 0) { red[0][w] = sa; red[1][w] = sb; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double ta = 0.0, tb = 0.0;
+        for (int k = 0; k < 1024 / kWave; ++k) { ta += red[0][k]; tb += red[1][k]; }
+        *out = (float)(ta * inv_a + tb * inv_b);
+    }
+}
+
 struct UpbF {
     int *upb;
     template <class L>
@@ -348,6 +386,18 @@ extern "C" int rg_mf_owner_prepare(void *stream, const rg_mf_owner_batch_t *b) {
     if (rc) return rc;
     hipLaunchKernelGGL(owner_prepare_kernel, dim3((unsigned)a.segs), dim3(kBlk), 0, (hipStream_t)stream, a);
     return check_launch("rg_mf_owner_prepare");
+}
+
+extern "C" int rg_mf_owner_loss(void *stream, const rg_mf_owner_batch_t *b, float *loss_out) {
+    OwnerArgs a;
+    int rc = owner_args(b, a);
+    if (rc) return rc;
+    if (!loss_out) return fail_arg("rg_mf_owner_loss: null output");
+    const double gp = (double)(b->n_pos > 0 ? b->n_pos : 1), n = (double)b->n_neg;
+    const double inv_a = b->loss == RG_LOSS_POINTWISE ? 1.0 / gp : 1.0 / (n * gp);
+    const double inv_b = b->loss == RG_LOSS_POINTWISE ? 1.0 / (n * (double)b->global_cols) : 0.0;
+    hipLaunchKernelGGL(owner_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, inv_a, inv_b, loss_out);
+    return check_launch("rg_mf_owner_loss");
 }
 
 extern "C" int rg_mf_owner_scores(void *stream, const rg_mf_tables_t *t, const rg_mf_owner_batch_t *b) {

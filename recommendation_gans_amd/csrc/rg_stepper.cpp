@@ -910,6 +910,31 @@ extern "C" int rg_mf_stepper_owner_end(void *h, void *stream, const rg_mf_step_i
     return owner_item_update(*st, s, o, loss_out);
 }
 
+extern "C" int rg_mf_stepper_owner_val_end(void *h, void *stream, float *loss_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !loss_out) return rg::fail_arg("rg_mf_stepper_owner_val_end: null argument");
+    if (st->cfg.dp_mode != 2 || st->own_stage != 1)
+        return rg::fail_arg("rg_mf_stepper_owner_val_end: needs dp_mode 2 after owner_begin");
+    const rg_mf_owner_batch_t b = owner_batch(*st, st->own_in, st->own_unit);
+    st->own_stage = 0;
+    return rg_mf_owner_loss((hipStream_t)stream, &b, loss_out);
+}
+
+extern "C" int rg_mf_stepper_owner_val(void *h, void *stream, const rg_mf_step_in_t *cur, float *loss_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !cur || !loss_out) return rg::fail_arg("rg_mf_stepper_owner_val: null argument");
+    if (st->cfg.dp_mode != 2 || !st->cfg.comm || st->own_stage != 0)
+        return rg::fail_arg("rg_mf_stepper_owner_val: needs dp_mode 2 with a communicator, between steps");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = owner_begin(*st, s, *cur);
+    if (rc) return rc;
+    const int64_t len = (int64_t)(1 + st->cfg.n_neg) * st->cfg.global_cols;
+    if ((rc = rg::comm_begin(st->cfg.comm, s, st->cfg.owner_scores[st->own_unit % 2], len)) ||
+        (rc = rg::comm_end(st->cfg.comm, s)))
+        return rc;
+    return rg_mf_stepper_owner_val_end(h, stream, loss_out);
+}
+
 extern "C" int rg_mf_stepper_owner_scores(void *h, float **scores_out, int64_t *len_out) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !scores_out || !len_out) return rg::fail_arg("rg_mf_stepper_owner_scores: null argument");

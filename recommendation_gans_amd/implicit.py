@@ -51,7 +51,7 @@ class ImplicitFactorizationModel:
     def __init__(self, loss="pointwise", embedding_dim=32, n_iter=10, batch_size=256, l2=0.0,
                  experiment_name="Implicit_Feedback", learning_rate=1e-2, optimizer_func=None, use_cuda=False,
                  representation=None, sparse=False, model_name="mf", random_state=None, neg_examples=None,
-                 num_negative_samples=3):
+                 num_negative_samples=3, world_size=1):
         self.exeriment_name = experiment_name
         self.experiment_folder = os.path.abspath("experiments_results/" + experiment_name)
         self.experiment_logs = os.path.join(self.experiment_folder, "result_outputs")
@@ -81,6 +81,19 @@ class ImplicitFactorizationModel:
         self.best_validation = None
         self.model_name = model_name
         self.best_epoch = -1
+        # additive: data-parallel training over world_size processes (one per GPU, under
+        # torchrun, torch.distributed initialised by the caller before any GPU work); the
+        # reference's single process at batch world_size * batch_size, reproduced by the
+        # owner-sharded layout (mf_engine.MFEngine dp="owner")
+        self._world = int(world_size)
+        self._rank = 0
+        self._full_tables = None
+        if self._world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized() or dist.get_world_size() != self._world:
+                raise RuntimeError("world_size > 1 needs torch.distributed initialised with that many ranks "
+                                   "(torchrun; mf_spotlight.py --world_size)")
+            self._rank = dist.get_rank()
         set_seed(self._random_state.randint(-10 ** 8, 10 ** 8), cuda=self._use_cuda)
 
     def __repr__(self):
@@ -140,10 +153,20 @@ class ImplicitFactorizationModel:
                             net.item_biases.weight]
             self._embedding_dim = net.user_embeddings.weight.shape[1]
             w = [p.detach() for p in self._params]
+            dp = {}
+            if self._world > 1:
+                import torch.distributed as dist
+                comm = None
+                if dist.get_backend() == "nccl":       # RCCL: the exchanges run inside the native step
+                    from .comm import RcclComm
+                    comm = RcclComm(dev)
+                dp = dict(rank=self._rank, world_size=self._world, dp="owner", comm=comm)
             self._engine = MFEngine(w[0], w[1], w[2].reshape(-1), w[3].reshape(-1), self._pool.user_ids,
-                                    self._pool.item_ids, _mtstate.current(), **common)
+                                    self._pool.item_ids, _mtstate.current(), **common, **dp)
         else:
             raise NotImplementedError("the fused steps train BilinearNet, the NCF MLP and NeuMF representations")
+        if self._world > 1 and self._kind != "mf":
+            raise NotImplementedError("world_size > 1: data-parallel training is implemented for BilinearNet")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
@@ -168,7 +191,13 @@ class ImplicitFactorizationModel:
         if not self._initialized:
             self._initialize(train_set)
         self._check_input(train_set.user_ids, train_set.item_ids)
-        e, B, dev = self._engine, self._batch_size, self._engine.device
+        e, dev = self._engine, self._engine.device
+        B = self._batch_size * self._world         # the global batch (one process at world * batch_size)
+        owner = self._world > 1
+        allreduce = None
+        if owner and e.comm is None:               # gloo process group: exchanges through torch.distributed
+            import torch.distributed as dist
+            allreduce = dist.all_reduce
         e.set_mt_state(_mtstate.current())
         tu = torch.from_numpy(np.ascontiguousarray(users, dtype=np.int64)).to(dev)
         ti = torch.from_numpy(np.ascontiguousarray(items, dtype=np.int64)).to(dev)
@@ -179,13 +208,17 @@ class ImplicitFactorizationModel:
         total = {"train_loss": [], "validation_loss": [], "curr_epoch": []}
         # the batches repeat every epoch (one shuffle): plans (and MF step inputs) are built once
         # (one launch builds every batch's plan, rg_mf_plans_build)
-        plans = e.make_plans(ti)
+        plans = e.make_plans(ti, users=tu) if owner else e.make_plans(ti)
+        vplans = e.make_plans(vi, users=vu) if owner else None
         if self._kind == "mf":
             inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
         for epoch in range(self._n_iter):
             for s in range(nb):
-                if self._kind == "mf":
-                    e.train_step_in(inputs[s], inputs[s + 1] if s + 1 < nb else None, loss_out=losses[s:s + 1])
+                nxt = inputs[s + 1] if self._kind == "mf" and s + 1 < nb else None
+                if self._kind == "mf" and allreduce is not None:
+                    e.train_step_owner_exchange(inputs[s], nxt, allreduce, loss_out=losses[s:s + 1])
+                elif self._kind == "mf":
+                    e.train_step_in(inputs[s], nxt, loss_out=losses[s:s + 1])
                 else:
                     nxt = (tu[(s + 1) * B:(s + 2) * B], ti[(s + 1) * B:(s + 2) * B], plans[s + 1]) \
                         if s + 1 < nb else None
@@ -195,7 +228,11 @@ class ImplicitFactorizationModel:
             train_epoch_loss = sum(tl) / nb
             if np.isnan(train_epoch_loss) or train_epoch_loss == 0.0:
                 raise ValueError("Degenerate epoch loss: {}".format(train_epoch_loss))
-            vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B])[0]) for s in range(0, len(vu), B)]
+            if owner:
+                vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B], plan=vplans[s // B], allreduce=allreduce)[0])
+                      for s in range(0, len(vu), B)]
+            else:
+                vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B])[0]) for s in range(0, len(vu), B)]
             valid_epoch_loss = sum(vl) / len(vl)
             if self.best_validation is None or valid_epoch_loss < self.best_validation:
                 self.best_model = [t.detach().clone() for t in e.params()]
@@ -207,16 +244,39 @@ class ImplicitFactorizationModel:
             total["train_loss"].append(np.mean(tl))
             total["validation_loss"].append(np.mean(vl))
             total["curr_epoch"].append(epoch)
-            save_statistics(experiment_log_dir=self.experiment_logs, filename="summary.csv", stats_dict=total,
-                            current_epoch=epoch, continue_from_mode=(self.starting_epoch != 0 or epoch > 0))
+            if self._rank == 0:
+                save_statistics(experiment_log_dir=self.experiment_logs, filename="summary.csv", stats_dict=total,
+                                current_epoch=epoch, continue_from_mode=(self.starting_epoch != 0 or epoch > 0))
         _mtstate.restore(e.mt_state())                 # the Python stream continues after fit
-        self._load_into_net(self.best_model)
         if self._kind == "mf":
             e.set_params(*self.best_model)
         else:
             e.set_params(self.best_model)
-        self.save_readable_model(self.experiment_saved_models, self._net.state_dict())
+        if owner:                                      # every rank gets the full best tables
+            self.best_model = self._gather_tables(self.best_model)
+            self._full_tables = [t.to(dev) for t in self.best_model]
+        self._load_into_net(self.best_model)
+        if self._rank == 0:
+            self.save_readable_model(self.experiment_saved_models, self._net.state_dict())
         logging.info("Model chosen from epoch %d", self.best_epoch)
+
+    def _gather_tables(self, local):
+        """Full (user_w, item_w, user_b, item_b) from every rank's user rows (u % R == rank,
+        local row u // R) and the replicated items."""
+        import torch.distributed as dist
+        from . import sharding
+        mine = [t.detach().cpu().numpy() for t in local]
+        shards = [None] * self._world
+        dist.all_gather_object(shards, mine[0::2])     # user rows and user biases
+        uw = sharding.unshard_rows([x[0] for x in shards], self._num_users)
+        ub = sharding.unshard_rows([x[1] for x in shards], self._num_users)
+        return [torch.from_numpy(uw), torch.from_numpy(mine[1]).clone(), torch.from_numpy(ub),
+                torch.from_numpy(mine[3]).clone()]
+
+    def _tables(self):
+        """The MF tables the evaluation reads: the engine's, or after a data-parallel fit
+        (the engine then holds this rank's users only) the gathered full tables."""
+        return self._full_tables if self._full_tables is not None else self._engine.params()
 
     def _load_into_net(self, tables):
         with torch.no_grad():
@@ -245,13 +305,24 @@ class ImplicitFactorizationModel:
         i = torch.from_numpy(np.asarray(item_ids, dtype=np.int64).reshape(-1))
         if u.numel() != i.numel():
             u = u.expand(i.numel())
+        if self._kind == "mf" and self._full_tables is not None:
+            from . import _lib
+            dev = self._engine.device
+            U, I, ub, ib = self._full_tables
+            u, i = u.to(dev).contiguous(), i.to(dev).contiguous()
+            out = torch.empty(u.numel(), dtype=torch.float32, device=dev)
+            lib = _lib.load()
+            _lib.check(lib.rg_mf_scores(_lib.stream_handle(), _lib.ptr(U), _lib.ptr(I), _lib.ptr(ub), _lib.ptr(ib),
+                                        U.shape[1], _lib.ptr(u), _lib.ptr(i), u.numel(), _lib.ptr(out)),
+                       "rg_mf_scores")
+            return out.cpu().numpy().flatten()
         return self._engine.scores(u, i).detach().cpu().numpy().flatten()
 
     def _device_scores(self, u):
         """(len(u), num_items) fp32 scores on the device: one GEMM of the tables (MF), or
         the eval-mode MLP / NeuMF over the block x items pairs."""
         if self._kind == "mf":
-            U, I, ub, ib = self._engine.params()
+            U, I, ub, ib = self._tables()
             return torch.sigmoid(U[u] @ I.T + ub[u][:, None] + ib[None, :])
         items = torch.arange(self._num_items, device=u.device)
         s = self._engine.scores(u.repeat_interleave(self._num_items), items.repeat(len(u)))

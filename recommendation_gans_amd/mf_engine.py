@@ -616,8 +616,26 @@ class MFEngine:
         self.finish_step()
         return self.loss_out
 
-    def val_loss(self, pos_u, pos_i, global_pos=None):
-        """run_val_iteration (implicit.py:366): forward + loss on the same draw stream, no update."""
+    def val_loss(self, pos_u, pos_i, global_pos=None, plan=None, allreduce=None):
+        """run_val_iteration (implicit.py:366): forward + loss on the same draw stream, no update.
+        Owner layout: (pos_u, pos_i) is the GLOBAL validation batch and ``plan`` this rank's
+        plan of it; the scores are exchanged by the communicator or ``allreduce``."""
+        if self.dp == "owner":
+            cur = self.step_input(pos_u, pos_i, None, plan)
+            out = torch.empty(1, dtype=torch.float32, device=self.device)
+            st = _lib.stream_handle()
+            if self.comm is not None:
+                check(self.lib.rg_mf_stepper_owner_val(self._stepper, st, ctypes.byref(cur), ptr(out)),
+                      "rg_mf_stepper_owner_val")
+            else:
+                if allreduce is None and self.world > 1:
+                    raise RuntimeError("owner-layout validation over several ranks needs a communicator or allreduce")
+                check(self.lib.rg_mf_stepper_owner_begin(self._stepper, st, ctypes.byref(cur)),
+                      "rg_mf_stepper_owner_begin")
+                if allreduce is not None:
+                    allreduce(self.current_scores())
+                check(self.lib.rg_mf_stepper_owner_val_end(self._stepper, st, ptr(out)), "rg_mf_stepper_owner_val_end")
+            return out
         cur = self.step_input(pos_u, pos_i, global_pos, None)
         batch, work = self._acquire(cur)
         stream = _lib.stream_handle()

@@ -21,9 +21,26 @@ from .utils.arg_extractor import get_args
 from .utils.data_provider import data_provider
 
 
+def init_data_parallel(world_size):
+    """--world_size N (additive): one process per GPU under torchrun; rank, local rank and the
+    rendezvous come from the environment.  Called before any GPU work.  The process group
+    carries the RCCL id and the final table gather; the step's exchanges run over RCCL inside
+    the native step (mf_engine.MFEngine dp="owner")."""
+    import torch.distributed as dist
+    if world_size <= 1:
+        return 0
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(local)
+    dist.init_process_group(os.environ.get("RG_DP_BACKEND", "nccl"), world_size=world_size,
+                            device_id=torch.device("cuda", local))
+    return dist.get_rank()
+
+
 def main(argv=None):
     logging.basicConfig(format="%(message)s", level=logging.INFO)
     args = get_args(argv)
+    rank = init_data_parallel(args.world_size)
     logging.info("DataSet MovieLens_%s will be used" % args.dataset)
     path = "/disk/scratch/s1877727/datasets/movielens/" if args.on_cluster else "datasets/movielens/"
     seed = 0
@@ -42,9 +59,12 @@ def main(argv=None):
                                        representation=technique, random_state=random_state,
                                        batch_size=args.batch_size, use_cuda=bool(args.use_gpu),
                                        learning_rate=args.learning_rate, optimizer_func=optim,
-                                       experiment_name=args.experiment_name, loss=args.mf_loss)
+                                       experiment_name=args.experiment_name, loss=args.mf_loss,
+                                       world_size=args.world_size)
     logging.info("Model set, training begins")
-    model.fit(train, valid, verbose=True)
+    model.fit(train, valid, verbose=rank == 0)
+    if rank != 0:                       # every rank holds the gathered model; rank 0 evaluates and logs
+        return model
     logging.info("Model is ready, testing performance")
     model.test(test, item_popularity, args.k, rmse_flag=args.rmse, precision_recall=args.precision_recall,
                map_recall=args.map_recall)

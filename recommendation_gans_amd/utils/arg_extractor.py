@@ -46,6 +46,9 @@ def build_parser():
     p.add_argument("--synthetic", type=str2bool, default=None,
                    help="synthetic MovieLens-shaped data when the dataset cache files are absent (default: auto)")
     p.add_argument("--zipf", type=float, default=1.0, help="item popularity skew of the synthetic data")
+    # additive: data-parallel MF training, one process per GPU under torchrun (the reference's
+    # single process at batch world_size * batch_size)
+    p.add_argument("--world_size", type=int, default=1)
     return p
 
 

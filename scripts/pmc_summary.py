@@ -49,7 +49,11 @@ def main():
                                       "hbm_bytes_per_launch": 2 * 1024 * f + 1024 * w})
     bench = os.path.join(root, "bench_FETCH_SIZE.json")
     cfg = json.load(open(bench)) if os.path.exists(bench) else {}
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "recommendation_gans_amd",
+                       "librg_hip.so")
     res = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --steps 20",
+           "lib_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
            "dim": cfg.get("config", {}).get("embedding_dim"), "batch": cfg.get("config", {}).get("global_batch"),
            "kernels": out}
     name = "pmc_apply.json"
