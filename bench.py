@@ -189,7 +189,18 @@ def bench_ncf(args):
     CLI's defaults (mlp_embedding_dim 16, mf_embedding_dim 50), same data and loop."""
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
-    dev = torch.device("cuda:0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    comm = None
+    if world > 1:     # replicated, reference-exact NCF data parallelism (ncf_engine.py): RCCL all-reduce
+        from recommendation_gans_amd.comm import RcclComm
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+            comm = RcclComm(torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
     neumf = args.model == "neumf"
     E, B, n = (args.mlp_dim if neumf else args.dim), args.batch, args.neg
     M = args.mf_dim if neumf else 0
@@ -211,22 +222,30 @@ def bench_ncf(args):
     mlp_params = params[4:] if neumf else params[2:]
     eng = NCFEngine(params[0], params[1], mlp_params, data.pool_u, data.pool_i, mt, loss="pointwise",
                     optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0,
-                    **extra)
+                    rank=rank, world_size=world, comm=comm, **extra)
     tu = torch.from_numpy(data.train_u).to(dev)
     ti = torch.from_numpy(data.train_i).to(dev)
-    nb = len(data.train_u) // B
-    nplan = min(nb, args.warmup + args.steps)
-    plans = eng.make_plans(ti[:nplan * B])
+    GC = B * world                      # rank r: columns [g*GC + r*B, +B) of global batch g
+    nb = len(data.train_u) // GC
+    nplan = min(nb, args.warmup + args.steps + 1)
+    plans = eng.make_plans(ti[:nplan * GC], offset=rank * B, stride=GC)
+
+    def cols(g):
+        lo = g * GC + rank * B
+        return tu[lo:lo + B], ti[lo:lo + B]
     for s in range(args.warmup):
         g = s % nplan
-        eng.train_step(tu[g * B:(g + 1) * B], ti[g * B:(g + 1) * B], plan=plans[g])
+        eng.train_step(*cols(g), plan=plans[g])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     every = max(1, args.events_every)
     evs = []
     t0 = time.perf_counter()
     for s in range(args.steps):
         g = (args.warmup + s) % nplan
-        u, i = tu[g * B:(g + 1) * B], ti[g * B:(g + 1) * B]
+        u, i = cols(g)
         if s % every == 0:
             a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             eng.kernel_events = (a, b_)
@@ -234,9 +253,15 @@ def bench_ncf(args):
         else:
             eng.kernel_events = None
         g2 = (args.warmup + s + 1) % nplan
-        eng.train_step(u, i, plan=plans[g], next_step=(tu[g2 * B:(g2 + 1) * B], ti[g2 * B:(g2 + 1) * B], plans[g2]))
+        eng.train_step(u, i, plan=plans[g], next_step=(*cols(g2), plans[g2]))
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
     ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
     # NeuMF adds per example: GMF product (M) + output dot (2M) forward; dW_out (2M), the GMF
     # unit gradients (M) and both table gradients (2M) backward
@@ -246,21 +271,28 @@ def bench_ncf(args):
               "train interactions/sec, NCF MLP dim=64 MovieLens-20M (config 3)")
     workload = (f"NeuMF tower {mlp_layers(E)} + GMF {M} -> affine_output({8 + M}), " if neumf else
                 f"NCF MLP {mlp_layers(E)}->1, ")
-    out = {"metric": metric, "value": args.steps * B / el,
-           "unit": "interactions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+    out = {"metric": metric, "value": args.steps * B * world / el,
+           "unit": "interactions/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "f32", "data": f"synthetic ML-20M-shaped (U={U}, I={I}); MLP init as the reference",
            "config": {"workload": workload + f"batch {B}, {n} negatives, pointwise, adam, "
-                                             f"dropout 0.5 (device hash RNG)", "global_batch": B, "embedding_dim": E,
-                      "mf_embedding_dim": M, "parallelism": "dp1"},
+                                             f"dropout 0.5 (device hash RNG)", "global_batch": GC, "embedding_dim": E,
+                      "mf_embedding_dim": M,
+                      "parallelism": f"dp{world}" + (" replicated (embedding + MLP gradient all-reduce, "
+                                                     "reference-exact)" if world > 1 else "")},
            "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (ncf_pairs_kernel)", "achieved": ach,
                         "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
                         "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
            "final_loss": float(eng.loss_out[0])}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = ncf_cpu_baseline([p.clone() for p in params], names, data, B, n, neumf,
                                                args.cpu_baseline_seconds)
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        del eng
+        comm.close()
+        dist.destroy_process_group()
 
 
 def gan_flops(N, S, H, E, Z, B):

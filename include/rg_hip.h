@@ -558,6 +558,24 @@ int rg_ncf_pairs(void *stream, const rg_ncf_model_t *model, const rg_mf_batch_t 
 int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *batch, rg_ncf_work_t *ncf_work, float *loss_partials);
 int rg_ncf_update(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t *ncf_work, int64_t nparts,
                   const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss);
+/* Data-parallel NCF / NeuMF step (replicated, reference-exact: R ranks take column slices of
+ * the global batch of ONE draw stream and equal the single process at batch R*B):
+ *   rg_ncf_mlp_grad   the MLP weight-gradient reduce of rg_ncf_update without the update:
+ *                     grad[0, P) and this rank's loss share (loss->inv_*: global means) in grad[P]
+ *   rg_ncf_grads      the embedding rows' data gradient pulled into grad = [nr*D | nr | 0]
+ *                     (nr = row_end - row_begin; gmf = 1: NeuMF GMF tables, whose lists are kept
+ *                     for the MLP tables' pass that follows)
+ * the caller all-reduces the buffers, then
+ *   rg_ncf_mlp_apply  the MLP update from grad (loss_out <- grad[P]),
+ *   rg_ncf_apply_dense every row's in-place update from its summed gradient. */
+int rg_ncf_mlp_grad(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t *ncf_work, int64_t nparts,
+                    const float *loss_partials, const rg_mf_loss_t *loss, float *grad);
+int rg_ncf_mlp_apply(void *stream, const rg_ncf_model_t *model, const float *grad, const rg_opt_t *opt,
+                     float *loss_out);
+int rg_ncf_grads(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
+                 float *grad, int64_t row_begin, int64_t row_end, int32_t gmf);
+int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *model, const float *grad, const rg_opt_t *opt,
+                       int64_t row_begin, int64_t row_end, int32_t gmf);
 /* Embedding rows [row_begin, row_end) (users then items): pull + optimizer, in place. */
 int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
                  const rg_opt_t *opt, int64_t row_begin, int64_t row_end);

@@ -188,6 +188,15 @@ SIGNATURES = [
                                        ctypes.c_void_p]),
     ("rg_ncf_update", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(NCFWork),
                                      ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p, ctypes.POINTER(MFLoss)]),
+    ("rg_ncf_mlp_grad", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(NCFWork),
+                                       ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(MFLoss), ctypes.c_void_p]),
+    ("rg_ncf_mlp_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.c_void_p,
+                                        ctypes.POINTER(Opt), ctypes.c_void_p]),
+    ("rg_ncf_grads", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
+                                    ctypes.POINTER(NCFWork), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int32]),
+    ("rg_ncf_apply_dense", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.c_void_p,
+                                          ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]),
     ("rg_ncf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),

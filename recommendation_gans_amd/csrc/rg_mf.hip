@@ -1529,6 +1529,69 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
     return dispatch_dim(m->dim, f);
 }
 
+// Data-parallel NCF / NeuMF step (replicated, reference-exact): the embedding rows' data
+// gradient pulled from the lists into the flat buffer (before the exchange), and the
+// in-place update of every row from the summed buffer (after it).  gmf: the NeuMF GMF tables
+// (their rows from ncf_work->mf_contrib; the lists are kept for the MLP tables' pass).
+static int ncf_table_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw, int gmf,
+                          int64_t row_begin, int64_t row_end, ApplyArgs &a) {
+    if (!m) return fail_arg("rg_ncf_grads: null model");
+    if (gmf && (m->mf_dim < 1 || !m->mf_user_w || !m->mf_item_w)) return fail_arg("rg_ncf_grads: no GMF tables");
+    const int64_t nrows = m->num_users + m->num_items;
+    if (row_begin < 0) row_begin = 0;
+    if (row_end < 0 || row_end > nrows) row_end = nrows;
+    if (row_begin > row_end) return fail_arg("rg_ncf_grads: row_begin > row_end");
+    a = ApplyArgs{};
+    a.w_in[0] = gmf ? m->mf_user_w : m->user_w;
+    a.w_in[1] = gmf ? m->mf_item_w : m->item_w;
+    a.w_out[0] = const_cast<float *>(a.w_in[0]);
+    a.w_out[1] = const_cast<float *>(a.w_in[1]);
+    a.w_m[0] = gmf ? m->mf_user_m : m->user_w_m; a.w_m[1] = gmf ? m->mf_item_m : m->item_w_m;
+    a.w_v[0] = gmf ? m->mf_user_v : m->user_w_v; a.w_v[1] = gmf ? m->mf_item_v : m->item_w_v;
+    a.num_users = m->num_users; a.num_items = m->num_items; a.dim = gmf ? m->mf_dim : m->dim;
+    a.row_begin = row_begin; a.row_end = row_end;
+    if (w) {
+        if (!w->row_count || !w->row_list || !nw) return fail_arg("rg_ncf_grads: null scratch");
+        a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
+        a.hot_grad = gmf ? nw->mf_hot_grad : w->hot_grad;
+        a.contrib = gmf ? nw->mf_contrib : nw->contrib;
+        a.contrib_stride = 2 * (int64_t)a.dim;
+        a.keep_count = gmf != 0;
+        if (w->plan_perm) {
+            a.item_slot_off = w->plan_item_slot_off;
+            a.part_row = gmf ? nw->mf_part_row : w->part_row;
+        }
+        if (!a.hot_grad || !a.contrib) return fail_arg("rg_ncf_grads: null contribution rows / overflow rows");
+    }
+    a.has_bias = false;
+    return RG_OK;
+}
+
+extern "C" int rg_ncf_grads(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                            float *grad, int64_t row_begin, int64_t row_end, int32_t gmf) {
+    if (!w || !nw || !grad) return fail_arg("rg_ncf_grads: null argument");
+    ApplyArgs a;
+    int rc = ncf_table_args(m, w, nw, gmf, row_begin, row_end, a);
+    if (rc) return rc;
+    a.grad = grad;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kGradOnly};
+    return dispatch_dim(a.dim, f);
+}
+
+extern "C" int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *m, const float *grad, const rg_opt_t *opt,
+                                  int64_t row_begin, int64_t row_end, int32_t gmf) {
+    if (!grad || !opt) return fail_arg("rg_ncf_apply_dense: null argument");
+    ApplyArgs a;
+    int rc = ncf_table_args(m, nullptr, nullptr, gmf, row_begin, row_end, a);
+    if (rc) return rc;
+    if (opt->kind == RG_OPT_ADAM && (!a.w_m[0] || !a.w_m[1])) return fail_arg("rg_ncf_apply_dense: Adam needs m");
+    if (opt->kind != RG_OPT_SGD && (!a.w_v[0] || !a.w_v[1])) return fail_arg("rg_ncf_apply_dense: needs v");
+    a.opt = *opt;
+    a.grad = const_cast<float *>(grad);
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyDense};
+    return dispatch_dim(a.dim, f);
+}
+
 // NeuMF (spotlight/dnn_models/neuMF.py:7-55): the GMF tables take their gradient rows
 // from ncf_work->mf_contrib through the same per-row lists (kept), then the MLP tables
 // pull theirs and reset the lists (rg_ncf_apply).

@@ -272,7 +272,9 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             sI[r] = i;
             // the example's identity for dropout: recorded-mask row, or the hash key
             const int64_t colid = (kPipe && pre_ok) ? (int64_t)ncol : a.perm && s < a.cols ? (int64_t)a.perm[s] : s;
-            const int64_t gj = q == 0 ? colid : (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
+            // (global: a data-parallel rank's column slice keys its examples as the single
+            // process at the global batch does -- draw index, or column for the positive)
+            const int64_t gj = q == 0 ? a.col_offset + colid : (int64_t)(q - 1) * a.global_cols + a.col_offset + colid;
             sR[r] = (int)gj;
             sK[r] = hash32(a.seed ^ ((uint64_t)(q == 0 ? 0 : 1) << 40) ^ ((uint64_t)gj * 0x9E3779B97F4A7C15ULL));
             // list slots are claimed now (the entry does not depend on the gradient), so the
@@ -645,13 +647,25 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
 // partials (coalesced 256-B loads, four independent chains so the loads pipeline)
 // and combine in LDS in a fixed order (deterministic); block 0 also finalises the loss
 constexpr int kUpdWaves = 16;
+// mode 0: reduce + update; 1 (data parallel, before the exchange): reduce into grad[0, P)
+// and this rank's loss share into grad[P]; 2 (after it): update from grad, loss = grad[P]
 __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, float *m, float *v, const float *wpart,
                                                         int nparts, int P, rg_opt_t opt, const float *loss_partials,
                                                         int64_t n_partials, double inv_a, double inv_b,
-                                                        float *loss_out) {
+                                                        float *loss_out, int mode, float *grad) {
     __shared__ float red[kUpdWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (loss_out && blockIdx.x == 0 && wave == 0) {
+    if (mode == 2) {
+        const int e = blockIdx.x * 64 + lane;
+        if (loss_out && blockIdx.x == 0 && threadIdx.x == 0) *loss_out = grad[P];
+        if (wave != 0 || e >= P) return;
+        float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
+        mlp[e] = opt_update(opt, mlp[e], grad[e], mm, vv);
+        if (m) m[e] = mm;
+        if (v) v[e] = vv;
+        return;
+    }
+    if ((loss_out || mode == 1) && loss_partials && blockIdx.x == 0 && wave == 0) {
         double sa = 0.0, sb = 0.0;
         for (int64_t i = lane; i < n_partials; i += 64) {
             sa += (double)loss_partials[2 * i];
@@ -661,7 +675,11 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
             sa += __shfl_xor(sa, off);
             sb += __shfl_xor(sb, off);
         }
-        if (lane == 0) *loss_out = (float)(sa * inv_a + sb * inv_b);
+        if (lane == 0) {
+            const float lv = (float)(sa * inv_a + sb * inv_b);
+            if (loss_out) *loss_out = lv;
+            if (mode == 1) grad[P] = lv;
+        }
     }
     const int e = blockIdx.x * 64 + lane;
     const int q = (nparts + kUpdWaves - 1) / kUpdWaves, k0 = wave * q, k1 = min(nparts, k0 + q);
@@ -682,6 +700,10 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
     g = red[0][lane];
 #pragma unroll
     for (int w = 1; w < kUpdWaves; ++w) g += red[w][lane];
+    if (mode == 1) {
+        grad[e] = g;
+        return;
+    }
     float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
     const float p = opt_update(opt, mlp[e], g, mm, vv);
     mlp[e] = p;
@@ -911,8 +933,33 @@ extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf
                        opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,
                        nw->mlp_partials, (int)nparts, P, *opt, with_loss ? loss_partials : nullptr,
                        with_loss ? loss->n_partials : 0, with_loss ? loss->inv_a : 0.0,
-                       with_loss ? loss->inv_b : 0.0, with_loss ? loss->out : nullptr);
+                       with_loss ? loss->inv_b : 0.0, with_loss ? loss->out : nullptr, 0, nullptr);
     return check_launch("rg_ncf_update");
+}
+
+extern "C" int rg_ncf_mlp_grad(void *stream, const rg_ncf_model_t *m, const rg_ncf_work_t *nw, int64_t nparts,
+                               const float *loss_partials, const rg_mf_loss_t *loss, float *grad) {
+    if (!m || !nw || !nw->mlp_partials || !grad || !loss || !loss_partials)
+        return fail_arg("rg_ncf_mlp_grad: null argument");
+    const int P = (int)ncf_param_len(m);
+    if (P < 0) return fail_arg("rg_ncf_mlp_grad: bad dim / mf_dim");
+    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(kUpdWaves * 64), 0, (hipStream_t)stream, m->mlp,
+                       nullptr, nullptr, nw->mlp_partials, (int)nparts, P, rg_opt_t{}, loss_partials,
+                       loss->n_partials, loss->inv_a, loss->inv_b, loss->out, 1, grad);
+    return check_launch("rg_ncf_mlp_grad");
+}
+
+extern "C" int rg_ncf_mlp_apply(void *stream, const rg_ncf_model_t *m, const float *grad, const rg_opt_t *opt,
+                                float *loss_out) {
+    if (!m || !grad || !opt || !m->mlp) return fail_arg("rg_ncf_mlp_apply: null argument");
+    if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_mlp_apply: Adam needs m state");
+    if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_mlp_apply: optimizer needs v state");
+    const int P = (int)ncf_param_len(m);
+    if (P < 0) return fail_arg("rg_ncf_mlp_apply: bad dim / mf_dim");
+    hipLaunchKernelGGL(ncf_update_kernel, dim3((P + 63) / 64), dim3(kUpdWaves * 64), 0, (hipStream_t)stream, m->mlp,
+                       opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr, opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v,
+                       nullptr, 0, P, *opt, nullptr, 0, 0.0, 0.0, loss_out, 2, const_cast<float *>(grad));
+    return check_launch("rg_ncf_mlp_apply");
 }
 
 #ifdef RG_DIAG_STAMPS

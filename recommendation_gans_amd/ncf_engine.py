@@ -13,7 +13,16 @@ or a per-(step, example, unit) hash (the documented device RNG).
 NeuMF (spotlight/dnn_models/neuMF.py:7-55): pass the GMF tables (``mf_user_w``,
 ``mf_item_w``); the same kernels run with mf_dim = M, the MLP parameters end in
 affine_output (1 x (8 + M)) and its bias, and rg_neumf_apply updates the GMF tables
-before the MLP tables."""
+before the MLP tables.
+
+Data parallelism (``world_size`` > 1, one process per GPU; replicated and reference-exact):
+rank r takes columns [r*B, (r+1)*B) of each global batch of R*B positives and of ONE global
+draw of n*R*B negatives over the full pool (implicit.py:262, :290, :351-354; dropout keyed
+by the global example), with loss means over the global batch; the embedding, GMF and MLP
+data gradients (rg_ncf_grads, rg_ncf_mlp_grad) go into one flat buffer that is all-reduced
+(RCCL ``comm``, or ``allreduce`` e.g. torch.distributed), then every rank applies the same
+update (rg_ncf_apply_dense, rg_ncf_mlp_apply).  R ranks at batch B equal one process at
+batch R*B."""
 import ctypes
 
 import numpy as np
@@ -27,8 +36,11 @@ from .mf_engine import build_plan, build_plans
 class NCFEngine:
     def __init__(self, user_w, item_w, mlp_params, pool_u, pool_i, mt_state, *, loss="pointwise", optimizer="adam",
                  lr=1e-3, weight_decay=0.0, betas=(0.5, 0.999), eps=1e-8, alpha=0.99, n_neg=5, batch_size=256,
-                 device="cuda", seed=0, mf_user_w=None, mf_item_w=None):
+                 device="cuda", seed=0, mf_user_w=None, mf_item_w=None, rank=0, world_size=1, comm=None):
         _lib.require_gpu()
+        self.rank, self.world, self.comm = int(rank), int(world_size), comm
+        if self.world > 1 and loss == "adaptive_hinge":
+            raise NotImplementedError("adaptive_hinge is implemented for world_size 1 (global max over all negatives)")
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
         if optimizer not in OPT_KINDS:
@@ -91,7 +103,15 @@ class NCFEngine:
         self.scores_buf = torch.zeros(self.rows, **f32)
         self.dp_buf = torch.zeros(self.rows, **f32)
         self.loss_out = torch.zeros(1, **f32)
+        self.neg_cols = B * self.world
         M = self.M
+        # data parallel: [embedding rows (U+I)(E+1)+1 | GMF rows (U+I)(M+1)+1 | MLP P+1], one all-reduce
+        self.dp_flat = None
+        if self.world > 1:
+            ne, nm = rows * (E + 1) + 1, (rows * (M + 1) + 1) if self.neumf else 0
+            self.dp_flat = torch.zeros(ne + nm + self.P + 1, **f32)
+            self.dp_emb, self.dp_gmf = self.dp_flat[:ne], self.dp_flat[ne:ne + nm]
+            self.dp_mlp = self.dp_flat[ne + nm:]
         self.mf_contrib = torch.zeros(self.rows * 2 * M, **f32) if self.neumf else None
         self.mf_hot_grad = torch.zeros(rows * M, **f32) if self.neumf else None
         self.mf_part_row = torch.zeros(B * M, **f32) if self.neumf else None
@@ -119,7 +139,7 @@ class NCFEngine:
         cfg.pairs[0], cfg.pairs[1] = ptr(self.pairs[0]), ptr(self.pairs[1])
         cfg.pool, cfg.pool_len = ptr(self.pool), len(pu)
         cfg.n_neg, cfg.loss = n, LOSS_KINDS[loss]
-        cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, 0, B, B
+        cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, self.rank * B, B * self.world, B * self.world
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
@@ -180,7 +200,7 @@ class NCFEngine:
     def _loss(self, global_pos, out):
         n = self.n_neg
         if self.loss == "pointwise":
-            ia, ib = 1.0 / global_pos, 1.0 / (n * self.batch_size)
+            ia, ib = 1.0 / global_pos, 1.0 / (n * self.neg_cols)
         elif self.loss in ("bpr", "hinge"):
             ia, ib = 1.0 / (n * global_pos), 0.0
         else:
@@ -200,24 +220,29 @@ class NCFEngine:
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 0), "rg_ncf_pairs")
 
-    @staticmethod
-    def _step_in_of(pos_u, pos_i, global_pos, plan):
+    def _step_in_of(self, pos_u, pos_i, global_pos, plan):
         n_pos = int(pos_u.numel())
         x = _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos,
-                          n_pos if global_pos is None else int(global_pos), None, None, None)
+                          n_pos * self.world if global_pos is None else int(global_pos), None, None, None)
         if plan is not None:
             x.plan_perm, x.plan_pos_slot, x.plan_item_slot_off = ptr(plan.perm), ptr(plan.pos_slot), \
                 ptr(plan.item_slot_off)
         return x
 
-    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None, next_step=None):
+    def train_step(self, pos_u, pos_i, global_pos=None, plan=None, masks=None, loss_out=None, next_step=None,
+                   allreduce=None):
         """One step; ``masks`` = (mask_pos [B, units] uint8, mask_neg [n*B, units] uint8) device
         tensors recorded from the reference, or None for the device dropout RNG.  The loss
         goes to ``loss_out`` (float32 device tensor) or the engine's own slot.  ``next_step``
         = (pos_u, pos_i, plan) of the following step: its negatives are prepared on the
-        side stream while this step's updates run (rg_mf_stepper_prefetch)."""
+        side stream while this step's updates run (rg_mf_stepper_prefetch).  Data parallel:
+        (pos_u, pos_i) are this rank's columns of the global batch, ``global_pos`` its size
+        (default R * n_pos), ``masks`` (if given) the GLOBAL batch's, and the exchange runs on
+        ``comm`` or ``allreduce(flat)``."""
         n_pos = int(pos_u.numel())
-        global_pos = n_pos if global_pos is None else int(global_pos)
+        global_pos = n_pos * self.world if global_pos is None else int(global_pos)
+        if self.world > 1 and self.comm is None and allreduce is None:
+            raise RuntimeError("a data-parallel NCF step needs an RcclComm or an allreduce")
         x = self._step_in_of(pos_u, pos_i, global_pos, plan)
         stream = _lib.stream_handle()
         batch, work = _lib.MFBatch(), _lib.MFWork()
@@ -239,6 +264,8 @@ class NCFEngine:
         o = self._opt(self.t)
         parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials
         out = self.loss_out if loss_out is None else loss_out
+        if self.world > 1:
+            return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce)
         check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
                                      ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
               "rg_ncf_update")
@@ -251,14 +278,39 @@ class NCFEngine:
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out
 
+    def _dp_update(self, work, nw, o, parts, global_pos, out, stream, allreduce):
+        """Data-parallel second half: data gradients -> one all-reduce -> the same update on
+        every rank."""
+        M, ref = self._model, ctypes.byref
+        check(self.lib.rg_ncf_mlp_grad(stream, ref(M), ref(nw), self.blocks, ptr(parts),
+                                       ref(self._loss(global_pos, out)), ptr(self.dp_mlp)), "rg_ncf_mlp_grad")
+        if self.neumf:
+            check(self.lib.rg_ncf_grads(stream, ref(M), ref(work), ref(nw), ptr(self.dp_gmf), 0, -1, 1),
+                  "rg_ncf_grads(gmf)")
+        check(self.lib.rg_ncf_grads(stream, ref(M), ref(work), ref(nw), ptr(self.dp_emb), 0, -1, 0), "rg_ncf_grads")
+        if self.comm is not None:
+            self.comm.allreduce_(self.dp_flat)
+        else:
+            allreduce(self.dp_flat)
+        check(self.lib.rg_ncf_mlp_apply(stream, ref(M), ptr(self.dp_mlp), ref(o), ptr(out)), "rg_ncf_mlp_apply")
+        check(self.lib.rg_ncf_apply_dense(stream, ref(M), ptr(self.dp_emb), ref(o), 0, -1, 0), "rg_ncf_apply_dense")
+        if self.neumf:
+            check(self.lib.rg_ncf_apply_dense(stream, ref(M), ptr(self.dp_gmf), ref(o), 0, -1, 1),
+                  "rg_ncf_apply_dense(gmf)")
+        check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
+        return out
+
     def _step_in(self, pos_u, pos_i, global_pos):
         n_pos = int(pos_u.numel())
         return _lib.MFStepIn(ptr(pos_u) if n_pos else None, ptr(pos_i) if n_pos else None, n_pos,
                              n_pos if global_pos is None else int(global_pos), None, None, None)
 
-    def val_loss(self, pos_u, pos_i, global_pos=None):
+    def val_loss(self, pos_u, pos_i, global_pos=None, allreduce=None):
         """run_val_iteration (implicit.py:366-379): eval-mode forward (no dropout) and the
-        loss on the same negative stream; no update."""
+        loss on the same negative stream; no update.  Data parallel: this rank's columns,
+        loss shares summed by ``comm`` / ``allreduce``."""
+        if global_pos is None:
+            global_pos = int(pos_u.numel()) * self.world
         x = self._step_in(pos_u, pos_i, global_pos)
         stream = _lib.stream_handle()
         batch, work = _lib.MFBatch(), _lib.MFWork()
@@ -280,6 +332,11 @@ class NCFEngine:
         check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
         check(self.lib.rg_loss_finalize(stream, ptr(parts), l.n_partials, l.inv_a, l.inv_b, ptr(out)),
               "rg_loss_finalize")
+        if self.world > 1:
+            if self.comm is not None:
+                self.comm.allreduce_(out)
+            else:
+                allreduce(out)
         return out
 
     def params(self):
