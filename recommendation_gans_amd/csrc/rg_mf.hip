@@ -37,6 +37,10 @@ constexpr int kCap = RG_MF_LIST_CAP;
 #endif
 constexpr int kNMax = RG_MF_MAX_NEG;
 constexpr int kBlock = 256;
+#ifndef RG_MF_PAIR_BLOCK
+#define RG_MF_PAIR_BLOCK 256
+#endif
+constexpr int kPairBlock = RG_MF_PAIR_BLOCK;   // threads of a pair-pass workgroup (the plan's block)
 
 // kFused: forward + loss + lists.  kLossOnly: forward + loss (validation).
 // Adaptive hinge needs the global max first: kAdaptFwd (scores + max),
@@ -94,7 +98,7 @@ __device__ int g_diag_flags;   // timing only (results are wrong): bit 0 skip th
         if (g_diag_stamps) {                                                                          \
             unsigned long long t_;                                                                    \
             asm volatile("s_waitcnt vmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-            if ((threadIdx.x & 63) == 0) g_diag_stamps[(blk * (kBlock / 64) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+            if ((threadIdx.x & 63) == 0) g_diag_stamps[(blk * (kPairBlock / 64) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
         }                                                                                             \
     } while (0)
 #else
@@ -164,7 +168,7 @@ __device__ __forceinline__ T pick(const T (&x)[N], int q) {
     return r;
 }
 
-constexpr int kLdsFloats = 1280;   // >= units per block * (dim + 1) for every layout
+constexpr int kLdsFloats = 1280 * (kPairBlock / 256);   // >= units per block * (dim + 1) for every layout
 
 // One unit = one batch column: pair q = 0 is the positive, q = 1..n the
 // negatives k*global_cols + col.  Every gather uses an always-valid index and is
@@ -181,11 +185,11 @@ constexpr int kLdsFloats = 1280;   // >= units per block * (dim + 1) for every l
 template <class L, int PHASE, int NMAX>
 __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk) {
     constexpr int LPU = L::LPU, EPL = L::EPL, NP = NMAX + 1;
-    constexpr int UPB = kBlock / LPU;                  // units per block
+    constexpr int UPB = kPairBlock / LPU;                  // units per block
     constexpr int TPL = (2 * NP + LPU - 1) / LPU;      // list tasks per lane
     constexpr bool kBackward = (PHASE == kFused) || (PHASE == kAdaptBwd);
     constexpr bool kScoresFromBuf = (PHASE == kAdaptBwd) || (PHASE == kAdaptLoss);
-    __shared__ float red[2][kBlock / kWave];
+    __shared__ float red[2][kPairBlock / kWave];
     __shared__ float lrow[kLdsFloats];
     __shared__ int lslot[UPB];
     __shared__ float ldz[kBackward ? UPB * NP : 1];
@@ -447,7 +451,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         if (threadIdx.x == 0) {
             float sa = 0.0f, sb = 0.0f;
 #pragma unroll
-            for (int i = 0; i < kBlock / kWave; ++i) { sa += red[0][i]; sb += red[1][i]; }
+            for (int i = 0; i < kPairBlock / kWave; ++i) { sa += red[0][i]; sb += red[1][i]; }
             a.partials[2 * blk] = sa;
             a.partials[2 * blk + 1] = sb;
         }
@@ -456,7 +460,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
 }
 
 template <class L, int PHASE, int NMAX>
-__global__ __launch_bounds__(kBlock) void mf_pairs_kernel(PairsArgs a) {
+__global__ __launch_bounds__(kPairBlock) void mf_pairs_kernel(PairsArgs a) {
     pairs_body<L, PHASE, NMAX>(a, blockIdx.x);
 }
 
@@ -528,6 +532,36 @@ struct ApplyArgs {
     int32_t world, rank;
 };
 
+#ifndef RG_MF_SORTED_PULL
+#define RG_MF_SORTED_PULL 1
+#endif
+// sort the first ne of kCap list entries ascending by (other, dz bits) -- an 8-input
+// sorting network (19 compare-exchanges, register only); entries past ne key as +inf
+__device__ __forceinline__ uint64_t ent_key(int2 e, bool valid) {
+    return valid ? ((uint64_t)(uint32_t)e.x << 32) | (uint64_t)(uint32_t)e.y : ~0ull;
+}
+__device__ __forceinline__ void sort_entries(int2 (&ent)[8], int ne) {
+    uint64_t k[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) k[e] = ent_key(ent[e], e < ne);
+#define RG_CX(i, j)                                     \
+    {                                                   \
+        const uint64_t lo = k[i] < k[j] ? k[i] : k[j];  \
+        const uint64_t hi = k[i] < k[j] ? k[j] : k[i];  \
+        k[i] = lo;                                      \
+        k[j] = hi;                                      \
+    }
+    RG_CX(0, 2) RG_CX(1, 3) RG_CX(4, 6) RG_CX(5, 7)
+    RG_CX(0, 4) RG_CX(1, 5) RG_CX(2, 6) RG_CX(3, 7)
+    RG_CX(0, 1) RG_CX(2, 3) RG_CX(4, 5) RG_CX(6, 7)
+    RG_CX(2, 4) RG_CX(3, 5)
+    RG_CX(1, 4) RG_CX(3, 6)
+    RG_CX(1, 2) RG_CX(3, 4) RG_CX(5, 6)
+#undef RG_CX
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ent[e] = make_int2((int)(uint32_t)(k[e] >> 32), (int)(uint32_t)k[e]);
+}
+
 // location of unified row r's gradient in the flat buffer: *row_base + k*D, bias at *bias
 __device__ __forceinline__ void grad_loc(const ApplyArgs &a, int t, int64_t lr_, int64_t gk, int64_t nr,
                                          const float *&row_base, int64_t &k, int64_t &bias) {
@@ -551,10 +585,22 @@ enum ApplyMode : int { kApplyPull = 0, kGradOnly = 1, kApplyDense = 2, kApplyCol
 // loss of the step from the pair kernel's per-block partials (one wave, fixed order)
 __device__ __forceinline__ float finalize_loss(const float *__restrict__ partials, int64_t np_, double inv_a,
                                                double inv_b, int lane) {
+    // eight partials per lane in flight per round (the owner step's backward leaves ~3k): one
+    // round trip per 512 partials instead of per 64; fixed order, so the sum is deterministic
+    constexpr int kU = 8;
     double sa = 0.0, sb = 0.0;
-    for (int64_t i = lane; i < np_; i += kWave) {
-        sa += (double)partials[2 * i];
-        sb += (double)partials[2 * i + 1];
+    for (int64_t i0 = lane; i0 < np_; i0 += kU * kWave) {
+        float2 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + (int64_t)u * kWave;
+            v[u] = i < np_ ? reinterpret_cast<const float2 *>(partials)[i] : make_float2(0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            sa += (double)v[u].x;
+            sb += (double)v[u].y;
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         sa += __shfl_xor(sa, off);
@@ -580,7 +626,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     float p[EPL], m[EPL], v[EPL], g[EPL];
     float pb = 0.0f, mb = 0.0f, vb = 0.0f;
     if (MODE != kGradOnly) {
-        if (NT >= 2) {
+        if (NT == 2) {
             L::load_nt(p, a.w_in[t], lr_, D, sub);
             if (adam) L::load_nt(m, a.w_m[t], lr_, D, sub); else L::zero(m);
             if (has_v) L::load_nt(v, a.w_v[t], lr_, D, sub); else L::zero(v);
@@ -631,6 +677,12 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 #pragma unroll
             for (int e = 0; e < kCap; ++e)
                 ent[e] = e < ne ? (SPEC ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
+#if RG_MF_SORTED_PULL
+            // the entries' slots were claimed by atomics in arrival order: sorted by (partner,
+            // dz bits) the row sums them in an order independent of that timing, so a step
+            // whose rows do not overflow is bit-reproducible run to run
+            sort_entries(ent, ne);
+#endif
             // MF: the partner row of the other table; NCF: the stored gradient half
             const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
             const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
@@ -704,7 +756,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 
 #pragma unroll
     for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
-    if (NT >= 1) {
+    if (NT == 3) {          // optimizer state streamed past the caches, the new row kept (next gathers)
+        L::store(a.w_out[t], lr_, D, sub, p);
+        if (adam) L::store_nt(a.w_m[t], lr_, D, sub, m);
+        if (has_v) L::store_nt(a.w_v[t], lr_, D, sub, v);
+    } else if (NT >= 1) {
         L::store_nt(a.w_out[t], lr_, D, sub, p);
         if (adam) L::store_nt(a.w_m[t], lr_, D, sub, m);
         if (has_v) L::store_nt(a.w_v[t], lr_, D, sub, v);
@@ -866,7 +922,7 @@ template <class L, int NMAX>
 __global__ __launch_bounds__(kBlock) void mf_front_kernel(PairsArgs pa, PairsArgs prep, ApplyArgs aa, FrontArgs f) {
     const int64_t blk = blockIdx.x;
     if (blk < f.pair_blocks) {
-        pairs_body<L, kFused, NMAX>(pa, blk);
+        if constexpr (kPairBlock == kBlock) pairs_body<L, kFused, NMAX>(pa, blk);   // (host refuses otherwise)
         return;
     }
     if (blk < f.pair_blocks + f.prep_blocks) {
@@ -978,7 +1034,7 @@ __global__ __launch_bounds__(kWave) void loss_finalize_kernel(const float *__res
 
 template <class L>
 int64_t pairs_blocks(int64_t cols) {
-    constexpr int64_t UPB = kBlock / L::LPU;
+    constexpr int64_t UPB = kPairBlock / L::LPU;
     return (cols + UPB - 1) / UPB;
 }
 
@@ -997,7 +1053,7 @@ struct PartialsLenF {
 struct UnitsPerBlockF {
     int64_t *upb;
     template <class L>
-    int operator()() { *upb = kBlock / L::LPU; return 0; }
+    int operator()() { *upb = kPairBlock / L::LPU; return 0; }
 };
 
 struct PairsLaunchF {
@@ -1014,20 +1070,20 @@ struct PairsLaunchF {
         const int64_t nb = pairs_blocks<L>(a->cols);
         if (!adaptive) {
             if (backward)
-                hipLaunchKernelGGL((mf_pairs_kernel<L, kFused, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+                hipLaunchKernelGGL((mf_pairs_kernel<L, kFused, NMAX>), dim3(nb), dim3(kPairBlock), 0, s, *a);
             else
-                hipLaunchKernelGGL((mf_pairs_kernel<L, kLossOnly, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+                hipLaunchKernelGGL((mf_pairs_kernel<L, kLossOnly, NMAX>), dim3(nb), dim3(kPairBlock), 0, s, *a);
             return check_launch("rg_mf_pairs");
         }
         if (hipMemsetAsync(a->max_key, 0, sizeof(unsigned long long), s) != hipSuccess ||
             hipMemsetAsync(a->active_count, 0, sizeof(int32_t), s) != hipSuccess)
             return check_launch("rg_mf_pairs(adaptive memset)");
-        hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptFwd, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+        hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptFwd, NMAX>), dim3(nb), dim3(kPairBlock), 0, s, *a);
         if (backward) {
-            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptBwd, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptBwd, NMAX>), dim3(nb), dim3(kPairBlock), 0, s, *a);
             hipLaunchKernelGGL((mf_adapt_max_kernel<L>), dim3(1), dim3(kWave), 0, s, *a);
         } else {
-            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptLoss, NMAX>), dim3(nb), dim3(kBlock), 0, s, *a);
+            hipLaunchKernelGGL((mf_pairs_kernel<L, kAdaptLoss, NMAX>), dim3(nb), dim3(kPairBlock), 0, s, *a);
         }
         return check_launch("rg_mf_pairs(adaptive)");
     }
@@ -1368,6 +1424,12 @@ struct BackLaunchF {
         if (own)
             hipLaunchKernelGGL((mf_back_kernel<L, 0, true, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen,
                                bg, oa);
+        else if (spec && nt == 1)
+            hipLaunchKernelGGL((mf_back_kernel<L, 1, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
+                               oa);
+        else if (spec && nt == 3)
+            hipLaunchKernelGGL((mf_back_kernel<L, 3, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
+                               oa);
         else if (spec)
             hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
                                oa);
@@ -1435,6 +1497,7 @@ extern "C" int rg_mf_step_front(void *stream, const rg_mf_tables_t *t, const rg_
                                 const rg_mf_mark_t *cur_mark, const rg_opt_t *opt, int64_t cold_begin,
                                 int64_t cold_end, const rg_mf_batch_t *next, const rg_mf_work_t *next_w,
                                 const rg_mf_mark_t *next_mark) {
+    if (kPairBlock != kBlock) return fail_arg("rg_mf_step_front: built with a pair-pass workgroup != 256 threads");
     if (!cur_mark || !cur_mark->stamp || cur_mark->serial == 0)
         return fail_arg("rg_mf_step_front: the current step's pairs must be prepared with row marks");
     if (cur && cur->loss == RG_LOSS_ADAPTIVE_HINGE)

@@ -59,11 +59,21 @@ def test_fit_matches_reference_golden(golden_dir, tmp_path, monkeypatch, loss, i
     assert got[0] == ref[0] and len(got) == len(ref)
     for g, r in zip(got[1:], ref[1:]):
         np.testing.assert_allclose([float(x) for x in g], [float(x) for x in r], rtol=1e-5)
-    # best tables (Adam over 2 epochs: tensor-norm parity; biases vs the fp32 restatement's own error)
+    # best tables: 1e-5 relative (tensor norm) against the reference's own, or -- where Adam
+    # amplifies a cancelled gradient's rounding -- as close to the float64 restatement of the
+    # same fit (oracle.mf.fit) as the reference's fp32 tables are
+    from oracle import rng as orng
+    o64 = omf.MFOracle(torch.from_numpy(z[f"{loss}_init_U"].copy()).double(),
+                       torch.from_numpy(z[f"{loss}_init_I"].copy()).double(), torch.zeros(U, 1, dtype=torch.float64),
+                       torch.zeros(I, 1, dtype=torch.float64), z["pool_u"], z["pool_i"], z[f"{loss}_mt_state"].copy(),
+                       loss=loss, optimizer="adam", lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B)
+    nps = orng.np_seed_state(0)
+    orng.np_randint(nps, -10 ** 8, 10 ** 8, 1)
+    _, best64, _ = omf.fit(o64, z["train_u"], z["train_i"], z["valid_u"], z["valid_i"], nps, 2)
     names = ["user_embeddings_weight", "item_embeddings_weight", "user_biases_weight", "item_biases_weight"]
-    for t, nm in zip(model.best_model, names):
+    for t, nm, r64 in zip(model.best_model, names, best64):
         ref_t = torch.from_numpy(z[f"{loss}_best_{nm}"])
-        ok, msg = omf.tensor_parity(t.reshape(ref_t.shape), ref_t, rtol=1e-5 if "embeddings" in nm else 1e-4)
+        ok, msg = omf.tensor_parity(t.reshape(ref_t.shape), ref_t, r64.reshape(ref_t.shape), rtol=1e-5)
         assert ok, (nm, msg)
     np.testing.assert_allclose(model.predict(3), z[f"{loss}_predict_u3"], rtol=1e-5, atol=1e-7)
     ck = torch.load(os.path.join(model.experiment_saved_models, "best_model"), weights_only=True)

@@ -140,5 +140,5 @@ def test_fused_oracle_trajectory_prefetch(dev, monkeypatch):
         for k in range(4):
             shp = e.params()[k].shape
             ok, msg = omf.tensor_parity(e.params()[k], o.params[k].reshape(shp), o64.params[k].reshape(shp),
-                                        rtol=1e-4 if k >= 2 else 1e-5)
+                                        rtol=1e-5)
             assert ok, f"step {s} table {k}: {msg}"

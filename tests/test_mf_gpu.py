@@ -33,15 +33,14 @@ def close(got, ref, rtol=RTOL, what=""):
 
 
 def close_adam(got, ref32, ref64, what="", small=False):
-    """Adam/RMSprop trajectories.  Embedding tables: 1e-5 relative (tensor norm), or
-    within the fp32 reference's own distance to the float64 result.  The bias vectors
-    (small=True) hold few touched elements and an element whose gradient cancels to
-    ~eps gets an update g/(|g|+eps) decided by summation order, so any two fp32
-    implementations differ there by up to ~lr; they are held to 1e-4 relative.  The
-    components are pinned tightly on their own: gradients elementwise
+    """Adam/RMSprop trajectories, every table (the bias vectors included): 1e-5 relative
+    (tensor norm), or -- where an element's gradient cancels to ~eps and its update
+    g/(|g|+eps) is decided by summation order, for any fp32 implementation -- within
+    the fp32 reference's own distance to the float64 result (oracle.mf.tensor_parity).
+    The components are pinned tightly on their own: gradients elementwise
     (test_mf_gradients_elementwise), the optimizer update given identical gradients
     (test_optimizer_update_matches_torch)."""
-    ok, msg = omf.tensor_parity(got, ref32, ref64, rtol=1e-4 if small else 1e-5)
+    ok, msg = omf.tensor_parity(got, ref32, ref64, rtol=1e-5)
     assert ok, f"{what}: {msg}"
 
 
