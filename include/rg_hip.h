@@ -120,8 +120,9 @@ typedef struct rg_mf_batch {
 typedef struct rg_mf_work {
     int32_t *row_count;      /* [num_users + num_items] */
     int32_t *row_list;       /* [(num_users + num_items) * RG_MF_LIST_CAP * 2] {other row, dz bits} */
-    float *hot_grad;         /* [(num_users + num_items) * dim] overflow accumulators */
-    float *hot_bias_grad;    /* [num_users + num_items] */
+    int64_t *hot_grad;       /* [(num_users + num_items) * dim] overflow accumulators, int64 fixed
+                                point (value * 2^52): order-independent, bit-reproducible sums */
+    int64_t *hot_bias_grad;  /* [num_users + num_items], the same */
     float *loss_partials;    /* [rg_mf_partials_len(cols, dim)] */
     float *scores;           /* [cols]  (adaptive hinge only) */
     uint64_t *max_key;       /* [1] (adaptive hinge only) */
@@ -538,7 +539,9 @@ typedef struct rg_ncf_work {
     int32_t training, pad_;                 /* 0: eval (no dropout) */
     /* NeuMF only: per-example GMF gradient rows [tiles * rows_per_tile * 2M] (user | item),
      * overflow rows [(U + I) * M] (zero between steps), planned positive partials [cols * M] */
-    float *mf_contrib, *mf_hot_grad, *mf_part_row;
+    float *mf_contrib;
+    int64_t *mf_hot_grad;                   /* int64 fixed point, as rg_mf_work_t.hot_grad */
+    float *mf_part_row;
 } rg_ncf_work_t;
 
 int64_t rg_ncf_mlp_len(int32_t dim);

@@ -115,6 +115,23 @@ __device__ __forceinline__ int64_t choice_index(uint32_t w0, uint32_t w1, int64_
 
 __device__ __forceinline__ float sigmoidf_ref(float z) { return 1.0f / (1.0f + expf(-z)); }
 
+// ---------------------------------------------------------------- overflow accumulators
+// Rows touched more than RG_MF_LIST_CAP times in a step add their surplus contributions
+// atomically.  The accumulators are int64 fixed point (2^-52 resolution, range +-2048):
+// integer addition is associative, so the sum does not depend on the atomics' arrival
+// order, and a row that overflowed sums ALL of its contributions (list and surplus) this
+// way -- its gradient is then bit-reproducible whichever contributions the list took.
+// Range: a row's gradient element is a sum of dz * (embedding element) with sum |dz| of
+// order one over a whole step (the loss is a mean), so it stays far inside +-2048; the
+// resolution keeps a gradient that cancels to ~1e-8 (where Adam's g / (|g| + eps) makes
+// its relative error visible) exact to ~1e-8 relative.
+constexpr double kFixScale = 4503599627370496.0;   // 2^52
+__device__ __forceinline__ long long to_fix(float v) { return __double2ll_rn((double)v * kFixScale); }
+__device__ __forceinline__ float from_fix(long long x) { return (float)((double)x * (1.0 / kFixScale)); }
+__device__ __forceinline__ void fix_add(long long *p, float v) {
+    atomicAdd(reinterpret_cast<unsigned long long *>(p), (unsigned long long)to_fix(v));
+}
+
 // torch.optim single-tensor update of one element, in the rounding torch's CPU
 // kernels use (checked on the reference's AVX-512 build): add(alpha) and addcmul
 // fuse their final multiply-add (FMA), addcdiv rounds (value * t1) / t2 then adds,

@@ -60,7 +60,7 @@ struct PairsArgs {
     float n_a, n_b;            // mean denominators (as ATen divides: grad / numel)
     int32_t *row_count;
     int2 *row_list;
-    float *hot_grad, *hot_bias_grad;
+    long long *hot_grad, *hot_bias_grad;     // int64 fixed point (rg_common.h fix_add)
     float *partials;
     float *scores;             // adaptive: [cols] positive scores
     unsigned long long *max_key;
@@ -148,14 +148,14 @@ __global__ __launch_bounds__(kBlock) void mf_prepare_kernel(PairsArgs a, int2 *_
     prepare_one(a, out, (int64_t)blockIdx.x * kBlock + threadIdx.x);
 }
 
-// atomically add a row-vector contribution (overflow path, rare)
+// atomically add a row-vector contribution (overflow path, rare; fixed point, rg_common.h)
 template <class L>
-__device__ __forceinline__ void overflow_add(float *__restrict__ hot, int64_t row, int D, int sub, float dz,
+__device__ __forceinline__ void overflow_add(long long *__restrict__ hot, int64_t row, int D, int sub, float dz,
                                              const float (&o)[L::EPL]) {
 #pragma unroll
     for (int e = 0; e < L::EPL; ++e) {
         const int c = L::elem(sub, e);
-        if (L::VEC || c < D) atomicAdd(hot + row * (int64_t)D + c, dz * o[e]);
+        if (L::VEC || c < D) fix_add(hot + row * (int64_t)D + c, dz * o[e]);
     }
 }
 
@@ -396,11 +396,11 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                         const int64_t row = a.num_users + iid[q];
                         L::load(o, a.user_w, uid[q], D, sub);
                         overflow_add<L>(a.hot_grad, row, D, sub, dz[q], o);
-                        if (sub == 0) atomicAdd(a.hot_bias_grad + row, dz[q]);
+                        if (sub == 0) fix_add(a.hot_bias_grad + row, dz[q]);
                     } else {
                         L::load(o, a.item_w, iid[q], D, sub);
                         overflow_add<L>(a.hot_grad, uid[q], D, sub, dz[q], o);
-                        if (sub == 0) atomicAdd(a.hot_bias_grad + uid[q], dz[q]);
+                        if (sub == 0) fix_add(a.hot_bias_grad + uid[q], dz[q]);
                     }
                 }
             }
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(kWave) void mf_adapt_max_kernel(PairsArgs a) {
             if (sub == 0) a.row_list[row * kCap + sl] = make_int2(side ? pr.x : pr.y, __float_as_int(dz));
         } else {
             overflow_add<L>(a.hot_grad, row, a.dim, sub, dz, side ? ur : ir);
-            if (sub == 0) atomicAdd(a.hot_bias_grad + row, dz);
+            if (sub == 0) fix_add(a.hot_bias_grad + row, dz);
         }
     }
 }
@@ -509,7 +509,7 @@ struct ApplyArgs {
     int64_t row_begin, row_end;   // unified rows: users [0, U), items [U, U + I)
     int32_t *row_count;
     const int2 *row_list;
-    float *hot_grad, *hot_bias_grad;
+    long long *hot_grad, *hot_bias_grad;     // int64 fixed point
     const int32_t *item_slot_off; // plan: item i's partial slots [off[i], off[i+1])
     const float *part_row, *part_bias;
     rg_opt_t opt;
@@ -690,6 +690,12 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             // 1-2 entries): a later group's gathers issue only when some row of the wave needs them,
             // and the smaller register footprint raises occupancy
             constexpr int PG = RG_MF_PULL_GROUP;
+            // an overflowed row (c > kCap) sums list and surplus in fixed point (see fix_add)
+            const bool fixp = c > kCap;
+            long long gf[EPL];
+            long long gbf = 0;
+#pragma unroll
+            for (int q = 0; q < EPL; ++q) gf[q] = 0;
 #pragma unroll
             for (int h = 0; h < kCap / PG; ++h) {
                 if (h > 0 && !__any(ne > h * PG)) break;
@@ -703,23 +709,36 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
                 for (int e = 0; e < PG; ++e) {
                     if (h * PG + e < ne) {
                         const float dz = __int_as_float(ent[h * PG + e].y);
+                        if (fixp) {
 #pragma unroll
-                        for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
-                        gb += dz;
+                            for (int q = 0; q < EPL; ++q) gf[q] += to_fix(dz * o[e][q]);
+                            gbf += to_fix(dz);
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
+                            gb += dz;
+                        }
                     }
                 }
             }
-            if (c > kCap) {
-                float h[EPL];
-                L::load(h, a.hot_grad, r, D, sub);
+            if (fixp) {
+                // the surplus' accumulators (fixed point), read and reset
 #pragma unroll
-                for (int q = 0; q < EPL; ++q) g[q] += h[q];
-                L::zero(h);
-                L::store(a.hot_grad, r, D, sub, h);
-                if (sub == 0 && a.has_bias) {
-                    gb += a.hot_bias_grad[r];
-                    a.hot_bias_grad[r] = 0.0f;
+                for (int e = 0; e < EPL; ++e) {
+                    const int cc = L::elem(sub, e);
+                    if (L::VEC || cc < D) {
+                        long long *hp = a.hot_grad + r * (int64_t)D + cc;
+                        gf[e] += *hp;
+                        *hp = 0;
+                    }
                 }
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) g[q] = from_fix(gf[q]);
+                if (sub == 0 && a.has_bias) {
+                    gbf += a.hot_bias_grad[r];
+                    a.hot_bias_grad[r] = 0;
+                }
+                gb = from_fix(gbf);
             }
             if (sub == 0 && !a.keep_count) a.row_count[r] = 0;
         }
@@ -1214,7 +1233,8 @@ static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_
     }
     a.row_count = w->row_count;
     a.row_list = reinterpret_cast<int2 *>(w->row_list);
-    a.hot_grad = w->hot_grad; a.hot_bias_grad = w->hot_bias_grad;
+    a.hot_grad = reinterpret_cast<long long *>(w->hot_grad);
+    a.hot_bias_grad = reinterpret_cast<long long *>(w->hot_bias_grad);
     a.partials = w->loss_partials; a.scores = w->scores;
     a.max_key = reinterpret_cast<unsigned long long *>(w->max_key);
     a.active_count = w->active_count;
@@ -1314,7 +1334,8 @@ static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const floa
     a.row_begin = row_begin; a.row_end = row_end;
     if (w) {
         a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
-        a.hot_grad = w->hot_grad; a.hot_bias_grad = w->hot_bias_grad;
+        a.hot_grad = reinterpret_cast<long long *>(w->hot_grad);
+    a.hot_bias_grad = reinterpret_cast<long long *>(w->hot_bias_grad);
         a.partials = w->loss_partials;
         if (w->plan_perm) {
             a.item_slot_off = w->plan_item_slot_off;
@@ -1582,7 +1603,7 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
     a.num_users = m->num_users; a.num_items = m->num_items; a.dim = m->dim;
     a.row_begin = row_begin; a.row_end = row_end;
     a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
-    a.hot_grad = w->hot_grad;
+    a.hot_grad = reinterpret_cast<long long *>(w->hot_grad);
     if (w->plan_perm) { a.item_slot_off = w->plan_item_slot_off; a.part_row = w->part_row; }
     a.opt = *opt;
     a.contrib = contrib;
@@ -1616,7 +1637,7 @@ static int ncf_table_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf
     if (w) {
         if (!w->row_count || !w->row_list || !nw) return fail_arg("rg_ncf_grads: null scratch");
         a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
-        a.hot_grad = gmf ? nw->mf_hot_grad : w->hot_grad;
+        a.hot_grad = reinterpret_cast<long long *>(gmf ? nw->mf_hot_grad : w->hot_grad);
         a.contrib = gmf ? nw->mf_contrib : nw->contrib;
         a.contrib_stride = 2 * (int64_t)a.dim;
         a.keep_count = gmf != 0;
@@ -1678,7 +1699,7 @@ extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_
     a.num_users = m->num_users; a.num_items = m->num_items; a.dim = m->mf_dim;
     a.row_begin = rb; a.row_end = re;
     a.row_count = w->row_count; a.row_list = reinterpret_cast<const int2 *>(w->row_list);
-    a.hot_grad = nw->mf_hot_grad;
+    a.hot_grad = reinterpret_cast<long long *>(nw->mf_hot_grad);
     if (w->plan_perm) { a.item_slot_off = w->plan_item_slot_off; a.part_row = nw->mf_part_row; }
     a.opt = *opt;
     a.contrib = nw->mf_contrib;

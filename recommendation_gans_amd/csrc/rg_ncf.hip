@@ -88,7 +88,7 @@ struct NcfArgs {
     const int32_t *perm, *pos_slot;   // plan (optional)
     int32_t *row_count;
     int2 *row_list;
-    float *hot_grad;
+    long long *hot_grad;                  // int64 fixed point (rg_common.h fix_add)
     float *part_row;
     float *loss_partials;             // [tiles * 2]
     float *contrib;                   // [tiles * kRows * 2E]
@@ -101,7 +101,9 @@ struct NcfArgs {
     // NeuMF (mf_dim > 0)
     int mf_dim;
     const float *mf_user_w, *mf_item_w;
-    float *mf_contrib, *mf_hot_grad, *mf_part_row;
+    float *mf_contrib;
+    long long *mf_hot_grad;
+    float *mf_part_row;
 };
 
 enum NcfPhase { kNcfFused = 0, kNcfScores = 1, kNcfGivenDp = 2, kNcfLossOnly = 3 };
@@ -531,8 +533,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                     float *row = a.mf_contrib + (tile * kRows + r) * (int64_t)(2 * M);
                     row[c] = du;
                     row[M + c] = di;
-                    if (sLu[r] >= kNcfCap) atomicAdd(a.mf_hot_grad + (int64_t)sU[r] * M + c, du);
-                    if (sLi[r] >= kNcfCap) atomicAdd(a.mf_hot_grad + (a.num_users + sI[r]) * M + c, di);
+                    if (sLu[r] >= kNcfCap) fix_add(a.mf_hot_grad + (int64_t)sU[r] * M + c, du);
+                    if (sLi[r] >= kNcfCap) fix_add(a.mf_hot_grad + (a.num_users + sI[r]) * M + c, di);
                 }
                 if (a.pos_slot != nullptr) {
                     for (int e = tid; e < tc * M; e += kNcfThreads) {
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             const int sl = half ? sLi[r] : sLu[r];
             if (sl >= kNcfCap) {
                 const int64_t row = half ? a.num_users + sI[r] : (int64_t)sU[r];
-                atomicAdd(a.hot_grad + row * E + c, sX[r * (IN0 + 1) + half * E + c]);
+                fix_add(a.hot_grad + row * E + c, sX[r * (IN0 + 1) + half * E + c]);
             }
         }
         if (a.pos_slot != nullptr) {
@@ -896,12 +898,13 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     }
     a.perm = w->plan_perm; a.pos_slot = w->plan_pos_slot;
     a.row_count = w->row_count; a.row_list = reinterpret_cast<int2 *>(w->row_list);
-    a.hot_grad = w->hot_grad; a.part_row = w->part_row;
+    a.hot_grad = reinterpret_cast<long long *>(w->hot_grad); a.part_row = w->part_row;
     a.loss_partials = w->loss_partials;
     a.contrib = nw->contrib; a.wpart = nw->mlp_partials; a.scores = nw->scores; a.dp_in = nw->dp;
     a.mask_pos = nw->mask_pos; a.mask_neg = nw->mask_neg; a.seed = nw->seed; a.training = nw->training;
     a.mf_dim = m->mf_dim; a.mf_user_w = m->mf_user_w; a.mf_item_w = m->mf_item_w;
-    a.mf_contrib = nw->mf_contrib; a.mf_hot_grad = nw->mf_hot_grad; a.mf_part_row = nw->mf_part_row;
+    a.mf_contrib = nw->mf_contrib; a.mf_hot_grad = reinterpret_cast<long long *>(nw->mf_hot_grad);
+    a.mf_part_row = nw->mf_part_row;
     const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg, m->dim, m->mf_dim);
     if (blocks <= 0) return fail_arg("rg_ncf_pairs: no launch shape for this dim / mf_dim");
     if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }

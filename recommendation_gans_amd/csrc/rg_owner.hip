@@ -26,18 +26,18 @@ struct OwnTables {
 struct OwnWork {
     int32_t *row_count;
     int2 *row_list;
-    float *hot_grad, *hot_bias;
+    long long *hot_grad, *hot_bias;      // int64 fixed point (rg_common.h fix_add)
     float *partials;
     float *part_row, *part_bias;
 };
 
 template <class L>
-__device__ __forceinline__ void overflow_row(float *__restrict__ hot, int64_t row, int D, int sub, float dz,
+__device__ __forceinline__ void overflow_row(long long *__restrict__ hot, int64_t row, int D, int sub, float dz,
                                              const float (&o)[L::EPL]) {
 #pragma unroll
     for (int e = 0; e < L::EPL; ++e) {
         const int c = L::elem(sub, e);
-        if (L::VEC || c < D) atomicAdd(hot + row * (int64_t)D + c, dz * o[e]);
+        if (L::VEC || c < D) fix_add(hot + row * (int64_t)D + c, dz * o[e]);
     }
 }
 
@@ -56,7 +56,7 @@ __device__ __forceinline__ void append(const OwnWork &w, const OwnTables &t, int
         float o[L::EPL];
         L::load(o, partner_table, other, t.dim, sub);
         overflow_row<L>(w.hot_grad, row, t.dim, sub, dz, o);
-        if (sub == 0) atomicAdd(w.hot_bias + row, dz);
+        if (sub == 0) fix_add(w.hot_bias + row, dz);
     }
 }
 
@@ -422,7 +422,8 @@ extern "C" int rg_mf_owner_back(void *stream, const rg_mf_tables_t *t, const rg_
     OwnWork ow{};
     ow.row_count = w->row_count;
     ow.row_list = reinterpret_cast<int2 *>(w->row_list);
-    ow.hot_grad = w->hot_grad; ow.hot_bias = w->hot_bias_grad;
+    ow.hot_grad = reinterpret_cast<long long *>(w->hot_grad);
+    ow.hot_bias = reinterpret_cast<long long *>(w->hot_bias_grad);
     ow.partials = w->loss_partials;
     ow.part_row = w->part_row; ow.part_bias = w->part_bias;
     OwnLaunchF f{&a, own_tables(t), ow, true, (hipStream_t)stream};

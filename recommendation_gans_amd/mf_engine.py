@@ -270,8 +270,9 @@ class MFEngine:
         rows = self.U + self.I
         self.row_count = torch.zeros(rows, dtype=torch.int32, device=dev)
         self.row_list = torch.empty(rows * RG_MF_LIST_CAP * 2, dtype=torch.int32, device=dev)
-        self.hot_grad = torch.zeros(rows * self.dim, **f32)
-        self.hot_bias = torch.zeros(rows, **f32)
+        # overflow accumulators: int64 fixed point (order-independent sums, rg_common.h fix_add)
+        self.hot_grad = torch.zeros(rows * self.dim, dtype=torch.int64, device=dev)
+        self.hot_bias = torch.zeros(rows, dtype=torch.int64, device=dev)
         if dp == "owner":
             self.n_partials = self.lib.rg_mf_owner_partials_len(self.global_cols, self.n_neg, self.dim,
                                                                 self.world) // 2

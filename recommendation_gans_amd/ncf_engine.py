@@ -93,8 +93,9 @@ class NCFEngine:
         rows = self.U + self.I
         self.row_count = torch.zeros(rows, dtype=torch.int32, device=dev)
         self.row_list = torch.empty(rows * RG_MF_LIST_CAP * 2, dtype=torch.int32, device=dev)
-        self.hot_grad = torch.zeros(rows * E, **f32)
-        self.hot_bias = torch.zeros(rows, **f32)
+        # overflow accumulators: int64 fixed point (order-independent sums, rg_common.h fix_add)
+        self.hot_grad = torch.zeros(rows * E, dtype=torch.int64, device=dev)
+        self.hot_bias = torch.zeros(rows, dtype=torch.int64, device=dev)
         self.partials = torch.zeros(2 * max(self.tiles, 1), **f32)
         self.adapt_partials = torch.zeros(2, **f32)
         self.part_row = torch.zeros(B * E, **f32)
@@ -113,7 +114,7 @@ class NCFEngine:
             self.dp_emb, self.dp_gmf = self.dp_flat[:ne], self.dp_flat[ne:ne + nm]
             self.dp_mlp = self.dp_flat[ne + nm:]
         self.mf_contrib = torch.zeros(self.rows * 2 * M, **f32) if self.neumf else None
-        self.mf_hot_grad = torch.zeros(rows * M, **f32) if self.neumf else None
+        self.mf_hot_grad = torch.zeros(rows * M, dtype=torch.int64, device=dev) if self.neumf else None
         self.mf_part_row = torch.zeros(B * M, **f32) if self.neumf else None
         self.pairs = [torch.zeros(int(lib.rg_mf_pairs_len(B, n)), dtype=torch.int32, device=dev) for _ in range(2)]
         self.mt_buf = torch.from_numpy(np.ascontiguousarray(np.asarray(mt_state, np.uint32)).view(np.int32)).to(dev)
