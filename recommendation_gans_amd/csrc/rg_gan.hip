@@ -80,7 +80,10 @@ void layout(const Dims &m, int64_t *g, int64_t *d) {
     d[RG_GAN_D_END] = o;
 }
 
-constexpr int64_t kPartTileSplits = 512;   // split-K: tiles * splits <= this
+constexpr int64_t kPartTileSplits = 1024;   // split-K: tiles * splits <= this (partials buffer)
+
+// tiles * splits aimed for: one whole wave of resident workgroups (3 per CU, rg_gemm.hip)
+int64_t part_target() { return std::max<int64_t>(64, std::min<int64_t>(kPartTileSplits, 3 * num_cus())); }
 
 // workspace carve-up (floats), sized for batch_max rows (2 * batch_max stacked in D)
 struct Ws {
@@ -667,7 +670,7 @@ int gemm_small(hipStream_t st, GemmDesc d, float *part) {
 
 int pick_splits(int64_t M, int64_t N, int64_t K) {
     const int64_t tiles = gemm_tiles_m(M) * gemm_tiles_n(N);
-    int64_t s = kPartTileSplits / tiles;
+    int64_t s = part_target() / tiles;
     s = std::min<int64_t>(s, std::max<int64_t>(1, K / 256));
     return (int)std::max<int64_t>(1, s);
 }

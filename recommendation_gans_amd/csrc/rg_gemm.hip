@@ -2,9 +2,12 @@
 //
 // Block tile 128 x 128, K step 32, 256 threads = 4 waves in a 2 x 2 grid of 64 x 64
 // wave tiles, each 2 x 2 v_mfma_f32_32x32x2_f32 accumulators (64 AGPR/VGPR).
-// Operands are staged through LDS, double-buffered, one barrier per K step; the
-// next step's global loads are in flight while the current step's 64 MFMAs per
-// wave issue.  K-major operands sit in LDS as [row][k] (stride 36 floats, 4 * odd
+// Operands are staged through LDS; the next step's global loads are in flight (in
+// registers) while the current step's 64 MFMAs per wave issue.  One LDS stage and two
+// barriers per K step (33.8 KB, <= 168 registers: 3 workgroups per CU) for every
+// epilogue but the argmax, which keeps two stages (one barrier per step) for its LDS
+// tile: at 2 workgroups per CU the lock-stepped workgroups of a CU left the matrix
+// cores idle through each other's epilogues (cGAN 144k -> 166k slates/s).  K-major operands sit in LDS as [row][k] (stride 36 floats, 4 * odd
 // mod 64: the ds_read_b128 lane groups of a 32-row column read are conflict-free);
 // M/N-major operands as [k][row] (stride 132), read with ds_read_b32 across
 // consecutive rows (conflict-free).
@@ -115,16 +118,36 @@ struct TileMap {
     }
 };
 
+__host__ __device__ inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 __device__ __forceinline__ bool better(float v, float i, float bv, float bi) {
     return v > bv || (v == bv && i < bi);
 }
 
-template <bool AK, bool BKM, int EPI>
-__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
+__device__ __forceinline__ void opt1(const rg_opt_t &o, float clampv, float &p, float g, float &m, float &v) {
+    float q = p;
+    if (clampv > 0.0f) q = fminf(fmaxf(q, -clampv), clampv);
+    p = opt_update(o, q, g, m, v);
+}
+
+__device__ __forceinline__ void opt4(const rg_opt_t &o, float clampv, float4 &p, const float4 &g, float4 &m,
+                                     float4 &v) {
+    opt1(o, clampv, p.x, g.x, m.x, v.x);
+    opt1(o, clampv, p.y, g.y, m.y, v.y);
+    opt1(o, clampv, p.z, g.z, m.z, v.z);
+    opt1(o, clampv, p.w, g.w, m.w, v.w);
+}
+
+// ONE: a single operand stage (two barriers per K step) for 3 workgroups per CU instead
+// of 2 -- the LDS (33.8 KB) and register budget (<= 168 per lane) of three; the argmax
+// epilogue needs the double-buffered footprint for its tile
+template <bool AK, bool BKM, int EPI, bool ONE>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONE ? 3 : 1, 8))) void gemm_kernel(GemmDesc d) {
     constexpr int kSA = Stage<AK>::kFloats, kSB = Stage<BKM>::kFloats;
-    __shared__ __attribute__((aligned(16))) float smem[2 * kSA + 2 * kSB];
-    auto sA = [&](int b) { return smem + b * kSA; };
-    auto sB = [&](int b) { return smem + 2 * kSA + b * kSB; };
+    constexpr int kStages = ONE ? 1 : 2;
+    __shared__ __attribute__((aligned(16))) float smem[kStages * (kSA + kSB)];
+    auto sA = [&](int b) { return smem + (kStages == 2 ? b : 0) * kSA; };
+    auto sB = [&](int b) { return smem + kStages * kSA + (kStages == 2 ? b : 0) * kSB; };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
     const int h = lane >> 5, l32 = lane & 31;
     // XCD-aware order (blocks L, L + 8, L + 16, ... share an XCD and its L2): tiles are
@@ -175,6 +198,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
         if (it + 1 < nk) {
+            if constexpr (kStages == 1) __syncthreads();   // every wave is done reading the stage
             sstore<AK>(sA(buf ^ 1), ra, tid);
             sstore<BKM>(sB(buf ^ 1), rb, tid);
         }
@@ -275,45 +299,82 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
                     }
             }
         }
-        // per 16-row fragment: load p (and m, v) for all rows, update, then store
+        // the gradient tile goes through LDS (the operand stages are free after the K
+        // loop's last barrier; with ONE, one 64-row half at a time) and is re-read as
+        // float4 column groups, a wave covering two rows of 512 B, so P and its state
+        // move in dwordx4 loads / stores along rows; kQ rows in flight per thread
+        constexpr int kQ = 4;
+        const int c4 = tid & 31, r0 = tid >> 5;
+        const bool vec = n0 + 4 * c4 + 3 < d.N && (d.ldp & 3) == 0 && aligned16(d.P) && (!d.Ms || aligned16(d.Ms)) &&
+                         (!d.Vs || aligned16(d.Vs));
+        constexpr int LDE = BN + 4;
+        constexpr int kPass = kStages == 2 ? 1 : 2;   // row halves through LDS one at a time
+        constexpr int kRows = BM / kPass;
+        static_assert(kStages * (kSA + kSB) >= kRows * LDE, "LDS reuse");
+        float *tile = smem;
+        const int64_t n = n0 + 4 * c4;
+        auto update_rows = [&](float4 (&pv)[kQ], float4 (&mv)[kQ], float4 (&vv)[kQ], int q0) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+            for (int q = 0; q < kQ; ++q) {
+                const int rl = r0 + 8 * (q0 + q);
+                const int64_t m = m0 + rl, e = m * d.ldp + n;
+                if (m >= d.M) continue;
+                const float4 g = *reinterpret_cast<const float4 *>(tile + (rl % kRows) * LDE + 4 * c4);
+                if (vec) {
+                    opt4(d.opt, d.clamp_p, pv[q], g, mv[q], vv[q]);
+                    *reinterpret_cast<float4 *>(d.P + e) = pv[q];
+                    if (d.Ms) *reinterpret_cast<float4 *>(d.Ms + e) = mv[q];
+                    if (d.Vs) *reinterpret_cast<float4 *>(d.Vs + e) = vv[q];
+                } else {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int64_t n = col_of(j);
-                if (n >= d.N) continue;
-                float pp[16], mm[16], vv[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t m = row_of(i, r);
-                    const int64_t e = m * d.ldp + n;
-                    const bool ok = m < d.M;
-                    pp[r] = ok ? d.P[e] : 0.0f;
-                    mm[r] = (ok && d.Ms) ? d.Ms[e] : 0.0f;
-                    vv[r] = (ok && d.Vs) ? d.Vs[e] : 0.0f;
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    float p = pp[r];
-                    if (d.clamp_p > 0.0f) p = fminf(fmaxf(p, -d.clamp_p), d.clamp_p);
-                    pp[r] = opt_update(d.opt, p, acc[i][j][r], mm[r], vv[r]);
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t m = row_of(i, r);
-                    if (m >= d.M) continue;
-                    const int64_t e = m * d.ldp + n;
-                    d.P[e] = pp[r];
-                    if (d.Ms) d.Ms[e] = mm[r];
-                    if (d.Vs) d.Vs[e] = vv[r];
+                    for (int c = 0; c < 4; ++c) {
+                        if (n + c >= d.N) continue;
+                        float p = d.P[e + c], mm = d.Ms ? d.Ms[e + c] : 0.0f, v1 = d.Vs ? d.Vs[e + c] : 0.0f;
+                        const float gc = c == 0 ? g.x : c == 1 ? g.y : c == 2 ? g.z : g.w;
+                        opt1(d.opt, d.clamp_p, p, gc, mm, v1);
+                        d.P[e + c] = p;
+                        if (d.Ms) d.Ms[e + c] = mm;
+                        if (d.Vs) d.Vs[e + c] = v1;
+                    }
                 }
             }
+        };
+#pragma unroll
+        for (int pass = 0; pass < kPass; ++pass) {
+            if (kPass == 1 || wm == pass) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            tile[((wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) % kRows) * LDE + wn * 64 +
+                                 j * 32 + l32] = acc[i][j][r];
+            }
+            __syncthreads();
+            const int qa = pass * (kRows / 8), qb = qa + kRows / 8;
+            for (int q0 = qa; q0 < qb; q0 += kQ) {
+                float4 pv[kQ], mv[kQ], vv[kQ];
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) {
+                    const int64_t m = m0 + r0 + 8 * (q0 + q), e = m * d.ldp + n;
+                    pv[q] = mv[q] = vv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (m < d.M && vec) {
+                        pv[q] = *reinterpret_cast<const float4 *>(d.P + e);
+                        if (d.Ms) mv[q] = *reinterpret_cast<const float4 *>(d.Ms + e);
+                        if (d.Vs) vv[q] = *reinterpret_cast<const float4 *>(d.Vs + e);
+                    }
+                }
+                update_rows(pv, mv, vv, q0);
+            }
+            if (pass + 1 < kPass) __syncthreads();
+        }
     } else if constexpr (EPI == kEpiArgmax) {
         // tanh(acc + bias) of the 128 x 128 tile into LDS (the operand buffers are free
         // now), then two threads per row scan 64 columns each: the first maximum per row
         // and head segment (the tile spans heads h0 and h0 + 1)
         constexpr int LDT = BN + 1;
-        static_assert(2 * kSA + 2 * kSB >= BM * LDT, "LDS reuse");
+        static_assert(2 * kSA + 2 * kSB >= BM * LDT || EPI != kEpiArgmax, "LDS reuse");
         float *tile = smem;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -359,14 +420,13 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmDesc d) {
 template <bool AK, bool BKM>
 void launch_epi(hipStream_t stream, const GemmDesc &d, dim3 grid) {
     switch (d.epi) {
-        case kEpiStore: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiStore>), grid, dim3(kThreads), 0, stream, d); break;
-        case kEpiPartial: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiPartial>), grid, dim3(kThreads), 0, stream, d); break;
-        case kEpiOpt: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiOpt>), grid, dim3(kThreads), 0, stream, d); break;
-        default: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiArgmax>), grid, dim3(kThreads), 0, stream, d); break;
+        case kEpiStore: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiStore, true>), grid, dim3(kThreads), 0, stream, d); break;
+        case kEpiPartial: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiPartial, true>), grid, dim3(kThreads), 0, stream, d); break;
+        case kEpiOpt: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiOpt, true>), grid, dim3(kThreads), 0, stream, d); break;
+        default: hipLaunchKernelGGL((gemm_kernel<AK, BKM, kEpiArgmax, false>), grid, dim3(kThreads), 0, stream, d); break;
     }
 }
 
-bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *__restrict__ part, int splits, int64_t M,
                                                               int64_t N, float *__restrict__ C, int64_t ldc,

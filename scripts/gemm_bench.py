@@ -40,13 +40,15 @@ w1s = torch.rand(H2, KS, device=dev) * 0.01
 wh = torch.rand(KS, H, device=dev) * 0.01
 a2 = torch.rand(B, H, device=dev)
 dl1 = torch.rand(B, H2, device=dev)
-for sp in (32, 64, 128):
+RMS_ONLY = "--rms-only" in sys.argv
+for sp in (() if RMS_ONLY else (32, 64, 128)):
     run(f"D1 fwd split{sp} (AK,BK)", fake, KS, 1, w1s, KS, 1, B, H2, KS, H2, splits=sp)
-run("heads fwd tanh (AK,BK)", a2, H, 1, wh, H, 1, B, SN, H, KS, post=1)
-run("D1 dX (AK,BN)", dl1, H2, 1, w1s, KS, 0, B, SN, H2, KS)
-run("D1 dW (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, SN, B, KS)
-run("heads dW (AM,BN)", fake, KS, 0, a2, H, 0, SN, H, B, H)
-for sp in (64, 128):
+if not RMS_ONLY:
+    run("heads fwd tanh (AK,BK)", a2, H, 1, wh, H, 1, B, SN, H, KS, post=1)
+    run("D1 dX (AK,BN)", dl1, H2, 1, w1s, KS, 0, B, SN, H2, KS)
+    run("D1 dW (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, SN, B, KS)
+    run("heads dW (AM,BN)", fake, KS, 0, a2, H, 0, SN, H, B, H)
+for sp in (() if RMS_ONLY else (64, 128)):
     run(f"heads dA split{sp} (AK,BN)", fake, KS, 1, wh, H, 0, B, H, KS, H, splits=sp)
 
 

@@ -66,6 +66,41 @@ def test_gemm_bias_tanh():
     assert (got.double() - ref).abs().max() < 2e-6
 
 
+@pytest.mark.parametrize("M,N,K,ldp", [(512, 20000, 256, 20000),   # several tiles per workgroup (persistent)
+                                       (300, 1001, 64, 1004),      # K < 8 steps, ragged float4 tail column
+                                       (130, 5003, 640, 5003)])    # K > 8 steps, rows not float4-aligned
+def test_gemm_rmsprop_matches_float64(M, N, K, ldp):
+    """The gradient GEMM fused with the RMSprop update (the cGAN's W1S / WH path,
+    CGANs.py:440-457 RMSprop on D and G) against a float64 product + update of the
+    same fp32 operands: P within the f32 GEMM bound propagated through the update."""
+    from recommendation_gans_amd import _lib
+    from recommendation_gans_amd.gan_engine import ptr
+    import ctypes
+    L = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K)
+    a, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    m4, n4 = (M + 3) // 4 * 4, (N + 3) // 4 * 4
+    A = torch.cat([a.t(), torch.zeros(K, m4 - M)], 1).contiguous().cuda()
+    B = torch.cat([b.t(), torch.zeros(K, n4 - N)], 1).contiguous().cuda()
+    p0 = torch.randn(M, ldp, generator=g) * 0.01
+    v0 = torch.rand(M, ldp, generator=g) * 1e-3
+    P, V = p0.clone().cuda(), v0.clone().cuda()
+    lr, alpha, eps = 1e-3, 0.99, 1e-8
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.rg_gemm_f32_rms(st, ptr(A), m4, 0, ptr(B), n4, 0, M, N, K, ptr(P), ptr(V), ldp, lr, alpha, eps),
+               "rg_gemm_f32_rms")
+    torch.cuda.synchronize()
+    gd = a.double() @ b.double().t()
+    vd = alpha * v0[:, :N].double() + (1 - alpha) * gd * gd
+    pd = p0[:, :N].double() - lr * gd / (vd.sqrt() + eps)
+    gb = 2e-6 * (a.double().abs() @ b.double().abs().t())
+    Pg, Vg = P.cpu().double(), V.cpu().double()
+    assert ((Vg[:, :N] - vd).abs() <= 2 * gd.abs() * gb + 1e-6 * vd).all()
+    # d(lr g / sqrt(v)) / dg <= lr * 2 / sqrt(v): the GEMM bound carried through, plus f32 rounding
+    assert ((Pg[:, :N] - pd).abs() <= 2 * lr * gb / vd.sqrt() + 1e-6 * pd.abs() + 1e-9).all()
+    assert torch.equal(P.cpu()[:, N:], p0[:, N:]) and torch.equal(V.cpu()[:, N:], v0[:, N:]), "pad columns touched"
+
+
 CASES = ["gan_rms_n50", "gan_adam_n50", "gan_sgd_n64"]
 
 
