@@ -164,38 +164,50 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
 // tile read row 0 and are zeroed after), then the K/4 MFMAs issue over four
 // independent accumulators: no LDS round trip or MFMA dependency between
 // consecutive MFMAs.
-template <int K>
+template <int K, int KB = K>
 __device__ __forceinline__ v4f mma16(const float *A, int ai, int ak, const float *B, int bk, int bj, int i0, int j0,
                                      int imax, int jmax, int lane) {
-    constexpr int NK = K / 4;
+    // KB: K values read per batch (a multiple of 16 dividing K); the accumulator sequence,
+    // and so the result, does not depend on it
+    constexpr int NK = K / 4, NB = (KB < K ? KB : K) / 4;
+    static_assert(NK % NB == 0 && NB % 4 == 0 || NB == NK, "batch shape");
     const int li = lane & 15, lk = lane >> 4;
     const bool iv = i0 + li < imax, jv = j0 + li < jmax;
     const float *pa = A + (iv ? (i0 + li) : 0) * ai + lk * ak;
     const float *pb = B + lk * bk + (jv ? (j0 + li) : 0) * bj;
-    float av[NK], bv[NK];
-#pragma unroll
-    for (int s = 0; s < NK; ++s) {
-        av[s] = pa[4 * s * ak];
-        bv[s] = pb[4 * s * bk];
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the read batch ahead of the MFMAs
     v4f acc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[c] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int s = 0; s < NK; ++s)
-        acc[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? av[s] : 0.0f, jv ? bv[s] : 0.0f, acc[s & 3], 0, 0, 0);
+    for (int s0 = 0; s0 < NK; s0 += NB) {
+        float av[NB], bv[NB];
+#pragma unroll
+        for (int s = 0; s < NB; ++s) {
+            av[s] = pa[4 * (s0 + s) * ak];
+            bv[s] = pb[4 * (s0 + s) * bk];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the read batch ahead of the MFMAs
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            acc[(s0 + s) & 3] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(iv ? av[s] : 0.0f, jv ? bv[s] : 0.0f, acc[(s0 + s) & 3], 0, 0, 0);
+    }
     return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+template <int E>
+constexpr int ncf_threads() { return E >= 64 ? 512 : kNcfThreads; }
+
 template <int E, int PHASE>
-__global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
+__global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) {
+    constexpr int kNT = ncf_threads<E>(), kNW = kNT / 64;
+    constexpr int kKB = kNT > kNcfThreads ? 32 : 1024;   // MFMA operand batch (K values): registers for 2 waves / SIMD
     using S = NcfShape<E>;
     constexpr int NH = S::NH, IN0 = 2 * E;
     // E = 64 takes a CU's LDS alone (one wave per SIMD, registers to spare): its serial
     // LDS reductions are unrolled into one batch of reads; the small towers keep their
     // registers for occupancy (several tiles per CU)
-    constexpr bool kWide = E >= 64;
+    constexpr bool kWide = E >= 64 && kNT == 256;
     const int M = a.mf_dim, P = S::P + M;  // flat parameters: tower, output W (8 + M), output b
     constexpr int WO = S::w_off(NH);       // flat offset of the output layer
     extern __shared__ float lds[];
@@ -230,8 +242,8 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     // so a tile starts with its inputs in hand (the id and gather phases were ~4 us of a
     // ~26 us tile).  The small towers keep their registers for occupancy.
     constexpr bool kPipe = kWide && kBackward;
-    constexpr int kPG = kPipe ? kRows * (IN0 / 4) / kNcfThreads : 1;   // float4 per thread of A_0
-    static_assert(!kPipe || kRows * (IN0 / 4) % kNcfThreads == 0, "A_0 prefetch shape");
+    constexpr int kPG = kPipe ? kRows * (IN0 / 4) / kNT : 1;   // float4 per thread of A_0
+    static_assert(!kPipe || kRows * (IN0 / 4) % kNT == 0, "A_0 prefetch shape");
     bool pre_ok = false;                  // registers hold this tile's ids, slots and A_0
     int nu = -1, ni = -1, nps = -1, nlu = -1, nli = -1, ncol = 0;
     float4 pg[kPG];
@@ -241,12 +253,12 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         const int in = S::H(k), out = S::H(k + 1);
         const float *W = a.mlp + S::w_off(k);
         float *dst = sW + S::sw_off(k);
-        for (int e = tid; e < out * in; e += kNcfThreads) dst[(e / in) * (in + 1) + e % in] = W[e];
-        for (int e = tid; e < out; e += kNcfThreads) dst[out * (in + 1) + e] = W[out * in + e];
+        for (int e = tid; e < out * in; e += kNT) dst[(e / in) * (in + 1) + e % in] = W[e];
+        for (int e = tid; e < out; e += kNT) dst[out * (in + 1) + e] = W[out * in + e];
     }
-    for (int e = tid; e < 9; e += kNcfThreads) sW[S::sw_off(NH) + e] = a.mlp[WO + (e < 8 ? e : 8 + M)];
-    for (int e = tid; e < M; e += kNcfThreads) sWm[e] = a.mlp[WO + 8 + e];
-    for (int e = tid; e < P; e += kNcfThreads) sG[e] = 0.0f;
+    for (int e = tid; e < 9; e += kNT) sW[S::sw_off(NH) + e] = a.mlp[WO + (e < 8 ? e : 8 + M)];
+    for (int e = tid; e < M; e += kNT) sWm[e] = a.mlp[WO + 8 + e];
+    for (int e = tid; e < P; e += kNT) sG[e] = 0.0f;
     __syncthreads();
 
     for (int64_t tile = blockIdx.x; tile < a.tiles; tile += gridDim.x) {
@@ -328,12 +340,12 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         if (kPipe && pre_ok) {
 #pragma unroll
             for (int j = 0; j < kPG; ++j) {
-                const int e = tid + j * kNcfThreads, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
+                const int e = tid + j * kNT, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
                 float *d = sA + r * (IN0 + 1) + c4;
                 d[0] = pg[j].x; d[1] = pg[j].y; d[2] = pg[j].z; d[3] = pg[j].w;
             }
         } else
-        for (int e = tid; e < kRows * (IN0 / 4); e += kNcfThreads) {
+        for (int e = tid; e < kRows * (IN0 / 4); e += kNT) {
             const int r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (sU[r] >= 0)
@@ -342,7 +354,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             float *d = sA + r * (IN0 + 1) + c4;
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
-        for (int e = tid; e < kRows * 2 * M; e += kNcfThreads) {      // NeuMF GMF rows
+        for (int e = tid; e < kRows * 2 * M; e += kNT) {      // NeuMF GMF rows
             const int r = e / (2 * M), c = e % (2 * M);
             float v = 0.0f;
             if (sU[r] >= 0)
@@ -361,9 +373,9 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             const float *Wk = sW + S::sw_off(k);
             const float *bk = Wk + out * (in + 1);
             constexpr int ct = out < 16 ? 1 : out / 16;
-            for (int t = wave; t < 2 * ct; t += 4) {
+            for (int t = wave; t < 2 * ct; t += kNW) {
                 const int i0 = (t / ct) * 16, j0 = (t % ct) * 16;
-                const v4f z = mma16<in>(Ak, in + 1, 1, Wk, 1, in + 1, i0, j0, kRows, out, lane);
+                const v4f z = mma16<in, kKB>(Ak, in + 1, 1, Wk, 1, in + 1, i0, j0, kRows, out, lane);
                 const int col = j0 + (lane & 15);
                 if (col < out) {
 #pragma unroll
@@ -507,7 +519,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             const float *wo = sW + S::sw_off(NH);
             const float *AN = sA + S::sa_off(NH);
             float *MN = sM + S::sa_off(NH);
-            for (int e = tid; e < 9 + M; e += kNcfThreads) {     // e: 8 tower units, bias, M GMF units
+            for (int e = tid; e < 9 + M; e += kNT) {     // e: 8 tower units, bias, M GMF units
                 float acc = 0.0f;
                 auto term = [&](int r) {
                     return e < 8 ? AN[r * 9 + e] : e == 8 ? 1.0f : sGm[r * gs + e - 9] * sGm[r * gs + M + e - 9];
@@ -520,13 +532,13 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                 }
                 sG[WO + (e < 8 ? e : e == 8 ? 8 + M : e - 1)] += acc;
             }
-            for (int e = tid; e < kRows * 8; e += kNcfThreads) {
+            for (int e = tid; e < kRows * 8; e += kNT) {
                 const int r = e / 8, j = e % 8;
                 MN[r * 9 + j] = (sDz[r] * wo[j]) * MN[r * 9 + j];      // delta_{NH-1} = G * m
             }
             if (M > 0) {
                 // GMF backward: dU_mf = (dz w_c) I_mf, dI_mf = (dz w_c) U_mf (neuMF.py:43-50 under autograd)
-                for (int e = tid; e < kRows * M; e += kNcfThreads) {
+                for (int e = tid; e < kRows * M; e += kNT) {
                     const int r = e / M, c = e % M;
                     const float dg = sDz[r] * sWm[c];
                     const float du = dg * sGm[r * gs + M + c], di = dg * sGm[r * gs + c];
@@ -537,7 +549,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                     if (sLi[r] >= kNcfCap) fix_add(a.mf_hot_grad + (a.num_users + sI[r]) * M + c, di);
                 }
                 if (a.pos_slot != nullptr) {
-                    for (int e = tid; e < tc * M; e += kNcfThreads) {
+                    for (int e = tid; e < tc * M; e += kNT) {
                         const int cl = e / M, c = e % M;
                         const int slot = sPs[cl];
                         if (slot < 0 || (cl > 0 && sPs[cl - 1] == slot)) continue;
@@ -554,7 +566,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             if (has_next) {
 #pragma unroll
                 for (int j = 0; j < kPG; ++j) {
-                    const int e = tid + j * kNcfThreads, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
+                    const int e = tid + j * kNT, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
                     const int u2 = sUn[r], i2 = sIn[r];
                     pg[j] = u2 < 0 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
                                    : c4 < E ? *reinterpret_cast<const float4 *>(a.user_w + (int64_t)u2 * E + c4)
@@ -572,7 +584,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             float *gW = sG + S::w_off(k);
             // dW_k (out x in) += delta^T A_k ; db_k += column sums of delta
             constexpr int ro = out < 16 ? 1 : out / 16, ci = in / 16;
-            for (int t = wave; t < ro * ci; t += 4) {
+            for (int t = wave; t < ro * ci; t += kNW) {
                 const int i0 = (t / ci) * 16, j0 = (t % ci) * 16;
                 const v4f c = mma16<kRows>(Dk, 1, out + 1, Ak, in + 1, 1, i0, j0, out, in, lane);
                 const int col = j0 + (lane & 15);
@@ -582,7 +594,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
                     if (o < out) gW[o * in + col] += c[rr];
                 }
             }
-            for (int o = tid; o < out; o += kNcfThreads) {
+            for (int o = tid; o < out; o += kNT) {
                 float acc = 0.0f;
                 if constexpr (kWide) {   // one batch of LDS reads, then the same in-order sum
                     float col[kRows];
@@ -597,9 +609,9 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             }
             // dA_k = delta W_k (kRows x in): k > 0 -> delta_{k-1} = dA * m_k ; k == 0 -> dX
             constexpr int cj = in / 16;
-            for (int t = wave; t < 2 * cj; t += 4) {
+            for (int t = wave; t < 2 * cj; t += kNW) {
                 const int i0 = (t / cj) * 16, j0 = (t % cj) * 16;
-                const v4f c = mma16<(out < 4 ? 4 : out)>(Dk, out + 1, 1, Wk, in + 1, 1, i0, j0, kRows, in, lane);
+                const v4f c = mma16<(out < 4 ? 4 : out), kKB>(Dk, out + 1, 1, Wk, in + 1, 1, i0, j0, kRows, in, lane);
                 const int col = j0 + (lane & 15);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
@@ -617,7 +629,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
             if (k == NH - 1) NS(6);
         });
         // ---- embedding gradient: overflow rows (hot users/items), planned item partials -----------
-        for (int e = tid; e < 2 * kRows * E; e += kNcfThreads) {
+        for (int e = tid; e < 2 * kRows * E; e += kNT) {
             const int r = e / (2 * E), half = (e / E) & 1, c = e % E;
             const int sl = half ? sLi[r] : sLu[r];
             if (sl >= kNcfCap) {
@@ -627,7 +639,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
         }
         if (a.pos_slot != nullptr) {
             // positives' item halves, same plan slot -> one partial row (fixed order, plain stores)
-            for (int e = tid; e < tc * E; e += kNcfThreads) {
+            for (int e = tid; e < tc * E; e += kNT) {
                 const int cl = e / E, c = e % E;
                 const int slot = sPs[cl];
                 if (slot < 0 || (cl > 0 && sPs[cl - 1] == slot)) continue;   // not the segment head
@@ -641,7 +653,7 @@ __global__ __launch_bounds__(kNcfThreads) void ncf_pairs_kernel(NcfArgs a) {
     }
     // ---- the workgroup's weight-gradient partial ------------------------------------------------
     if (kBackward)
-        for (int e = tid; e < P; e += kNcfThreads) a.wpart[(int64_t)blockIdx.x * P + e] = sG[e];
+        for (int e = tid; e < P; e += kNT) a.wpart[(int64_t)blockIdx.x * P + e] = sG[e];
 }
 
 // reduce the weight-gradient partials + optimizer update of the MLP parameters in
@@ -779,7 +791,7 @@ struct NcfLaunchF {
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      kLdsMax * (int)sizeof(float)) == hipSuccess;
         if (!attr) return fail_arg("ncf_pairs_kernel: cannot reserve LDS");
-        hipLaunchKernelGGL((ncf_pairs_kernel<E, PHASE>), dim3(blocks), dim3(kNcfThreads), lds, s, *a);
+        hipLaunchKernelGGL((ncf_pairs_kernel<E, PHASE>), dim3(blocks), dim3(ncf_threads<E>()), lds, s, *a);
         return check_launch("rg_ncf_pairs");
     }
     int operator()(int E) {
