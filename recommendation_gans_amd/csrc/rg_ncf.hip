@@ -241,9 +241,12 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
     // slots claimed and its A_0 rows gathered into registers during this tile's backward,
     // so a tile starts with its inputs in hand (the id and gather phases were ~4 us of a
     // ~26 us tile).  The small towers keep their registers for occupancy.
-    constexpr bool kPipe = kWide && kBackward;
-    constexpr int kPG = kPipe ? kRows * (IN0 / 4) / kNT : 1;   // float4 per thread of A_0
-    static_assert(!kPipe || kRows * (IN0 / 4) % kNT == 0, "A_0 prefetch shape");
+    // With 8 waves (registers for two per SIMD) only the ids and slots run ahead (kPipe);
+    // the A_0 rows are gathered at the tile's start (kPipeRows off).
+    constexpr bool kPipe = E >= 64 && kBackward;
+    constexpr bool kPipeRows = kPipe && kWide;
+    constexpr int kPG = kPipeRows ? kRows * (IN0 / 4) / kNT : 1;   // float4 per thread of A_0
+    static_assert(!kPipeRows || kRows * (IN0 / 4) % kNT == 0, "A_0 prefetch shape");
     bool pre_ok = false;                  // registers hold this tile's ids, slots and A_0
     int nu = -1, ni = -1, nps = -1, nlu = -1, nli = -1, ncol = 0;
     float4 pg[kPG];
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
         __syncthreads();
         NS(1);
         // ---- gather A_0 = [U[u] | I[i]] ------------------------------------------------
-        if (kPipe && pre_ok) {
+        if (kPipeRows && pre_ok) {
 #pragma unroll
             for (int j = 0; j < kPG; ++j) {
                 const int e = tid + j * kNT, r = e / (IN0 / 4), c4 = (e % (IN0 / 4)) * 4;
@@ -415,6 +418,7 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
                 for (int c = 0; c < M; ++c) d = fmaf(gu[c] * gu[M + c], sWm[c], d);   // GMF = U_mf * I_mf
                 const float p = sigmoidf_ref(d + wo[8]);
                 sP[tid] = p;
+                sDz[tid] = 0.0f;   // rows no column writes below keep dz = 0
                 if (PHASE == kNcfScores) a.scores[tile * kRows + tid] = sU[tid] >= 0 ? p : 0.0f;
             }
         }
@@ -422,8 +426,6 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
         NS(4);
         if (PHASE == kNcfScores) continue;
         // dL/dlogit per row (columns: one thread each) and the tile's loss partials
-        if (tid < kRows) sDz[tid] = 0.0f;
-        __syncthreads();
         if (tid < tc) {
             float la = 0.0f, lb = 0.0f;
             {
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
             a.loss_partials[2 * tile] = la;
             a.loss_partials[2 * tile + 1] = lb;
         }
-        __syncthreads();
+        // (no barrier: thread 0 only reads sLa / sLb, rewritten at the next tile's loss phase)
         NS(5);
         if (PHASE == kNcfLossOnly) continue;         // validation: loss only (run_val_iteration)
         // ---- backward ------------------------------------------------------------------------
@@ -524,9 +526,22 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
                 auto term = [&](int r) {
                     return e < 8 ? AN[r * 9 + e] : e == 8 ? 1.0f : sGm[r * gs + e - 9] * sGm[r * gs + M + e - 9];
                 };
-                if constexpr (kWide) {
+                // in row order; E = 64 reads the operands in batches of kCh (one LDS round
+                // trip per batch; all rows at once with 4 waves), the small towers one by one
+                // (their registers buy occupancy)
+                if constexpr (E >= 64) {
+                    constexpr int kCh = kWide ? kRows : 8;
+#pragma unroll 1
+                    for (int r0 = 0; r0 < kRows; r0 += kCh) {
+                        float dz[kCh], tv[kCh];
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], term(r), acc);
+                        for (int r = 0; r < kCh; ++r) {
+                            dz[r] = sDz[r0 + r];
+                            tv[r] = term(r0 + r);
+                        }
+#pragma unroll
+                        for (int r = 0; r < kCh; ++r) acc = fmaf(dz[r], tv[r], acc);
+                    }
                 } else {
                     for (int r = 0; r < kRows; ++r) acc = fmaf(sDz[r], term(r), acc);
                 }
@@ -562,7 +577,7 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
             }
             __syncthreads();
         }
-        if constexpr (kPipe) {
+        if constexpr (kPipeRows) {
             if (has_next) {
 #pragma unroll
                 for (int j = 0; j < kPG; ++j) {
@@ -573,6 +588,8 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
                                             : *reinterpret_cast<const float4 *>(a.item_w + (int64_t)i2 * E + (c4 - E));
                 }
             }
+        }
+        if constexpr (kPipe) {
             pre_ok = has_next;
         }
         static_for<NH>([&](auto kc) {
@@ -596,12 +613,16 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
             }
             for (int o = tid; o < out; o += kNT) {
                 float acc = 0.0f;
-                if constexpr (kWide) {   // one batch of LDS reads, then the same in-order sum
-                    float col[kRows];
+                if constexpr (E >= 64) {   // batches of LDS reads, then the same in-order sum
+                    constexpr int kCh = kWide ? kRows : 8;
+#pragma unroll 1
+                    for (int r0 = 0; r0 < kRows; r0 += kCh) {
+                        float col[kCh];
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) col[r] = Dk[r * (out + 1) + o];
+                        for (int r = 0; r < kCh; ++r) col[r] = Dk[(r0 + r) * (out + 1) + o];
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) acc += col[r];
+                        for (int r = 0; r < kCh; ++r) acc += col[r];
+                    }
                 } else {
                     for (int r = 0; r < kRows; ++r) acc += Dk[r * (out + 1) + o];
                 }
