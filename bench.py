@@ -104,8 +104,9 @@ def parse():
                     help="run the DP code path at N = 1 too (identity exchange; bench-path check)")
     ap.add_argument("--comm-at-1", action="store_true",
                     help="with --dp-at-1 --dp owner: the native step with a one-rank RCCL communicator")
-    ap.add_argument("--events-every", type=int, default=8,
-                    help="record the dominant kernel's timing events on every k-th timed step")
+    ap.add_argument("--events-every", type=int, default=10,
+                    help="record the dominant kernel's timing events on every k-th timed step (each event "
+                         "pair leaves a ~6 us bubble on the stream: 2 pairs in the driver's 20 steps)")
     return ap.parse_args()
 
 
