@@ -173,6 +173,17 @@ int rg_mt_window_to_cpython(const uint32_t *window_host, int32_t pos, uint32_t *
  * in place, as k calls of getrandbits(32) would. */
 int rg_mt_advance_host(uint32_t *state_host, int64_t k);
 
+/* NumPy legacy RandomState.randint(low, high, n_out) (int64) from raw MT19937 words
+ * (rg_mt_generate started at the RandomState's (key, pos) state): NumPy's masked rejection
+ * (distributions.c random_bounded_uint64_fill) as an ordered compaction.  Replaces the host
+ * draw of spotlight/sampling.py:9-35 sample_items (random_state.randint(0, num_items, shape)).
+ * Needs 2 <= high - low <= 2^32.  *consumed_dev = words the draw used (advance the state by
+ * it), or 0 when n_words held fewer than n_out accepted words (generate more and retry).
+ * scratch: rg_uniform_scratch_len(n_words) int32 elements, 8-byte aligned. */
+int64_t rg_uniform_scratch_len(int64_t n_words);
+int rg_uniform_int64(void *stream, const uint32_t *words_dev, int64_t n_words, int64_t low, int64_t high,
+                     int64_t n_out, int64_t *out_dev, int32_t *scratch_dev, int64_t *consumed_dev);
+
 /* int32 elements of a prepared-pairs buffer: one record of S int2 per column (S = 8
  * for n_neg <= 6, else 16): [q] = (user, item) of pair q (0 = the positive, 1 + k =
  * negative k), [n_neg + 1] = (the positive's plan slot or -1, 0), zero padding. */

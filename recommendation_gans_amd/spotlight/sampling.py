@@ -48,11 +48,67 @@ class NegativePool:
         return NegativePool(a[:, 0], a[:, 1])
 
 
-def sample_items(interaction, user_ids, num_items, shape, random_state=None):
-    """Uniform item ids (sampling.py:9-35)."""
+RG_MT_PAD = 1280   # include/rg_hip.h: words rg_mt_generate may write past the requested count
+
+
+def sample_items(interaction, user_ids, num_items, shape, random_state=None, device=None):
+    """Uniform item ids (sampling.py:9-35): ``random_state.randint(0, num_items, shape)``.
+
+    ``device`` (additive): draw on that GPU instead (``sample_items_device``) and return an
+    int64 tensor there; the values and the generator state afterwards are NumPy's."""
     if random_state is None:
         random_state = np.random.RandomState()
+    if device is not None:
+        return sample_items_device(num_items, shape, random_state, device)
     return random_state.randint(0, num_items, shape, dtype=np.int64)
+
+
+def sample_items_device(num_items, shape, random_state=None, device="cuda"):
+    """NumPy legacy ``RandomState.randint(0, num_items, shape)`` on the GPU, bit-exact, with
+    ``random_state`` advanced exactly as NumPy advances it: the MT19937 words are generated
+    from the RandomState's (key, pos) state (rg_mt_generate) and NumPy's masked rejection
+    runs as an ordered compaction (rg_uniform_int64); the words the draw consumed advance
+    the host state (rg_mt_advance_host).  Returns an int64 tensor of ``shape`` on
+    ``device``."""
+    import torch
+    from .. import _lib
+    if random_state is None:
+        random_state = np.random.RandomState()
+    num_items = int(num_items)
+    if num_items <= 0:
+        raise ValueError("high <= 0")
+    if num_items - 1 > 0xFFFFFFFF:
+        raise ValueError("sample_items_device: num_items above 2^32 is not supported")
+    shape = (shape,) if np.isscalar(shape) else tuple(shape)
+    n = int(np.prod(shape, dtype=np.int64))
+    out = torch.zeros(n, dtype=torch.int64, device=device)
+    if n == 0 or num_items == 1:   # NumPy draws no words for a one-value range
+        return out.reshape(shape)
+    lib = _lib.load()
+    name, key, pos, has_gauss, gauss = random_state.get_state()
+    state = np.empty(625, np.uint32)
+    state[:624] = key
+    state[624] = pos
+    rng = num_items - 1
+    mask = (1 << int(rng).bit_length()) - 1
+    nwords = int(n * (mask + 1) / (rng + 1) * 1.05) + 4096   # expected words + margin
+    stream = _lib.stream_handle(torch.cuda.current_stream(device))
+    consumed = torch.zeros(1, dtype=torch.int64, device=device)
+    while True:
+        st = torch.from_numpy(state.view(np.int32).copy()).to(device)
+        words = torch.empty(nwords + RG_MT_PAD, dtype=torch.int32, device=device)
+        _lib.check(lib.rg_mt_generate(stream, _lib.ptr(st), _lib.ptr(words), nwords, None), "rg_mt_generate")
+        scratch = torch.empty(int(lib.rg_uniform_scratch_len(nwords)) + 2, dtype=torch.int32, device=device)
+        _lib.check(lib.rg_uniform_int64(stream, _lib.ptr(words), nwords, 0, num_items, n, _lib.ptr(out),
+                                        _lib.ptr(scratch), _lib.ptr(consumed)), "rg_uniform_int64")
+        c = int(consumed.item())
+        if c > 0:
+            break
+        nwords *= 2   # fewer accepted words than outputs (far tail): redraw from the same state
+    host = state.copy()
+    _lib.check(lib.rg_mt_advance_host(host.ctypes.data, c), "rg_mt_advance_host")
+    random_state.set_state((name, host[:624].copy(), int(host[624]), has_gauss, gauss))
+    return out.reshape(shape)
 
 
 def get_negative_samples(train, num_samples):
