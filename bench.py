@@ -296,6 +296,28 @@ def bench_ncf(args):
         dist.destroy_process_group()
 
 
+def stream_copy_gbs(dev, mib=1024, reps=10):
+    """Achievable HBM bandwidth of this box: a grid-stride float4 copy of `mib` MiB
+    (rg_stream_copy, read + write bytes counted) timed with events, best of `reps`."""
+    from recommendation_gans_amd import _lib
+    lib = _lib.load()
+    n4 = mib * (1 << 20) // 16
+    src = torch.ones(n4 * 4, device=dev)
+    dst = torch.empty_like(src)
+    st = _lib.stream_handle()
+    _lib.check(lib.rg_stream_copy(st, _lib.ptr(dst), _lib.ptr(src), n4), "rg_stream_copy")
+    best = float("inf")
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        lib.rg_stream_copy(st, _lib.ptr(dst), _lib.ptr(src), n4)
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) * 1e-3)
+    del src, dst
+    return 2 * n4 * 16 / best / 1e9
+
+
 def gan_flops(N, S, H, E, Z, B):
     """Algorithmic FLOPs of one discriminator and one generator iteration:
     2 * multiply-adds of every dense contraction, the real slates' one-hot layer counted
@@ -705,6 +727,12 @@ def main():
                 else:
                     out["roofline"]["traffic_source"] = (f"profiles/{os.path.basename(pmc)} is of another build "
                                                          f"(lib {p.get('lib_sha16')} vs {sha}): not used")
+        if out.get("roofline"):
+            # the box's achievable HBM rate (STREAM-style copy, after the timed region), reported
+            # beside the 8 TB/s nominal peak
+            bw = stream_copy_gbs(dev)
+            out["roofline"]["stream_copy_GBs"] = bw
+            out["roofline"]["frac_of_stream_copy"] = out["roofline"]["achieved"] / bw
         out["final_loss"] = loss_last
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, d, B, n, args.loss, args.cpu_baseline_seconds)

@@ -181,6 +181,8 @@ int rg_mt_advance_host(uint32_t *state_host, int64_t k);
  * it), or 0 when n_words held fewer than n_out accepted words (generate more and retry).
  * scratch: rg_uniform_scratch_len(n_words) int32 elements, 8-byte aligned. */
 int64_t rg_uniform_scratch_len(int64_t n_words);
+/* Measurement only (bench.py's STREAM-copy ceiling): dst[i] = src[i] for n_float4 float4s. */
+int rg_stream_copy(void *stream, float *dst_dev, const float *src_dev, int64_t n_float4);
 int rg_uniform_int64(void *stream, const uint32_t *words_dev, int64_t n_words, int64_t low, int64_t high,
                      int64_t n_out, int64_t *out_dev, int32_t *scratch_dev, int64_t *consumed_dev);
 

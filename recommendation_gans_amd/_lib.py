@@ -211,6 +211,7 @@ SIGNATURES = [
     ("rg_mt_window_to_cpython", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_advance_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("rg_uniform_scratch_len", ctypes.c_int64, [ctypes.c_int64]),
+    ("rg_stream_copy", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     ("rg_uniform_int64", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
