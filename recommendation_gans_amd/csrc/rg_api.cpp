@@ -8,6 +8,9 @@
 namespace rg {
 
 static thread_local std::string g_last_error;
+static thread_local LaunchEvents g_launch_events;
+
+LaunchEvents &launch_events() { return g_launch_events; }
 
 void set_error(const std::string &msg) { g_last_error = msg; }
 

@@ -13,6 +13,14 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------- errors
 void set_error(const std::string &msg);
 int fail_arg(const std::string &msg);
+// Timing events for the next instrumented launch on this thread (the dense pass of the
+// split step): recorded by the kernel dispatch itself (hipExtLaunchKernel), so they time
+// the kernel alone and add no marker packets (and no bubbles) to the stream.  Consumed
+// (reset) by the launch that uses them.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents &launch_events();
 int check_launch(const char *what);
 // rg_comm.cpp: all-reduce of buf on the communicator stream, fenced against `stream`
 int comm_begin(void *comm, hipStream_t stream, float *buf, int64_t n);

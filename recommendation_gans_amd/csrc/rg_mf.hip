@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "rg_common.h"
 #include "rg_mt.h"
 #include "rg_owner.h"
@@ -1442,24 +1444,22 @@ struct BackLaunchF {
         // RG_APPLY_SPEC=0 turns it off)
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
         const OwnerArgs oa = own ? *own : OwnerArgs{};
-        if (own)
-            hipLaunchKernelGGL((mf_back_kernel<L, 0, true, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen,
-                               bg, oa);
-        else if (spec && nt == 1)
-            hipLaunchKernelGGL((mf_back_kernel<L, 1, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
-                               oa);
-        else if (spec && nt == 3)
-            hipLaunchKernelGGL((mf_back_kernel<L, 3, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
-                               oa);
-        else if (spec)
-            hipLaunchKernelGGL((mf_back_kernel<L, 0, true>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg,
-                               oa);
-        else if (nt == 1)
-            hipLaunchKernelGGL((mf_back_kernel<L, 1>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
-        else if (nt >= 2)
-            hipLaunchKernelGGL((mf_back_kernel<L, 2>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
-        else
-            hipLaunchKernelGGL((mf_back_kernel<L, 0>), grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
+        LaunchEvents &le = launch_events();
+        const hipEvent_t e0 = le.start, e1 = le.stop;
+        le = LaunchEvents{};
+        auto go = [&](auto kernel) {
+            if (e0 || e1)
+                hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, e0, e1, 0, *a, *prep, prep_out, nb, gen, bg, oa);
+            else
+                hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
+        };
+        if (own) go(mf_back_kernel<L, 0, true, true>);
+        else if (spec && nt == 1) go(mf_back_kernel<L, 1, true>);
+        else if (spec && nt == 3) go(mf_back_kernel<L, 3, true>);
+        else if (spec) go(mf_back_kernel<L, 0, true>);
+        else if (nt == 1) go(mf_back_kernel<L, 1>);
+        else if (nt >= 2) go(mf_back_kernel<L, 2>);
+        else go(mf_back_kernel<L, 0>);
         return check_launch("rg_mf_apply_prepare");
     }
 };

@@ -425,12 +425,12 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
                                                 tb->num_items * (int64_t)(tb->dim + 1) + 1)))
             return rc;
     }
-    if ((rc = record(ev0, s))) return rc;
-    if ((rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
-                                      next ? &nbatch : nullptr, next ? &nw : nullptr, gen_slot >= 0 ? &gen : nullptr)))
-        return rc;
+    rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // timed by the dispatch itself
+    rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
+                                 next ? &nbatch : nullptr, next ? &nw : nullptr, gen_slot >= 0 ? &gen : nullptr);
+    rg::launch_events() = rg::LaunchEvents{};
+    if (rc) return rc;
     if (gen_slot >= 0) end_production(st, s, gen_slot);
-    if ((rc = record(ev1, s))) return rc;
     if (st.cfg.item_grad) {
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
         if ((rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out))) return rc;
