@@ -280,6 +280,24 @@ __global__ __launch_bounds__(256) void d_real_l1_kernel(const float *__restrict_
 }
 
 // split-K reduction + bias (+ history-embedding columns of W1) -> Dropout -> LeakyReLU
+// sum over split-K partials in split order (part[z * stride + e], z = 0..splits-1), the
+// loads issued kSplitBatch at a time ahead of the in-order adds: the same sums as the
+// plain loop, with kSplitBatch loads in flight per thread instead of the compiler's few
+constexpr int kSplitBatch = 16;
+__device__ __forceinline__ float sum_splits(const float *__restrict__ part, int splits, int64_t stride, int64_t e) {
+    float v = 0.0f;
+    int z = 0;
+    for (; z + kSplitBatch <= splits; z += kSplitBatch) {
+        float x[kSplitBatch];
+#pragma unroll
+        for (int u = 0; u < kSplitBatch; ++u) x[u] = part[(int64_t)(z + u) * stride + e];
+#pragma unroll
+        for (int u = 0; u < kSplitBatch; ++u) v += x[u];
+    }
+    for (; z < splits; ++z) v += part[(int64_t)z * stride + e];
+    return v;
+}
+
 __global__ __launch_bounds__(256) void reduce_act_kernel(const float *__restrict__ part, int splits, int64_t zstride,
                                                          int rows, int C,
                                                          const float *__restrict__ bias,
@@ -291,8 +309,7 @@ __global__ __launch_bounds__(256) void reduce_act_kernel(const float *__restrict
     if (e >= total) return;
     const int64_t r = e / C;
     const int un = (int)(e % C);
-    float v = 0.0f;
-    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * zstride + e];
+    float v = sum_splits(part, splits, zstride, e);
     if (we)
         for (int k = 0; k < E; ++k) v = fmaf(we[(int64_t)un * E + k], c[r * E + k], v);
     v += bias[un];
@@ -310,8 +327,7 @@ __global__ __launch_bounds__(256) void reduce_lrelu_grad_kernel(const float *__r
                                                                 float *__restrict__ out) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= total) return;
-    float v = 0.0f;
-    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * total + e];
+    float v = sum_splits(part, splits, total, e);
     v = v * (U[e] > 0.0f ? 1.0f : kSlope);
     if (Mult) v = v * Mult[e];
     out[e] = v;
@@ -389,8 +405,7 @@ __global__ __launch_bounds__(256) void reduce_post_kernel(const float *__restric
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= M * N) return;
     const int64_t m = e / N, n = e % N;
-    float v = 0.0f;
-    for (int z = 0; z < splits; ++z) v += part[(int64_t)z * M * N + e];
+    float v = sum_splits(part, splits, M * N, e);
     if (bias) v += bias[n];
     if (post == kPostTanh) {
         v = tanhf(v);
