@@ -168,12 +168,25 @@ __global__ __launch_bounds__(256) void hist_sum_kernel(const float *__restrict__
         float acc[kEChunk];
 #pragma unroll
         for (int e = 0; e < kEChunk; ++e) acc[e] = 0.0f;
-        for (int l = t; l < L; l += 256) {
-            const int it = hist[(int64_t)row * L + l];
-            if (it == pad) continue;
+        // the thread's positions t, t + 256, ... in order; ids and rows of kB positions in flight
+        constexpr int kB = 4;
+        for (int l0 = t; l0 < L; l0 += 256 * kB) {
+            int it[kB];
 #pragma unroll
-            for (int e = 0; e < kEChunk; ++e)
-                if (e0 + e < E) acc[e] += emb[(int64_t)it * E + e0 + e];
+            for (int u = 0; u < kB; ++u) it[u] = l0 + 256 * u < L ? hist[(int64_t)row * L + l0 + 256 * u] : pad;
+            float x[kB][kEChunk];
+#pragma unroll
+            for (int u = 0; u < kB; ++u)
+#pragma unroll
+                for (int e = 0; e < kEChunk; ++e)
+                    x[u][e] = (it[u] != pad && e0 + e < E) ? emb[(int64_t)it[u] * E + e0 + e] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                if (it[u] == pad) continue;
+#pragma unroll
+                for (int e = 0; e < kEChunk; ++e)
+                    if (e0 + e < E) acc[e] += x[u][e];
+            }
         }
 #pragma unroll
         for (int e = 0; e < kEChunk; ++e) {
@@ -426,10 +439,19 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float *__restrict__ 
     const int64_t c = (int64_t)blockIdx.x * 64 + lane;
     float s = 0.0f;
     if (c < C) {
-#pragma unroll 4
-        for (int64_t r = wave; r < rows; r += 16) {
-            const float x = X ? X[r * ld + c] : 1.0f;
-            s = w ? fmaf(w[r], x, s) : s + x;
+        // the wave's rows wave, wave + 16, ... in order; their loads issued kB at a time
+        constexpr int kB = 8;
+        for (int64_t r0 = wave; r0 < rows; r0 += 16 * kB) {
+            float x[kB], wr[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int64_t r = r0 + 16 * u;
+                x[u] = (X && r < rows) ? X[r * ld + c] : 1.0f;
+                wr[u] = (w && r < rows) ? w[r] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u)
+                if (r0 + 16 * u < rows) s = w ? fmaf(wr[u], x[u], s) : s + x[u];
         }
     }
     red[wave][lane] = s;
@@ -453,14 +475,28 @@ __global__ __launch_bounds__(1024) void d_l1_w1e_grad_kernel(const float *__rest
         float acc[kEChunk];
 #pragma unroll
         for (int e = 0; e < kEChunk; ++e) acc[e] = 0.0f;
-        if (un < H2)
-            for (int r = wave; r < 2 * B; r += 16) {
-                const float g = dl1[(int64_t)r * H2 + un];
-                const float *cr = c + (int64_t)(r % B) * E + e0;
+        if (un < H2) {
+            constexpr int kB = 4;   // rows whose loads are issued together (same fma order)
+            for (int r0 = wave; r0 < 2 * B; r0 += 16 * kB) {
+                float g[kB], cv[kB][kEChunk];
 #pragma unroll
-                for (int e = 0; e < kEChunk; ++e)
-                    if (e0 + e < E) acc[e] = fmaf(g, cr[e], acc[e]);
+                for (int u = 0; u < kB; ++u) {
+                    const int r = r0 + 16 * u;
+                    const bool ok = r < 2 * B;
+                    g[u] = ok ? dl1[(int64_t)r * H2 + un] : 0.0f;
+                    const float *cr = c + (int64_t)((ok ? r : 0) % B) * E + e0;
+#pragma unroll
+                    for (int e = 0; e < kEChunk; ++e) cv[u][e] = (e0 + e < E) ? cr[e] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < kB; ++u) {
+                    if (r0 + 16 * u >= 2 * B) continue;
+#pragma unroll
+                    for (int e = 0; e < kEChunk; ++e)
+                        if (e0 + e < E) acc[e] = fmaf(g[u], cv[u][e], acc[e]);
+                }
             }
+        }
 #pragma unroll
         for (int e = 0; e < kEChunk; ++e) {
             if (e0 + e >= E) break;
