@@ -170,7 +170,7 @@ __device__ __forceinline__ T pick(const T (&x)[N], int q) {
     return r;
 }
 
-constexpr int kLdsFloats = 1280 * (kPairBlock / 256);   // >= units per block * (dim + 1) for every layout
+constexpr int kLdsFloats = 5 * kPairBlock;   // >= units per block * (dim + 1) for every layout (1280 at 256 threads)
 
 // One unit = one batch column: pair q = 0 is the positive, q = 1..n the
 // negatives k*global_cols + col.  Every gather uses an always-valid index and is
