@@ -133,7 +133,10 @@ def test_gan_steps_match_reference(golden_dir, case):
         dval = eng.last_d_out(2 * B).cpu().numpy()
         np.testing.assert_allclose(dval[:B], z[f"d{k}_d_real"].ravel(), rtol=1e-5, err_msg=f"{case} D{k} real")
         np.testing.assert_allclose(dval[B:], z[f"d{k}_d_fake"].ravel(), rtol=1e-5, err_msg=f"{case} D{k} fake")
-        np.testing.assert_allclose(eng.last_fake(B).cpu().numpy(), z[f"d{k}_fake"], rtol=1e-4, atol=1e-5)
+        # G(z): every element within 1e-5 of the tensor's scale (max |reference|), the bar
+        # the C4 config test holds against the float64 oracle
+        fk, fref = eng.last_fake(B).cpu().numpy(), z[f"d{k}_fake"]
+        assert np.abs(fk - fref).max() <= 1e-5 * np.abs(fref).max(), f"{case} D{k} fake"
         assert abs(out[0] - z[f"d{k}_loss"][0]) <= 1e-5 * abs(z[f"d{k}_d_real"]).mean()
         dsd = eng.d_state_dict()
         for n in dn:
