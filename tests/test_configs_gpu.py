@@ -11,7 +11,9 @@
   (1e-5 relative per table);
 * C4 (cGAN, N = 20,108, S = 5, H = 256, E = 5, B = 256, histories of the synthetic
   ML-20M users): one discriminator iteration and one generator iteration with
-  recorded z and dropout masks against the float64 oracle (oracle/gan.py).
+  recorded z and dropout masks against the float64 oracle (oracle/gan.py);
+* C3 (NCF, ML-20M-shaped, mlp_embedding_dim 64, B = 8192): two native steps with
+  item plans and recorded dropout masks against oracle/ncf.py in fp32 and fp64.
 
 The CPU oracle runs at these sizes in a few seconds per step on the box's host cores."""
 import numpy as np
@@ -190,3 +192,46 @@ def test_gan_full_size_iterations(ml20m):
     for k in o.g_params:
         ok, msg = param_ok(gsd[k].numpy(), o.G[k], o.last_grads[k], lr, exempt=k in o.pre_bn_biases())
         assert ok, f"G {k}: {msg}"
+
+
+def test_ncf_full_size_steps(ml20m):
+    """C3 (ncf_spotlight.py at ML-20M shape: mlp_embedding_dim 64, tower [128, 64, 32, 16, 8],
+    B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5): two native steps with item plans and
+    recorded dropout masks against the oracle (oracle/ncf.py) run in fp32 and fp64 from the
+    same MLP(...) init: MT state bit-exact, loss 1e-5 relative, every parameter by tensor
+    parity (oracle.mf.tensor_parity, as the golden-size NCF test)."""
+    from oracle import ncf as oncf
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    data = ml20m
+    dev = torch.device("cuda:0")
+    U, I, E, B, n = data.num_users, data.num_items, 64, 8192, 5
+    torch.manual_seed(0)                                   # ncf_spotlight.py: MLP(...) init
+    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    names = [k for k, _ in net.named_parameters()]
+    params = [p.detach().clone() for p in net.parameters()]
+    mt = orng.py_seed_state(0)
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                  device=dev, **kw)
+    o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
+    rs = np.random.RandomState(5)
+    for s in range(2):
+        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
+        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
+        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
+        pi_d = torch.from_numpy(pi).to(dev)
+        got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
+        l32 = o32.step(pu, pi, mp, mn)
+        o64.step(pu, pi, mp, mn)
+        torch.cuda.synchronize()
+        assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
+        assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
+        for nm, p, r32, r64 in zip(names, e.params(), o32.P.t, o64.P.t):
+            ok, msg = omf.tensor_parity(p.reshape(r32.shape), r32, r64)
+            assert ok, f"step {s} {nm}: {msg}"
