@@ -13,7 +13,8 @@
   ML-20M users): one discriminator iteration and one generator iteration with
   recorded z and dropout masks against the float64 oracle (oracle/gan.py);
 * C3 (NCF, ML-20M-shaped, mlp_embedding_dim 64, B = 8192): two native steps with
-  item plans and recorded dropout masks against oracle/ncf.py in fp32 and fp64.
+  item plans and recorded dropout masks against oracle/ncf.py in fp32 and fp64;
+  NeuMF (neuMF_spotlight.py defaults, mlp 16 / mf 50) the same way.
 
 The CPU oracle runs at these sizes in a few seconds per step on the box's host cores."""
 import numpy as np
@@ -234,4 +235,48 @@ def test_ncf_full_size_steps(ml20m):
         assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
         for nm, p, r32, r64 in zip(names, e.params(), o32.P.t, o64.P.t):
             ok, msg = omf.tensor_parity(p.reshape(r32.shape), r32, r64)
+            assert ok, f"step {s} {nm}: {msg}"
+
+
+def test_neumf_full_size_steps(ml20m):
+    """neuMF_spotlight.py's defaults at ML-20M shape (mlp_embedding_dim 16, mf_embedding_dim 50,
+    B = 8192, n = 5, pointwise, Adam lr 1e-3): two native steps with item plans and recorded
+    dropout masks against oracle/ncf.py's NeuMFOracle in fp32 and fp64 from the same NeuMF(...)
+    init: MT state bit-exact, loss 1e-5 relative, every parameter (GMF tables included) by
+    tensor parity."""
+    from oracle import ncf as oncf
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
+    data = ml20m
+    dev = torch.device("cuda:0")
+    U, I, E, M, B, n = data.num_users, data.num_items, 16, 50, 8192, 5
+    torch.manual_seed(0)
+    net = NeuMF(mlp_layers(E), U, I, mf_embedding_dim=M, mlp_embedding_dim=E)
+    names = [k for k, _ in net.named_parameters()]
+    params = [p.detach().clone() for p in net.parameters()]
+    mt = orng.py_seed_state(0)
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    e = NCFEngine(params[0], params[1], params[4:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                  device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
+    o32 = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o64 = oncf.NeuMFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    widths = oncf.layer_sizes(E)[1:]
+    rs = np.random.RandomState(6)
+    for s in range(2):
+        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
+        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
+        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
+        prev = [t.detach().cpu().clone() for t in e.params()]
+        pi_d = torch.from_numpy(pi).to(dev)
+        got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
+        l32 = o32.step(pu, pi, mp, mn)
+        o64.step(pu, pi, mp, mn)
+        torch.cuda.synchronize()
+        assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
+        assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
+        for nm, p, r32, r64, b in zip(names, e.params(), o32.P.t, o64.P.t, prev):
+            ok, msg = omf.tensor_parity(p.reshape(r32.shape), r32, r64, before=b.reshape(r32.shape))
             assert ok, f"step {s} {nm}: {msg}"
