@@ -3,7 +3,8 @@
 * C2 / C5 (MF-BPR, ML-20M-shaped: U = 136,677, I = 20,108, 8.1 M train positives,
   8.1 M pool pairs, B = 8192, n = 5, Adam): three native steps (item plans, the
   next step's prepare fused into the dense pass, the inline MT walk) at d = 64 and
-  d = 128 against the single-process oracle (oracle/mf.py, fp32 and fp64): negative
+  d = 128 (and at d = 64 with the pointwise, hinge and adaptive-hinge losses too)
+  against the single-process oracle (oracle/mf.py, fp32 and fp64): negative
   ids and MT state bit-exact, loss 1e-5 relative, tables by tensor parity;
 * C5's data-parallel shard: rank 3 of 8 in the replicated layout at d = 128 -- its
   column slice of the global draw of 5 * 65,536 indices (jump-ahead walk) and its
@@ -46,14 +47,15 @@ def _rel(got, ref):
     return float((got - ref).norm() / max(float(ref.norm()), 1e-30))
 
 
-@pytest.mark.parametrize("d", [64, 128])
-def test_mf_full_size_steps(ml20m, d):
+@pytest.mark.parametrize("d,loss", [(64, "bpr"), (128, "bpr"), (64, "pointwise"), (64, "hinge"),
+                                    (64, "adaptive_hinge")])
+def test_mf_full_size_steps(ml20m, d, loss):
     from recommendation_gans_amd.mf_engine import MFEngine
     dev = torch.device("cuda:0")
     U, I, B, n = ml20m.num_users, ml20m.num_items, 8192, 5
     tabs = _tables(U, I, d)
     st = orng.py_seed_state(0)
-    kw = dict(loss="bpr", optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    kw = dict(loss=loss, optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
     o = omf.MFOracle(*[t.clone() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **kw)
     o64 = omf.MFOracle(*[t.clone().double() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **kw)
     e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), ml20m.pool_u, ml20m.pool_i, st.copy(),
