@@ -15,13 +15,22 @@ overlapped two-launch step (rg_mf_step_front + rg_mf_step_hot, measured slower).
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
 With N > 1 ranks (one process per GPU) the default is the reference-exact
-replicated step: global batch N*B, rank r takes columns [r*B, (r+1)*B)
-of it and of ONE global negative draw over the full pool, the rank-major gradient
-is reduce-scattered with RCCL, each rank updates its row shard (p, m, v), the tables
-are all-gathered -- N ranks compute exactly the reference's step at batch N*B.
---dp user_shard selects the faster user-sharded opt-in (sharding.py: rank r owns
-users u % N == r, its own positives, sub-pool and MT stream; item gradient
-all-reduce), which is NOT the reference's sampling at N > 1.
+owner-sharded step: rank r keeps the users u % N == r and every
+item, every rank walks ONE global negative draw of n*N*B indices over the full pool and
+keeps the pairs whose user it owns; the pair scores (not for pointwise) and the item
+gradient are all-reduced with RCCL -- N ranks compute exactly the reference's step at
+batch N*B.  --dp global_stream selects the replicated reference-exact step (rank-major
+gradient reduce-scatter + table all-gather); --dp user_shard the user-sharded opt-in
+(sharding.py: own sub-pool and MT stream per rank, item-gradient all-reduce), which is
+NOT the reference's sampling at N > 1.
+
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the
+N rank processes itself (a torch.distributed.run child started before this process
+touches the GPU) and exits with its status; it never falls back to one rank.
+`--launch-check` runs only that plumbing (gloo, no GPU): rendezvous, barrier, max-over-
+ranks timing, one JSON line from rank 0.  `--emulate-rank R/W` times rank R's owner step
+at W-rank geometry on ONE GPU (global batch W*B, the global draw, U/W users, every item)
+with the collectives replaced by same-size local copies (comm.LocalComm).
 
 Rank 0 prints ONE JSON line.  `value` = positives processed by all ranks / the
 max over ranks of the timed wall time.  `roofline` is for the dominant kernel
@@ -34,6 +43,7 @@ import contextlib
 import json
 import os
 import random
+import subprocess
 import sys
 import time
 
@@ -104,6 +114,12 @@ def parse():
                     help="run the DP code path at N = 1 too (identity exchange; bench-path check)")
     ap.add_argument("--comm-at-1", action="store_true",
                     help="with --dp-at-1 --dp owner: the native step with a one-rank RCCL communicator")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only the multi-rank launch plumbing (gloo on the CPU, no GPU): every rank joins, "
+                         "times a barrier, rank 0 prints the JSON line with n_gpus = WORLD_SIZE")
+    ap.add_argument("--emulate-rank", default=None, metavar="R/W",
+                    help="one GPU runs rank R's owner step at W-rank geometry (global batch W*B, the global draw, "
+                         "U/W users, every item), collectives replaced by same-size local copies")
     ap.add_argument("--events-every", type=int, default=10,
                     help="record the dominant kernel's timing events on every k-th timed step (each event "
                          "pair leaves a ~6 us bubble on the stream: 2 pairs in the driver's 20 steps)")
@@ -507,8 +523,71 @@ def bench_eval(args):
     print(json.dumps(out), flush=True)
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without WORLD_SIZE: start the N rank processes as ONE child,
+    `torch.distributed.run` on this node over 127.0.0.1, before this process makes any
+    GPU call (so no exec and no GPU state in the parent), and exit with its status --
+    a failed launch is a failed bench, never a 1-rank run."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    rc = subprocess.call(cmd, env=env)
+    if rc != 0:
+        print(f"bench.py: the {args.gpus}-rank launch failed with status {rc}", file=sys.stderr)
+    sys.exit(rc if rc != 0 else 0)
+
+
+def launch_check(args):
+    """The multi-rank plumbing alone (gloo, CPU): rendezvous, barrier-bracketed timing of
+    a trivial all-reduce per step, max over ranks, one JSON line from rank 0."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.ones(1024)
+    for _ in range(args.warmup):
+        if world > 1:
+            dist.all_reduce(x)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.all_reduce(x)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "launch check (gloo all-reduce of 1024 floats)", "value": args.steps / el,
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "launch plumbing only", "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    if args.launch_check:
+        return launch_check(args)
+    if args.gpus > 1 and args.model in ("gan", "eval"):
+        raise SystemExit(f"--model {args.model} runs on one GPU (cGAN: replicas only, SURVEY §8e); "
+                         f"--gpus {args.gpus} refused")
     if args.model == "eval":
         return bench_eval(args)
     if args.model in ("ncf", "neumf"):
@@ -518,8 +597,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and "WORLD_SIZE" in os.environ:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    emu = None
+    if args.emulate_rank:
+        if world > 1:
+            raise SystemExit("--emulate-rank runs one process on one GPU")
+        r_, w_ = (int(x) for x in args.emulate_rank.split("/"))
+        if not (w_ > 1 and 0 <= r_ < w_):
+            raise SystemExit("--emulate-rank R/W needs W > 1 and 0 <= R < W")
+        emu = (r_, w_)
+        args.dp = "owner"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
@@ -550,6 +636,11 @@ def main():
         from recommendation_gans_amd.comm import RcclComm
         with stdout_to_stderr():          # RCCL's init banner
             comm = RcclComm(dev)
+    if emu is not None:
+        # one GPU, rank emu[0] of emu[1]: the owner step at that geometry with local-copy exchanges
+        from recommendation_gans_amd.comm import LocalComm
+        comm = LocalComm(dev, emu[1], emu[0])
+        rank, world = emu
     gs = args.dp == "global_stream" and (world > 1 or args.dp_at_1)
     own = args.dp == "owner" and (world > 1 or args.dp_at_1)
     solo_pg = False
@@ -641,7 +732,8 @@ def main():
         if ev is not None:
             ev[0].record()
             ev[1].record()
-    if world > 1:
+    multi = world > 1 and emu is None     # real ranks (an emulated rank is one process)
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -649,15 +741,17 @@ def main():
         step(args.warmup + s, evs[s])
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if multi:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss_last = float(eng.loss_out[0])
 
+    if emu is not None:
+        return report_emulated(args, emu, eng, evs, el, U, I, d, B, n)
     if rank == 0:
         value = args.steps * B * world / el
         # per rank: its user shard + every item go through the dense optimizer pass
@@ -741,6 +835,32 @@ def main():
         del eng
         comm.close()
         dist.destroy_process_group()
+
+
+def report_emulated(args, emu, eng, evs, el, U, I, d, B, n):
+    """--emulate-rank: one JSON line for rank R's step at W-rank geometry (NOT the driver's
+    metric line): its time per step, the user-update kernel's events, and what W ranks each
+    taking this step time would process (exchange time over xGMI NOT included: the
+    collectives were local copies)."""
+    from recommendation_gans_amd import _lib
+    r_, w_ = emu
+    ms_step = el / args.steps * 1e3
+    ev = [_lib.elapsed_ms(a, b) for a, b in (e for e in evs if e is not None)]
+    rows_user = eng.U
+    out = {"metric": f"emulated rank {r_} of {w_}: owner-sharded MF step time (local-copy exchanges)",
+           "value": args.steps * B * w_ / el, "unit": "interactions/s (projected: W ranks at this step time)",
+           "n_gpus": 1, "emulated_world": w_, "emulated_rank": r_, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": f"synthetic ML-20M-shaped: U={U} I={I}",
+           "config": {"workload": f"MF-{args.loss.upper()} d={d}, batch {B}/rank, global batch {B * w_}, {n} "
+                                  f"negatives, {args.optim}; this rank: {rows_user} user rows + {I} item rows",
+                      "global_batch": B * w_, "embedding_dim": d, "parallelism": f"emulated dp{w_} owner"},
+           "exchange_floats_per_step": {"scores": (1 + n) * B * w_ if args.loss != "pointwise" else 0,
+                                        "item_grad": I * (d + 1) + 1},
+           "user_update_us": float(np.mean(ev)) * 1e3 if ev else None,
+           "final_loss": float(eng.loss_out[0])}
+    print(json.dumps(out), flush=True)
+    eng.comm.close()
 
 
 if __name__ == "__main__":

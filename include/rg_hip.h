@@ -401,6 +401,10 @@ int rg_mf_scores(void *stream, const float *user_w, const float *item_w,
 #define RG_COMM_ID_BYTES 128
 int rg_comm_unique_id(uint8_t *out, int64_t len);
 void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, int32_t device);
+/* One-GPU stand-in for rank `rank` of a `world`-rank communicator (bench.py
+ * --emulate-rank): every collective is a same-size local copy out and back on the
+ * communicator stream (data unchanged), placed and fenced like the RCCL path. */
+void *rg_comm_create_local(int32_t world, int32_t rank, int32_t device);
 int rg_comm_destroy(void *comm);
 /* In-place sum over ranks, stream-ordered with respect to `stream` (runs on the
  * communicator's own stream between two events). */

@@ -217,6 +217,7 @@ SIGNATURES = [
                                         ctypes.c_void_p]),
     ("rg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("rg_comm_create", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rg_comm_create_local", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("rg_comm_allreduce_sum_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     ("rg_mt_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,

@@ -64,3 +64,20 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+class LocalComm(RcclComm):
+    """One-GPU stand-in for rank ``rank`` of ``world`` (bench.py --emulate-rank): the native
+    step's collectives become same-size local copies on the communicator stream
+    (rg_comm_create_local), so one rank's step at the multi-rank geometry can be timed and
+    profiled on a single GPU.  The data is left unchanged (an identity exchange)."""
+
+    def __init__(self, device, world, rank):
+        self.lib = _lib.load()
+        self.rank, self.world = int(rank), int(world)
+        self.device = torch.device(device)
+        index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.handle = self.lib.rg_comm_create_local(self.world, self.rank, index)
+        if not self.handle:
+            raise RuntimeError("rg_comm_create_local: " + self.lib.rg_last_error().decode())
+

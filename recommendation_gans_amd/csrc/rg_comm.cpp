@@ -6,6 +6,12 @@
 // communicator (rg_comm_create).  The collective runs on the communicator's own
 // stream, fenced by events against the caller's compute stream, so compute
 // enqueued between rg_comm_allreduce_begin and rg_comm_allreduce_end overlaps it.
+//
+// rg_comm_create_local: a one-GPU stand-in for rank `rank` of a `world`-rank
+// communicator (bench.py --emulate-rank): every collective becomes same-size local
+// copies on the communicator stream (an all-reduce: buf -> scratch -> buf, so the data
+// is left as it was), with the same events and stream placement as the RCCL path.  It
+// measures one rank's compute at the multi-rank geometry on a box with one GPU.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -22,7 +28,34 @@ struct Comm {
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     int world = 0, rank = 0;
+    bool local = false;           // rg_comm_create_local: collectives are local copies
+    float *scratch = nullptr;     // local: copy target
+    size_t scratch_floats = 0;
 };
+
+// local stand-in: n floats out to the scratch buffer and back, on `stream`
+static int local_roundtrip(Comm *c, hipStream_t stream, float *buf, int64_t n) {
+    if (n <= 0) return RG_OK;
+    if ((size_t)n > c->scratch_floats) {
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e == hipSuccess && c->scratch) e = hipFree(c->scratch);
+        c->scratch = nullptr;
+        c->scratch_floats = 0;
+        if (e == hipSuccess) e = hipMalloc(&c->scratch, (size_t)n * sizeof(float));
+        if (e != hipSuccess) {
+            set_error(std::string("rg_comm (local): scratch: ") + hipGetErrorString(e));
+            return RG_E_LAUNCH;
+        }
+        c->scratch_floats = (size_t)n;
+    }
+    hipError_t e = hipMemcpyAsync(c->scratch, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(buf, c->scratch, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) {
+        set_error(std::string("rg_comm (local): copy: ") + hipGetErrorString(e));
+        return RG_E_LAUNCH;
+    }
+    return RG_OK;
+}
 
 static int nccl_fail(const char *what, ncclResult_t r) {
     set_error(std::string(what) + ": " + ncclGetErrorString(r));
@@ -40,6 +73,7 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
     hipError_t e = hipEventRecord(c->ev_in, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
     if (e != hipSuccess) return hip_fail("rg_comm_allreduce_begin", e);
+    if (c->local) return local_roundtrip(c, c->stream, buf, n);
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return nccl_fail("ncclAllReduce", r);
     return RG_OK;
@@ -59,6 +93,7 @@ int comm_end(void *h, hipStream_t stream) {
 int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || !buf || chunk < 0) return fail_arg("rg_comm_reduce_scatter_f32: bad argument");
+    if (c->local) return local_roundtrip(c, stream, buf + (int64_t)c->rank * chunk, chunk * c->world);
     const ncclResult_t r = ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
                                              ncclSum, c->comm, stream);
     return r == ncclSuccess ? RG_OK : nccl_fail("ncclReduceScatter", r);
@@ -67,6 +102,13 @@ int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) 
 int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const int64_t *counts) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || n < 0 || (n > 0 && (!bufs || !counts))) return fail_arg("rg_comm_allgather_f32: bad argument");
+    if (c->local) {
+        for (int k = 0; k < n; ++k) {
+            const int rc = local_roundtrip(c, stream, bufs[k], counts[k] * c->world);
+            if (rc) return rc;
+        }
+        return RG_OK;
+    }
     ncclResult_t r = ncclGroupStart();
     for (int k = 0; k < n && r == ncclSuccess; ++k)
         r = ncclAllGather(bufs[k] + (int64_t)c->rank * counts[k], bufs[k], (size_t)counts[k], ncclFloat32, c->comm,
@@ -130,10 +172,37 @@ extern "C" void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, 
     return c;
 }
 
+extern "C" void *rg_comm_create_local(int32_t world, int32_t rank, int32_t device) {
+    if (world < 1 || rank < 0 || rank >= world) {
+        rg::set_error("rg_comm_create_local: bad argument");
+        return nullptr;
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { rg::hip_fail("rg_comm_create_local: hipSetDevice", e); return nullptr; }
+    rg::Comm *c = new (std::nothrow) rg::Comm();
+    if (!c) { rg::set_error("rg_comm_create_local: out of memory"); return nullptr; }
+    c->world = world;
+    c->rank = rank;
+    c->local = true;
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
+    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, evf);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, evf);
+    if (e != hipSuccess) {
+        rg::hip_fail("rg_comm_create_local", e);
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
 extern "C" int rg_comm_destroy(void *h) {
     rg::Comm *c = static_cast<rg::Comm *>(h);
     if (!c) return RG_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->scratch) hipFree(c->scratch);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     if (c->ev_out) hipEventDestroy(c->ev_out);
