@@ -121,7 +121,7 @@ typedef struct rg_mf_work {
     int32_t *row_count;      /* [num_users + num_items] */
     int32_t *row_list;       /* [(num_users + num_items) * RG_MF_LIST_CAP * 2] {other row, dz bits} */
     int64_t *hot_grad;       /* [(num_users + num_items) * dim] overflow accumulators, int64 fixed
-                                point (value * 2^52): order-independent, bit-reproducible sums */
+                                point (value * 2^48): order-independent, bit-reproducible sums */
     int64_t *hot_bias_grad;  /* [num_users + num_items], the same */
     float *loss_partials;    /* [rg_mf_partials_len(cols, dim)] */
     float *scores;           /* [cols]  (adaptive hinge only) */

@@ -125,15 +125,20 @@ __device__ __forceinline__ float sigmoidf_ref(float z) { return 1.0f / (1.0f + e
 
 // ---------------------------------------------------------------- overflow accumulators
 // Rows touched more than RG_MF_LIST_CAP times in a step add their surplus contributions
-// atomically.  The accumulators are int64 fixed point (2^-52 resolution, range +-2048):
+// atomically.  The accumulators are int64 fixed point (2^-48 resolution, range +-32768):
 // integer addition is associative, so the sum does not depend on the atomics' arrival
 // order, and a row that overflowed sums ALL of its contributions (list and surplus) this
 // way -- its gradient is then bit-reproducible whichever contributions the list took.
-// Range: a row's gradient element is a sum of dz * (embedding element) with sum |dz| of
-// order one over a whole step (the loss is a mean), so it stays far inside +-2048; the
-// resolution keeps a gradient that cancels to ~1e-8 (where Adam's g / (|g| + eps) makes
-// its relative error visible) exact to ~1e-8 relative.
-constexpr double kFixScale = 4503599627370496.0;   // 2^52
+// Range (no run-time guard: a contribution or running sum of magnitude >= 32768 would wrap):
+//  * MF: an element's gradient is sum dz * (partner embedding element), with sum |dz| <= 1
+//    over a step (|dL/dp| <= 1/B per pair of a mean loss, |dp/dz| <= 1/4) and embeddings of
+//    order 1/d at init, so |sum| stays below ~1 unless the tables themselves diverge;
+//  * NCF / NeuMF: dz times the tower's back-propagated input vector (|W|-bounded products of
+//    Xavier weights, order 1) or the GMF partner row (N(0,1) init): again sum |dz| <= 1 times
+//    an order-one vector.
+// Both leave > 4 orders of magnitude of headroom.  Resolution: 2^-49 rounding per
+// contribution, below fp32's own rounding of the ~1e-6 contributions a step produces.
+constexpr double kFixScale = 281474976710656.0;   // 2^48
 __device__ __forceinline__ long long to_fix(float v) { return __double2ll_rn((double)v * kFixScale); }
 __device__ __forceinline__ float from_fix(long long x) { return (float)((double)x * (1.0 / kFixScale)); }
 __device__ __forceinline__ void fix_add(long long *p, float v) {

@@ -194,8 +194,16 @@ __global__ __launch_bounds__(kPT) void plan_kernel(PlanArgs a) {
         for (int64_t j = j0; j < j1; ++j) c += owned(a, lo + j) ? 1 : 0;
         block_excl_scan(c, sh, &n_own);
     }
-    if (n_own <= kLdsKeys) plan_body<true>(a, k, lo, m, n_own, lds_keys, sh);
-    else plan_body<false>(a, k, lo, m, n_own, lds_keys, sh);
+    if (n_own <= kLdsKeys) {
+        plan_body<true>(a, k, lo, m, n_own, lds_keys, sh);
+    } else if (a.scratch == nullptr) {   // owner filter without scratch: refused per batch (host retries)
+        if (threadIdx.x == 0) {
+            a.counts[2 * k] = -1;
+            a.counts[2 * k + 1] = -1;
+        }
+    } else {
+        plan_body<false>(a, k, lo, m, n_own, lds_keys, sh);
+    }
 }
 
 }  // namespace
@@ -226,13 +234,17 @@ extern "C" int rg_mf_plans_build(void *stream, const int64_t *users, const int64
     if (batch_len > cols) return fail_arg("rg_mf_plans_build: batch_len > cols (the output stride)");
     if (cols >= ((int64_t)1 << 31)) return fail_arg("rg_mf_plans_build: cols too large");
     const int64_t need = rg_mf_plans_scratch_len(cols, n_batches);
-    if (need > 0 && !scratch) return fail_arg("rg_mf_plans_build: batches over 16384 planned positives need scratch");
+    // owner filter (world > 1): a rank plans ~cols / world positives per batch, almost always
+    // within the LDS path, so scratch may be omitted; a batch that needs it then reports
+    // counts = -1 and the caller rebuilds with scratch
+    if (need > 0 && !scratch && owner_world <= 1)
+        return fail_arg("rg_mf_plans_build: batches over 16384 planned positives need scratch");
     PlanArgs a{};
     a.users = users; a.items = items; a.n = n; a.offset = offset; a.stride = stride; a.batch_len = batch_len;
     a.cols = cols; a.num_items = num_items; a.upb = units_per_block; a.world = owner_world; a.rank = owner_rank;
     a.perm = perm; a.pos_slot = pos_slot; a.item_slot_off = item_slot_off; a.counts = counts;
     a.scratch = scratch;
-    a.scratch_stride = n_batches > 0 && need > 0 ? need / n_batches : 0;
+    a.scratch_stride = n_batches > 0 && need > 0 && scratch ? need / n_batches : 0;
     hipLaunchKernelGGL(plan_kernel, dim3((unsigned)n_batches), dim3(kPT), 0, (hipStream_t)stream, a);
     return check_launch("rg_mf_plans_build");
 }

@@ -39,6 +39,7 @@ from .spotlight.optimizers import describe
 from .spotlight.sampling import NegativePool
 from .spotlight.torch_utils import set_seed, shuffle
 from .spotlight import evaluation
+from .spotlight import losses
 from .utils.storage_utils import save_statistics
 
 logging.basicConfig(format="%(message)s", level=logging.INFO)
@@ -119,6 +120,9 @@ class ImplicitFactorizationModel:
             net = BilinearNet(self._num_users, self._num_items, self._embedding_dim, sparse=self._sparse)
         self._net = net.to(dev)
         self._opt = describe(self._optimizer_func, self._learning_rate, self._l2)
+        # the reference's loss selection (implicit.py:194-199); the fused step computes the same
+        # loss in its kernel, this is the function for callers that score pairs themselves
+        self._loss_func = losses.bpr_loss if self._loss == "pairwise_bpr" else losses.loss_for(self._loss)
         if not self.neg_examples:
             raise NotImplementedError("training without a negative pool (neg_examples) is not supported")
         self._pool = NegativePool.from_pairs(self.neg_examples)
@@ -171,8 +175,9 @@ class ImplicitFactorizationModel:
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
                               "epochs": self._n_iter}
-        with open(os.path.join(self.experiment_logs, "configuration.json"), "w") as fp:
-            json.dump(self.configuration, fp)
+        if self._rank == 0:            # one writer per experiment folder in a data-parallel fit
+            with open(os.path.join(self.experiment_logs, "configuration.json"), "w") as fp:
+                json.dump(self.configuration, fp)
 
     def _check_input(self, user_ids, item_ids, allow_items_none=False):
         user_id_max = user_ids if isinstance(user_ids, int) else user_ids.max()

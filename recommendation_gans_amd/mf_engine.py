@@ -134,15 +134,23 @@ def build_plans(items, batch_size, units_per_block, num_items, *, offset=0, stri
     pos_slot = torch.empty(n_batches * cols, dtype=torch.int32, device=dev)
     off = torch.empty(n_batches * (num_items + 1), dtype=torch.int32, device=dev)
     counts = torch.empty(2 * n_batches, dtype=torch.int32, device=dev)
-    sl = int(lib.rg_mf_plans_scratch_len(cols, n_batches))
-    scratch = torch.empty(max(sl, 1), dtype=torch.int64, device=dev) if sl > 0 else None
     for t in (items, users):
         if t is not None and (t.dtype != torch.int64 or not t.is_contiguous() or t.device != dev):
             raise ValueError("plan inputs must be contiguous int64 tensors on one device")
-    check(lib.rg_mf_plans_build(_lib.stream_handle(), ptr(users) if world > 1 else None, ptr(items), n, offset,
-                                stride, batch_size, n_batches, cols, units_per_block, num_items, world, rank,
-                                ptr(perm), ptr(pos_slot), ptr(off), ptr(counts), ptr(scratch)), "rg_mf_plans_build")
-    planned = counts.cpu().numpy()[0::2]
+
+    def run(with_scratch):
+        sl = int(lib.rg_mf_plans_scratch_len(cols, n_batches)) if with_scratch else 0
+        scratch = torch.empty(max(sl, 1), dtype=torch.int64, device=dev) if sl > 0 else None
+        check(lib.rg_mf_plans_build(_lib.stream_handle(), ptr(users) if world > 1 else None, ptr(items), n, offset,
+                                    stride, batch_size, n_batches, cols, units_per_block, num_items, world, rank,
+                                    ptr(perm), ptr(pos_slot), ptr(off), ptr(counts), ptr(scratch)),
+              "rg_mf_plans_build")
+        return counts.cpu().numpy()[0::2]
+    # the owner filter plans ~cols / world positives of a batch: the LDS path, no scratch
+    # (~12 B per training positive otherwise); a batch over the LDS capacity reports -1
+    planned = run(with_scratch=world <= 1)
+    if (planned < 0).any():
+        planned = run(with_scratch=True)
     return [MFPlan(perm[k * cols:(k + 1) * cols], pos_slot[k * cols:(k + 1) * cols],
                    off[k * (num_items + 1):(k + 1) * (num_items + 1)], int(planned[k])) for k in range(n_batches)]
 

@@ -40,27 +40,68 @@ def test_python_binding_covers_header():
     assert b"gfx950" in L.rg_version()
 
 
+CTYPES_MIRRORS = {
+    "rg_mf_tables_t": "MFTables", "rg_mf_batch_t": "MFBatch", "rg_mf_work_t": "MFWork",
+    "rg_mf_loss_t": "MFLoss", "rg_opt_t": "Opt", "rg_mf_mark_t": "MFMark", "rg_mt_gen_t": "MTGen",
+    "rg_mf_owner_batch_t": "MFOwnerBatch", "rg_mf_stepper_config_t": "MFStepperConfig",
+    "rg_mf_step_in_t": "MFStepIn", "rg_ncf_model_t": "NCFModel", "rg_ncf_work_t": "NCFWork",
+    "rg_gan_dims_t": "GANDims", "rg_gan_model_t": "GANModel", "rg_gan_batch_t": "GANBatch",
+    "rg_gan_noise_t": "GANNoise"}
+
+
+def header_structs():
+    """{typedef name: [field names in declaration order]} for every struct of include/rg_hip.h."""
+    txt = open(os.path.join(ROOT, "include", "rg_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"typedef\s+struct\s+\w*\s*\{(.*?)\}\s*(\w+)\s*;", txt, flags=re.S):
+        fields = []
+        for decl in m.group(1).split(";"):
+            decl = " ".join(decl.split())
+            if not decl:
+                continue
+            # "const float *a, *b" / "int64_t n" / "void *masks[8]": names after the type
+            head, *rest = decl.split(",")
+            names = [head.split()[-1]] + [r.strip() for r in rest]
+            fields += [re.sub(r"[\*\s]|\[.*\]", "", nm) for nm in names]
+        out[m.group(2)] = fields
+    return out
+
+
+def test_every_header_struct_has_a_ctypes_mirror():
+    assert set(header_structs()) == set(CTYPES_MIRRORS), set(header_structs()) ^ set(CTYPES_MIRRORS)
+
+
 def test_struct_layouts_match_header():
-    """ctypes mirrors of the structs have the sizes the C compiler gives them."""
+    """Every ctypes mirror has the C compiler's size and, field by field, the same names
+    and offsets (the GAN / NCF / owner structs cross the boundary on every call too)."""
     import subprocess
     import tempfile
     from recommendation_gans_amd import _lib
-    src = r'''
-#include <stdio.h>
-#include "rg_hip.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(rg_mf_tables_t), sizeof(rg_mf_batch_t),
- sizeof(rg_mf_work_t), sizeof(rg_opt_t), sizeof(rg_mf_loss_t), sizeof(rg_mf_stepper_config_t),
- sizeof(rg_mf_step_in_t)); return 0;}
-'''
+    structs = header_structs()
+    lines = []
+    for name, fields in sorted(structs.items()):
+        lines.append(f'printf("{name} %zu", sizeof({name}));')
+        for f in fields:
+            lines.append(f'printf(" %zu", offsetof({name}, {f}));')
+        lines.append('printf("\\n");')
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"rg_hip.h\"\nint main(void){" + "\n".join(lines) + \
+        "return 0;}\n"
     with tempfile.TemporaryDirectory() as td:
         c = os.path.join(td, "s.c")
         open(c, "w").write(src)
         exe = os.path.join(td, "s")
         subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
-        sizes = [int(x) for x in subprocess.check_output([exe]).split()]
-    assert sizes == [ctypes.sizeof(_lib.MFTables), ctypes.sizeof(_lib.MFBatch),
-                     ctypes.sizeof(_lib.MFWork), ctypes.sizeof(_lib.Opt), ctypes.sizeof(_lib.MFLoss),
-                     ctypes.sizeof(_lib.MFStepperConfig), ctypes.sizeof(_lib.MFStepIn)]
+        got = {}
+        for ln in subprocess.check_output([exe]).decode().splitlines():
+            name, *nums = ln.split()
+            got[name] = [int(x) for x in nums]
+    for name, fields in structs.items():
+        cls = getattr(_lib, CTYPES_MIRRORS[name])
+        cfields = [f[0] for f in cls._fields_]
+        assert cfields == fields, (name, cfields, fields)
+        want = [ctypes.sizeof(cls)] + [getattr(cls, f).offset for f in fields]
+        assert got[name] == want, (name, got[name], want)
 
 
 def test_no_gpu_means_loud_failure():
