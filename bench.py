@@ -717,7 +717,8 @@ def main():
 
     # step inputs (ids + plan pointers) built before timing; each call also hands the
     # NEXT step's input to the native stepper, which generates its words ahead
-    inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + 1)]
+    n_extra = 6          # untimed steps after the timed region (lazy-pass row counts)
+    inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + n_extra + 1)]
 
     def step(s, ev=None):
         return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev)
@@ -739,6 +740,9 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s, evs[s])
+    # the lazy pass leaves cold user rows behind: catching them all up is part of the timed
+    # work (after this every row equals the eager pass's; no-op when eager)
+    eng.flush()
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if multi:
@@ -749,6 +753,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss_last = float(eng.loss_out[0])
+    lazy_rows = None
+    if eng.lazy_rows(enable=True) is not None:
+        # untimed: user rows the lazy pass processes per step (the counter is contended, so it
+        # runs only here), over steps that continue the timed sequence
+        base = args.warmup + args.steps
+        for s in range(n_extra - 1):
+            eng.train_step_in(inputs[base + s], inputs[base + s + 1])
+        lazy_rows = eng.lazy_rows(enable=False) / (n_extra - 1)
+        eng.flush()
 
     if emu is not None:
         return report_emulated(args, emu, eng, evs, el, U, I, d, B, n)
@@ -780,6 +793,13 @@ def main():
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
                                 "frac": step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS}
         out["host_enqueue_us_per_step"] = t_enq / args.steps * 1e6
+        if lazy_rows is not None:
+            out["lazy_dense_pass"] = {
+                "user_rows_per_step": lazy_rows, "user_rows": U_local,
+                "note": "deferred cold user-row updates (DESIGN §4.1): a user row is processed when it has a "
+                        "gradient or the next step reads it, its skipped cold updates applied in order on the "
+                        "way; bit-identical to the eager dense pass (tests/test_lazy_gpu.py); the timed region "
+                        "ends with the flush that brings every row up to date"}
         if any(ev is not None for ev in evs):
             from recommendation_gans_amd import _lib
             ms = [_lib.elapsed_ms(a, b) for a, b in (ev for ev in evs if ev is not None)]
@@ -798,6 +818,12 @@ def main():
                 # (DP: up to the user-shard update; the item update follows the exchange)
                 alg = gather + ids + user_adam
                 kname = "rg_mf_step_front + rg_mf_step_hot (mf_front_kernel, mf_hot_kernel)"
+            elif lazy_rows is not None:
+                # rg_mf_apply_lazy: p, m, v of every item row and of the user rows it processes
+                # (a gradient this step or a next-step mark), read + written once
+                alg = 6 * (I + lazy_rows) * (4 * d + 4)
+                kname = ("rg_mf_apply_lazy (mf_back_kernel<LAZY>: every item row + the user rows with a "
+                         "gradient or a next-step mark; deferred cold updates applied on the way)")
             else:
                 # rg_mf_apply_prepare: the dense optimizer pass and the next step's prepare
                 # (ids in, prepared pairs out) in one launch
@@ -811,7 +837,7 @@ def main():
             # PMC traffic (scripts/pmc_apply.sh: FETCH_SIZE / WRITE_SIZE passes) of THIS build only:
             # the profile is stamped with the library's hash, a profile of another build is refused
             pmc = os.path.join(ROOT, "profiles", "pmc_step.json" if fused else "pmc_back.json")
-            if world == 1 and not own and not gs and os.path.exists(pmc):
+            if world == 1 and not own and not gs and lazy_rows is None and os.path.exists(pmc):
                 import hashlib
                 p = json.load(open(pmc))
                 sha = hashlib.sha256(open(os.environ.get("RG_LIB") or rg_build.LIB, "rb").read()).hexdigest()[:16]

@@ -360,10 +360,16 @@ typedef struct rg_mf_owner_batch {
     int32_t world, rank;
     int32_t *neg_rec;                    /* [4 * rg_mf_owner_rec_len(GC, n_neg)] prepared records */
     int32_t *seg_count;                  /* [rg_mf_owner_segments(GC, n_neg)] */
-    float *scores;                       /* [(1 + n_neg) * GC] */
+    float *scores;                       /* [(1 + n_neg) * GC] (+ 4 for the adaptive hinge: max, its
+                                            pair, the active count -- rg_mf_owner_adapt) */
 } rg_mf_owner_batch_t;
 
 int64_t rg_mf_owner_segments(int64_t global_cols, int32_t n_neg);
+/* Adaptive hinge, after the score exchange: the global max negative (largest score, first
+ * draw on ties) and the active-positive count, computed from the full score vector on every
+ * rank (no further exchange), into scores[(1 + n_neg) * GC + {0, 1, 2}]; rg_mf_owner_back
+ * then gives the positives the hinge against it and the max's owner its gradient. */
+int rg_mf_owner_adapt(void *stream, const rg_mf_owner_batch_t *b);
 int64_t rg_mf_owner_rec_len(int64_t global_cols, int32_t n_neg);
 /* float loss partials rg_mf_owner_back writes (upper bound over any n_planned <= GC) */
 int64_t rg_mf_owner_partials_len(int64_t global_cols, int32_t n_neg, int32_t dim, int32_t world);
@@ -394,6 +400,42 @@ int rg_mf_scores(void *stream, const float *user_w, const float *item_w,
                  const int64_t *users, const int64_t *items, int64_t n, float *out);
 
 /* ------------------------------------------------------------------------------
+ * Lazy dense pass.  The reference's dense coupled-L2 optimizer moves EVERY
+ * row every step (optimizers.py:10-16 over sparse=False tables, mf_spotlight.py:55); a
+ * user row no pair touches gets the cold update opt(p, grad = wd * p) only.  The lazy
+ * pass defers those cold updates: a user row is processed at step t iff it has a data
+ * gradient at t (list count), the NEXT step's pair pass reads it (a mark the next step's
+ * prepare wrote), or the pass is a full one; a processed row first applies its skipped
+ * cold updates in step order with each step's own Adam constants (the eager pass's exact
+ * operation sequence), so every row any kernel reads is bit-identical to the eager
+ * pass's, and rg_mf_lazy_flush brings every row up to date (before validation, predict,
+ * a checkpoint, the end of a fit).  Item rows are always processed.
+ * ---------------------------------------------------------------------------- */
+typedef struct rg_mf_lazy {
+    int32_t *last_rel;         /* [num_users] last step applied to each user row, minus base */
+    int32_t *umark;            /* [num_users] step whose pair pass reads the row (prepare marks) */
+    const float *step_consts;  /* [2 * n_consts] Adam (step_size, bias_correction2_sqrt) of absolute step s */
+    int64_t n_consts;
+    int64_t base;              /* absolute step of last_rel == 0 */
+    int64_t step;              /* rg_mf_apply_lazy: the step applied; rg_mf_lazy_flush: the step caught up to */
+    int32_t full;              /* rg_mf_apply_lazy: process every user row */
+    int32_t pad_;
+    uint64_t *rows_done;       /* optional: += user rows processed (diagnostics; contended) */
+} rg_mf_lazy_t;
+
+/* The pair pass of this step (rg_mf_pairs, backward) and the prepare of `next` in one
+ * launch; the prepare stores umark[user] = umark_step for every pair's user. */
+int rg_mf_pairs_prepare(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *b, rg_mf_work_t *w,
+                        const rg_mf_batch_t *next, const rg_mf_work_t *next_w, int32_t *umark, int32_t umark_step);
+/* Lazy dense pass of step lazy->step over every row (items always, users by the rule
+ * above), loss finalisation, optional MT walk; writes the *_out tables. */
+int rg_mf_apply_lazy(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                     const rg_mf_loss_t *loss, const rg_mf_lazy_t *lazy, const rg_mt_gen_t *gen);
+/* Every user row caught up to step lazy->step, into the tables' IN side (the current set;
+ * a row whose value is in the other set is read from the *_out side). */
+int rg_mf_lazy_flush(void *stream, const rg_mf_tables_t *t, const rg_opt_t *opt, const rg_mf_lazy_t *lazy);
+
+/* ------------------------------------------------------------------------------
  * RCCL communicator (rg_comm.cpp) for the user-sharded data-parallel step: one
  * process per GPU; rank 0 makes the id, the caller broadcasts it (torch.distributed),
  * every rank creates its communicator on `device`.
@@ -405,6 +447,14 @@ void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, int32_t dev
  * --emulate-rank): every collective is a same-size local copy out and back on the
  * communicator stream (data unchanged), placed and fenced like the RCCL path. */
 void *rg_comm_create_local(int32_t world, int32_t rank, int32_t device);
+/* Host-staged stand-in (tests: two processes sharing one GPU, where RCCL refuses a second
+ * rank on a device): each all-reduce runs on the communicator stream, placed and fenced like
+ * the RCCL one, as a D2H copy into pinned staging, a host callback fn(ctx, host_buf, n)
+ * (stream-ordered, hipLaunchHostFunc; must sum host_buf over the ranks in place and return
+ * 0; no HIP calls), and an H2D copy back.  All-reduce only; n <= max_floats. */
+typedef int (*rg_host_allreduce_fn)(void *ctx, float *host_buf, int64_t n);
+void *rg_comm_create_host(int32_t world, int32_t rank, int32_t device, int64_t max_floats,
+                          rg_host_allreduce_fn fn, void *ctx);
 int rg_comm_destroy(void *comm);
 /* In-place sum over ranks, stream-ordered with respect to `stream` (runs on the
  * communicator's own stream between two events). */
@@ -526,6 +576,16 @@ int rg_mf_stepper_advance(void *stepper, int32_t flip_sets, int64_t steps);
 /* direction 0: copy the MT state after the last consumed word to host_state[625];
  * 1: load host_state into the device state (drops words generated ahead).  Synchronises. */
 int rg_mf_stepper_sync_mt(void *stepper, uint32_t *host_state, int32_t direction);
+/* Lazy split step (single rank; RG_LAZY=0 disables): bring every user row up to the
+ * current step in the current set (rg_mf_lazy_flush; no-op when none lags).  The
+ * stepper flushes by itself before an external consumer (acquire) and before a step
+ * whose pairs it did not prepare; callers that read the tables directly (predict, a
+ * checkpoint, set_params) call it first. */
+int rg_mf_stepper_flush(void *stepper, void *stream);
+/* Diagnostics: *rows_out = user rows the lazy passes processed since the last call
+ * (synchronises; then reset); `enable` turns the counting on for later steps.  Returns 1
+ * if the stepper runs the lazy pass, 0 if not. */
+int rg_mf_stepper_lazy_count(void *stepper, int32_t enable, uint64_t *rows_out);
 
 /* ------------------------------------------------------------------------------
  * NCF MLP (rg_ncf.hip): spotlight/dnn_models/mlp.py:5-46 trained by
@@ -576,6 +636,18 @@ int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim);
 int rg_ncf_pairs(void *stream, const rg_ncf_model_t *model, const rg_mf_batch_t *batch, rg_mf_work_t *work,
                  rg_ncf_work_t *ncf_work, int32_t phase);
 int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *batch, rg_ncf_work_t *ncf_work, float *loss_partials);
+/* Adaptive hinge over several ranks (data-parallel NCF / NeuMF): this rank's largest
+ * negative (score, draw index) into slot `rank` of a zeroed [world * 4] float buffer
+ * (the caller then SUM all-reduces it: one writer per slot, so it acts as an all-gather),
+ * its local row in *local_row; then the positives' dp against the global maximum, this
+ * rank's active-positive count in *count (SUM all-reduce it) and loss share; then the
+ * winning rank sets the maximum's dp = global count / global_pos. */
+int rg_ncf_adapt_local(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w, rg_ncf_work_t *nw,
+                       float *slots, int32_t rank, int32_t world, int32_t *local_row);
+int rg_ncf_adapt_global(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, const float *slots,
+                        int32_t world, float *count, float *loss_partials);
+int rg_ncf_adapt_winner(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, const float *slots,
+                        int32_t world, int32_t rank, const int32_t *local_row, const float *count);
 int rg_ncf_update(void *stream, const rg_ncf_model_t *model, const rg_ncf_work_t *ncf_work, int64_t nparts,
                   const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss);
 /* Data-parallel NCF / NeuMF step (replicated, reference-exact: R ranks take column slices of

@@ -27,6 +27,8 @@ c_i64p = ctypes.POINTER(ctypes.c_int64)
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
 c_u64p = ctypes.POINTER(ctypes.c_uint64)
+# rg_host_allreduce_fn (include/rg_hip.h): int (*)(void *ctx, float *host_buf, int64_t n)
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 
 class MFTables(ctypes.Structure):
@@ -138,6 +140,12 @@ GAN_D_BLOCKS = ["W1S", "EMB", "W1E", "B1", "W2", "B2", "W3", "B3", "W4", "B4"]
 GAN_WS_FAKE, GAN_WS_DOUT = 0, 1
 
 
+class MFLazy(ctypes.Structure):
+    _fields_ = [("last_rel", ctypes.c_void_p), ("umark", ctypes.c_void_p), ("step_consts", ctypes.c_void_p),
+                ("n_consts", ctypes.c_int64), ("base", ctypes.c_int64), ("step", ctypes.c_int64),
+                ("full", ctypes.c_int32), ("pad_", ctypes.c_int32), ("rows_done", ctypes.c_void_p)]
+
+
 class MFStepIn(ctypes.Structure):
     _fields_ = [("pos_user", ctypes.c_void_p), ("pos_item", ctypes.c_void_p), ("n_pos", ctypes.c_int64),
                 ("global_pos", ctypes.c_int64), ("plan_perm", ctypes.c_void_p), ("plan_pos_slot", ctypes.c_void_p),
@@ -184,6 +192,14 @@ SIGNATURES = [
     ("rg_ncf_blocks", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFBatch),
                                     ctypes.POINTER(MFWork), ctypes.POINTER(NCFWork), ctypes.c_int32]),
+    ("rg_ncf_adapt_local", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                          ctypes.POINTER(NCFWork), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_void_p]),
+    ("rg_ncf_adapt_global", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(NCFWork),
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_ncf_adapt_winner", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(NCFWork),
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     ("rg_ncf_adapt_dp", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(NCFWork),
                                        ctypes.c_void_p]),
     ("rg_ncf_update", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(NCFWork),
@@ -218,6 +234,8 @@ SIGNATURES = [
     ("rg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("rg_comm_create", ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_comm_create_local", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rg_comm_create_host", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("rg_comm_allreduce_sum_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     ("rg_mt_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
@@ -272,6 +290,7 @@ SIGNATURES = [
     ("rg_mf_owner_partials_used", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                    ctypes.c_int64]),
     ("rg_mf_owner_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFOwnerBatch)]),
+    ("rg_mf_owner_adapt", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFOwnerBatch)]),
     ("rg_mf_owner_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFOwnerBatch)]),
     ("rg_mf_owner_back", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFOwnerBatch),
                                         ctypes.POINTER(MFWork)]),
@@ -307,6 +326,16 @@ SIGNATURES = [
     ("rg_mf_stepper_state", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_mf_stepper_advance", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]),
     ("rg_mf_stepper_sync_mt", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
+    ("rg_mf_stepper_flush", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_lazy_count", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("rg_mf_pairs_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
+                                           ctypes.POINTER(MFWork), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                           ctypes.c_void_p, ctypes.c_int32]),
+    ("rg_mf_apply_lazy", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                        ctypes.POINTER(Opt), ctypes.POINTER(MFLoss), ctypes.POINTER(MFLazy),
+                                        ctypes.POINTER(MTGen)]),
+    ("rg_mf_lazy_flush", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(Opt),
+                                        ctypes.POINTER(MFLazy)]),
     ("rg_event_elapsed_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_last_error", ctypes.c_char_p, []),
     ("rg_version", ctypes.c_char_p, []),

@@ -81,3 +81,45 @@ class LocalComm(RcclComm):
         if not self.handle:
             raise RuntimeError("rg_comm_create_local: " + self.lib.rg_last_error().decode())
 
+
+class HostComm(RcclComm):
+    """Test stand-in for rank ``rank`` of a torch.distributed (gloo) group whose ranks share one
+    GPU (RCCL refuses that): the native step's all-reduces run on the communicator stream as
+    D2H -> a stream-ordered host callback summing over the group with torch.distributed -> H2D
+    (rg_comm_create_host), so the step's own placement -- the score exchange fenced on the main
+    stream, the item gradient's exchange on the side stream beside the user update -- runs as in
+    production.  Reduce-scatter / all-gather are not provided.
+
+    The callback takes the GIL on the runtime's callback thread: while the step's work is in
+    flight, wait with ``sync()`` (a ctypes call, which releases the GIL), not with a torch call
+    that may hold it."""
+
+    def __init__(self, device, group=None, max_floats=1 << 26):
+        import torch.distributed as dist
+        self.lib = _lib.load()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.group = group
+
+        def _allreduce(ctx, buf, n):
+            try:
+                arr = np.ctypeslib.as_array((ctypes.c_float * n).from_address(buf))
+                dist.all_reduce(torch.from_numpy(arr), group=self.group)
+                return 0
+            except Exception:      # reported by the next collective call (rg_comm host_error)
+                return 1
+        self._cb = _lib.HOST_ALLREDUCE_FN(_allreduce)
+        index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.handle = self.lib.rg_comm_create_host(self.world, self.rank, index, int(max_floats),
+                                                   ctypes.cast(self._cb, ctypes.c_void_p), None)
+        if not self.handle:
+            raise RuntimeError("rg_comm_create_host: " + self.lib.rg_last_error().decode())
+        self._hip = ctypes.CDLL("libamdhip64.so.7")
+
+    def sync(self):
+        """hipDeviceSynchronize through ctypes (the GIL is released while it waits)."""
+        rc = self._hip.hipDeviceSynchronize()
+        if rc != 0:
+            raise RuntimeError(f"hipDeviceSynchronize failed: {rc}")
+

@@ -31,7 +31,43 @@ struct Comm {
     bool local = false;           // rg_comm_create_local: collectives are local copies
     float *scratch = nullptr;     // local: copy target
     size_t scratch_floats = 0;
+    // rg_comm_create_host: the all-reduce staged through pinned host memory and done by a
+    // host callback in stream order on the communicator stream (tests: gloo across two
+    // processes sharing one GPU, where RCCL refuses a second rank on the device)
+    rg_host_allreduce_fn host_fn = nullptr;
+    void *host_ctx = nullptr;
+    float *pinned = nullptr;
+    int64_t pinned_floats = 0;
+    struct HostCall {
+        Comm *c;
+        int64_t n;
+    } calls[64];
+    int next_call = 0;
+    int host_error = 0;
 };
+
+static void host_trampoline(void *p) {
+    Comm::HostCall *hc = static_cast<Comm::HostCall *>(p);
+    if (hc->c->host_fn(hc->c->host_ctx, hc->c->pinned, hc->n) != 0) hc->c->host_error = 1;
+}
+
+// host-staged all-reduce: D2H -> host callback -> H2D, all on the communicator stream
+static int host_allreduce(Comm *c, float *buf, int64_t n) {
+    if (n > c->pinned_floats) return fail_arg("rg_comm (host): buffer larger than the staging area");
+    if (c->host_error) return fail_arg("rg_comm (host): an earlier host all-reduce failed");
+    Comm::HostCall *hc = &c->calls[c->next_call];
+    c->next_call = (c->next_call + 1) % 64;
+    hc->c = c;
+    hc->n = n;
+    hipError_t e = hipMemcpyAsync(c->pinned, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipLaunchHostFunc(c->stream, host_trampoline, hc);
+    if (e == hipSuccess) e = hipMemcpyAsync(buf, c->pinned, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+        set_error(std::string("rg_comm (host): ") + hipGetErrorString(e));
+        return RG_E_LAUNCH;
+    }
+    return RG_OK;
+}
 
 // local stand-in: n floats out to the scratch buffer and back, on `stream`
 static int local_roundtrip(Comm *c, hipStream_t stream, float *buf, int64_t n) {
@@ -74,6 +110,7 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
     if (e != hipSuccess) return hip_fail("rg_comm_allreduce_begin", e);
     if (c->local) return local_roundtrip(c, c->stream, buf, n);
+    if (c->host_fn) return host_allreduce(c, buf, n);
     const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return nccl_fail("ncclAllReduce", r);
     return RG_OK;
@@ -94,6 +131,7 @@ int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) 
     Comm *c = static_cast<Comm *>(h);
     if (!c || !buf || chunk < 0) return fail_arg("rg_comm_reduce_scatter_f32: bad argument");
     if (c->local) return local_roundtrip(c, stream, buf + (int64_t)c->rank * chunk, chunk * c->world);
+    if (c->host_fn) return fail_arg("rg_comm (host): reduce-scatter not supported (all-reduce only)");
     const ncclResult_t r = ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
                                              ncclSum, c->comm, stream);
     return r == ncclSuccess ? RG_OK : nccl_fail("ncclReduceScatter", r);
@@ -102,6 +140,7 @@ int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) 
 int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const int64_t *counts) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || n < 0 || (n > 0 && (!bufs || !counts))) return fail_arg("rg_comm_allgather_f32: bad argument");
+    if (c->host_fn) return fail_arg("rg_comm (host): all-gather not supported (all-reduce only)");
     if (c->local) {
         for (int k = 0; k < n; ++k) {
             const int rc = local_roundtrip(c, stream, bufs[k], counts[k] * c->world);
@@ -198,11 +237,35 @@ extern "C" void *rg_comm_create_local(int32_t world, int32_t rank, int32_t devic
     return c;
 }
 
+extern "C" void *rg_comm_create_host(int32_t world, int32_t rank, int32_t device, int64_t max_floats,
+                                     rg_host_allreduce_fn fn, void *ctx) {
+    if (world < 1 || rank < 0 || rank >= world || max_floats <= 0 || !fn) {
+        rg::set_error("rg_comm_create_host: bad argument");
+        return nullptr;
+    }
+    void *h = rg_comm_create_local(world, rank, device);
+    if (!h) return nullptr;
+    rg::Comm *c = static_cast<rg::Comm *>(h);
+    c->local = false;
+    c->host_fn = fn;
+    c->host_ctx = ctx;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->pinned), (size_t)max_floats * sizeof(float),
+                                 hipHostMallocDefault);
+    if (e != hipSuccess) {
+        rg::hip_fail("rg_comm_create_host: pinned staging", e);
+        rg_comm_destroy(h);
+        return nullptr;
+    }
+    c->pinned_floats = max_floats;
+    return c;
+}
+
 extern "C" int rg_comm_destroy(void *h) {
     rg::Comm *c = static_cast<rg::Comm *>(h);
     if (!c) return RG_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->scratch) hipFree(c->scratch);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     if (c->ev_out) hipEventDestroy(c->ev_out);

@@ -73,6 +73,8 @@ struct PairsArgs {
     const int2 *pairs;         // prepared (user, item) per pair: [(1 + n) * cols], processing order
     int32_t *stamp;            // prepare: per-row serial of the last stamping prepare (null: no stamps)
     int32_t serial;
+    int32_t *umark;            // prepare (lazy dense pass): umark[user] = umark_step for every pair's user
+    int32_t umark_step;
 };
 
 // Prepared ids carry ownership flags in bit 31 when the prepare pass stamped rows:
@@ -134,6 +136,7 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         const uint2 w = a.words[j];
         r = a.pool[choice_index(w.x, w.y, a.pool_len)];
     }
+    if (a.umark != nullptr) a.umark[r.x] = a.umark_step;   // plain store: every writer stores the same value
     if (a.stamp != nullptr) {
         const int32_t ou = atomicExch(a.stamp + r.x, a.serial);
         const int32_t oi = atomicExch(a.stamp + a.num_users + r.y, a.serial);
@@ -466,6 +469,22 @@ __global__ __launch_bounds__(kPairBlock) void mf_pairs_kernel(PairsArgs a) {
     pairs_body<L, PHASE, NMAX>(a, blockIdx.x);
 }
 
+// the pair pass of this step (blocks [0, pair_blocks)) and the prepare pass of the NEXT
+// step (the remaining blocks) in one launch: the lazy split step needs the
+// next step's user marks before its dense pass starts, so the prepare moves out of the
+// dense pass into this latency-bound launch, where its random pool reads run beside the
+// pair pass's gathers
+template <class L, int NMAX>
+__global__ __launch_bounds__(kPairBlock) void mf_pairs_prep_kernel(PairsArgs a, PairsArgs prep, int2 *prep_out,
+                                                                   int64_t pair_blocks) {
+    const int64_t blk = blockIdx.x;
+    if (blk < pair_blocks) {
+        pairs_body<L, kFused, NMAX>(a, blk);
+        return;
+    }
+    if constexpr (kPairBlock == kBlock) prepare_one(prep, prep_out, (blk - pair_blocks) * kBlock + threadIdx.x);
+}
+
 // adaptive hinge: the global-max negative receives sum_b 1/Bp over active b
 // (spotlight/losses.py:170 torch.max(dim 0) backward -> argmax, first index on ties)
 template <class L>
@@ -532,6 +551,16 @@ struct ApplyArgs {
     // biases (Us + Is) | loss], D floats per row
     int64_t shard_users, shard_items, chunk;
     int32_t world, rank;
+    // lazy dense pass: a USER row with a zero data gradient that the next step
+    // does not read is skipped; its cold updates (weight decay + optimizer state only) are
+    // applied, in order and with each step's constants, when the row is next processed
+    int32_t *last_rel;            // [num_users] last step applied to the row, minus lazy_base
+    const int32_t *umark;         // [num_users] step whose pair pass reads the row (prepare marks)
+    const float2 *step_consts;    // [s] Adam (step_size, bias_correction2_sqrt) of absolute step s
+    int64_t lazy_base;            // absolute step of last_rel == 0
+    int32_t lazy_t;               // this step (absolute)
+    int32_t lazy_full;            // process every user row (no next step known)
+    unsigned long long *lazy_rows;   // optional: count of user rows processed (diagnostic steps)
 };
 
 #ifndef RG_MF_SORTED_PULL
@@ -614,8 +643,51 @@ __device__ __forceinline__ float finalize_loss(const float *__restrict__ partial
 // Gradient + optimizer update of unified row r (users [0, U), items [U, U + I)).
 // COLD: a row no pair of the step touches -- its data gradient is exactly zero
 // (only the coupled weight decay acts), so nothing of the step's scratch is read.
-template <class L, int MODE, int NT, bool COLD, bool SPEC = false>
-__device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub) {
+// Adam constants of the last kConstWin steps before this one, staged in LDS by every
+// workgroup of a lazy pass (a row's catch-up loop reads one per skipped step; from global
+// memory each would be a dependent round trip); older steps fall back to global loads
+constexpr int kConstWin = kBlock;
+struct LazyRow {
+    int cnt;          // list count (data gradient this step)
+    int32_t mk, lsr;  // prepare mark, last step applied (relative)
+};
+
+__device__ __forceinline__ float2 step_const(const ApplyArgs &a, const float2 *lconst, int64_t s) {
+    const int64_t w = s - ((int64_t)a.lazy_t - kConstWin);
+    return (w >= 0 && w < kConstWin) ? lconst[w] : a.step_consts[s];
+}
+
+// the cold updates of steps lazy_base + lsr + 1 .. + lag of one row (zero data gradient: the
+// coupled weight decay and the optimizer state only), in step order, each with its own
+// Adam constants -- the exact operation sequence the eager dense pass applies to a row no
+// pair touches (opt_update with gdata = 0), so the row ends bit-identical
+template <class L>
+__device__ __forceinline__ void catch_up(const ApplyArgs &a, const float2 *lconst, int lag, int32_t lsr, int sub,
+                                         float (&p)[L::EPL], float (&m)[L::EPL], float (&v)[L::EPL], float &pb,
+                                         float &mb, float &vb) {
+    rg_opt_t o = a.opt;
+    const bool adam = o.kind == RG_OPT_ADAM;
+    for (int k = 0; k < lag; ++k) {
+        if (adam) {
+            const float2 sc = step_const(a, lconst, a.lazy_base + lsr + 1 + k);
+            o.step_size = sc.x;
+            o.bias_correction2_sqrt = sc.y;
+        }
+#pragma unroll
+        for (int q = 0; q < L::EPL; ++q) p[q] = opt_update(o, p[q], 0.0f, m[q], v[q]);
+        if (sub == 0 && a.has_bias) pb = opt_update(o, pb, 0.0f, mb, vb);
+    }
+}
+
+// every thread of the workgroup: this step's window of Adam constants into LDS
+__device__ __forceinline__ void stage_consts(const ApplyArgs &a, float2 *lconst) {
+    const int64_t s = (int64_t)a.lazy_t - kConstWin + threadIdx.x;
+    if (a.opt.kind == RG_OPT_ADAM && s >= 1) lconst[threadIdx.x] = a.step_consts[s];
+}
+
+template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false>
+__device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub,
+                                          const LazyRow lzr = LazyRow{}, const float2 *lconst = nullptr) {
     constexpr int EPL = L::EPL;
     const int64_t rb = a.row_begin, nr = a.row_end - rb;
     const int D = a.dim;
@@ -625,22 +697,54 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     const bool adam = a.opt.kind == RG_OPT_ADAM;
     const bool has_v = a.opt.kind != RG_OPT_SGD;
 
+    // lazy user row: processed iff it has a data gradient this step (list count), the next
+    // step's pair pass reads it (prepare mark), or the pass is a full one; its current value
+    // is in the set written at its last step -- w_in if an even number of steps was missed
+    // since, else w_out (then the update is in place)
+    const bool lz = LAZY && t == 0;
+    int lag = 0;
+    const int cnt = lzr.cnt;
+    const int32_t lsr = lzr.lsr;
+    const float *src_w = a.w_in[t], *src_b = a.b_in[t];
     float p[EPL], m[EPL], v[EPL], g[EPL];
     float pb = 0.0f, mb = 0.0f, vb = 0.0f;
+    if (lz) {
+        // LSPEC: the optimizer state (one copy, not ping-ponged) is loaded before the decision,
+        // so a processed row's loads take one dependent round trip fewer
+        if (LSPEC) {
+            if (adam) L::load(m, a.w_m[0], lr_, D, sub); else L::zero(m);
+            if (has_v) L::load(v, a.w_v[0], lr_, D, sub); else L::zero(v);
+            if (sub == 0 && a.has_bias) {
+                if (adam) mb = a.b_m[0][lr_];
+                if (has_v) vb = a.b_v[0][lr_];
+            }
+        }
+        if (!(a.lazy_full || cnt > 0 || lzr.mk == a.lazy_t + 1)) return;
+        lag = (int)((int64_t)a.lazy_t - 1 - a.lazy_base - lsr);
+        if (lag & 1) {
+            src_w = a.w_out[t];
+            src_b = a.b_out[t];
+        }
+    }
+
     if (MODE != kGradOnly) {
         if (NT == 2) {
-            L::load_nt(p, a.w_in[t], lr_, D, sub);
+            L::load_nt(p, src_w, lr_, D, sub);
             if (adam) L::load_nt(m, a.w_m[t], lr_, D, sub); else L::zero(m);
             if (has_v) L::load_nt(v, a.w_v[t], lr_, D, sub); else L::zero(v);
         } else {
-            L::load(p, a.w_in[t], lr_, D, sub);
-            if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
-            if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+            L::load(p, src_w, lr_, D, sub);
+            if (!(LSPEC && lz)) {
+                if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
+                if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+            }
         }
         if (sub == 0 && a.has_bias) {
-            pb = a.b_in[t][lr_];
-            if (adam) mb = a.b_m[t][lr_];
-            if (has_v) vb = a.b_v[t][lr_];
+            pb = src_b[lr_];
+            if (!(LSPEC && lz)) {
+                if (adam) mb = a.b_m[t][lr_];
+                if (has_v) vb = a.b_v[t][lr_];
+            }
         }
     }
     L::zero(g);
@@ -656,14 +760,14 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 #ifdef RG_X_NOPULL   // timing experiments only (wrong results): the pass without the pulls
         const int c = a.row_count[r] < 0 ? 1 : 0;
 #else
-        const int c = a.row_count[r];
+        const int c = lz ? cnt : a.row_count[r];
 #endif
         // SPEC: the list and the item's partial-slot range are loaded beside the count
         // (entries past the count are stale and never used), so a touched row's partner
         // rows are its only dependent round trip
         int2 spec[SPEC ? kCap : 1];
         int s0 = 0, s1 = 0;
-        if (SPEC) {
+        if (SPEC && !lz) {
             const int4 *lst = reinterpret_cast<const int4 *>(a.row_list + r * kCap);
 #pragma unroll
             for (int e = 0; e < kCap / 2; ++e) {
@@ -678,7 +782,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             int2 ent[kCap];
 #pragma unroll
             for (int e = 0; e < kCap; ++e)
-                ent[e] = e < ne ? (SPEC ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
+                ent[e] = e < ne ? ((SPEC && !lz) ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
 #if RG_MF_SORTED_PULL
             // the entries' slots were claimed by atomics in arrival order: sorted by (partner,
             // dz bits) the row sums them in an order independent of that timing, so a step
@@ -745,7 +849,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             if (sub == 0 && !a.keep_count) a.row_count[r] = 0;
         }
         if (t == 1 && a.item_slot_off != nullptr) {   // planned positive partials of this item
-            if (!SPEC) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
+            if (!SPEC || lz) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
             for (int sl = s0; sl < s1; sl += 4) {
                 float h[4][EPL];
                 float hb[4];
@@ -775,6 +879,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         }
     }
 
+    if (lz && lag > 0) catch_up<L>(a, lconst, lag, lsr, sub, p, m, v, pb, mb, vb);
 #pragma unroll
     for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
     if (NT == 3) {          // optimizer state streamed past the caches, the new row kept (next gathers)
@@ -795,6 +900,60 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         a.b_out[t][lr_] = pb;
         if (adam) a.b_m[t][lr_] = mb;
         if (has_v) a.b_v[t][lr_] = vb;
+    }
+    if (lz && sub == 0) {
+        a.last_rel[r] = (int32_t)((int64_t)a.lazy_t - a.lazy_base);
+        if (a.lazy_rows) atomicAdd(a.lazy_rows, 1ull);
+    }
+}
+
+// Catch every lazily skipped user row up to step lazy_t (all of its cold updates), into the
+// current set: the in-side tables of `a` (the set the last step wrote).  A row last updated
+// at step ls holds its value in the set written then: the current one if lazy_t - ls is even
+// (updated in place), else the other (a.w_out).
+template <class L>
+__global__ __launch_bounds__(kBlock) void mf_lazy_flush_kernel(ApplyArgs a) {
+    constexpr int LPU = L::LPU, UPW = L::UPW, EPL = L::EPL;
+    __shared__ float2 lconst[kConstWin];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t r = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * UPW + (lane / LPU);
+    const int32_t lsr = r < a.num_users ? a.last_rel[r] : 0;
+    // the window ends at lazy_t + 1: the flush's last catch-up step is lazy_t itself
+    {
+        const int64_t s = (int64_t)a.lazy_t + 1 - kConstWin + threadIdx.x;
+        if (a.opt.kind == RG_OPT_ADAM && s >= 1) lconst[threadIdx.x] = a.step_consts[s];
+    }
+    lds_barrier();
+    if (r >= a.num_users) return;
+    const int lag = (int)((int64_t)a.lazy_t - a.lazy_base - lsr);
+    if (lag <= 0) return;
+    const int D = a.dim;
+    const bool adam = a.opt.kind == RG_OPT_ADAM;
+    const bool has_v = a.opt.kind != RG_OPT_SGD;
+    const float *src_w = (lag & 1) ? a.w_out[0] : a.w_in[0];
+    const float *src_b = (lag & 1) ? a.b_out[0] : a.b_in[0];
+    float p[EPL], m[EPL], v[EPL];
+    float pb = 0.0f, mb = 0.0f, vb = 0.0f;
+    L::load(p, src_w, r, D, sub);
+    if (adam) L::load(m, a.w_m[0], r, D, sub); else L::zero(m);
+    if (has_v) L::load(v, a.w_v[0], r, D, sub); else L::zero(v);
+    if (sub == 0) {
+        pb = src_b[r];
+        if (adam) mb = a.b_m[0][r];
+        if (has_v) vb = a.b_v[0][r];
+    }
+    ApplyArgs b = a;           // step_const's window is relative to lazy_t: shift it by one
+    b.lazy_t = a.lazy_t + 1;
+    catch_up<L>(b, lconst, lag, lsr, sub, p, m, v, pb, mb, vb);
+    L::store(const_cast<float *>(a.w_in[0]), r, D, sub, p);
+    if (adam) L::store(a.w_m[0], r, D, sub, m);
+    if (has_v) L::store(a.w_v[0], r, D, sub, v);
+    if (sub == 0) {
+        const_cast<float *>(a.b_in[0])[r] = pb;
+        if (adam) a.b_m[0][r] = mb;
+        if (has_v) a.b_v[0][r] = vb;
+        a.last_rel[r] = (int32_t)((int64_t)a.lazy_t - a.lazy_base);
     }
 }
 
@@ -864,7 +1023,7 @@ struct BackGrid {
     int32_t prep_first, xcd_map;
 };
 
-template <class L, int NT, bool SPEC = false, bool OWN = false>
+template <class L, int NT, bool SPEC = false, bool OWN = false, bool LAZY = false, bool LSPEC = false>
 __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
                                                         int64_t apply_blocks, MtGenArgs gen, BackGrid bg,
                                                         OwnerArgs own) {
@@ -910,10 +1069,25 @@ __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs 
         const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
         if (lane == 0) *a.loss_out = lv;
     }
-    if (k >= nr) return;
     const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item rows first, as mf_apply_kernel
     const int64_t ni = re > ia0 ? re - ia0 : 0;
     const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
+    if (LAZY) {
+        // a user row's decision words and the workgroup's constants window, loaded together
+        __shared__ float2 lconst[kConstWin];
+        LazyRow lzr{0, 0, 0};
+        if (k < nr && r < a.num_users) {
+            lzr.cnt = a.row_count[r];
+            lzr.mk = a.umark[r];
+            lzr.lsr = a.last_rel[r];
+        }
+        stage_consts(a, lconst);
+        lds_barrier();
+        if (k >= nr) return;
+        apply_row<L, kApplyPull, NT, false, SPEC, true, LSPEC>(a, r, sub, lzr, lconst);
+        return;
+    }
+    if (k >= nr) return;
     apply_row<L, kApplyPull, NT, false, SPEC>(a, r, sub);
 }
 
@@ -1422,6 +1596,7 @@ struct BackLaunchF {
     MtGenArgs gen;
     hipStream_t s;
     const OwnerArgs *own = nullptr;   // owner-sharded DP: the next step's owner prepare
+    bool lazy = false;                // lazy dense pass (rg_mf_apply_lazy)
     template <class L>
     int operator()() {
         const int64_t rows = a->row_end - a->row_begin;
@@ -1443,6 +1618,8 @@ struct BackLaunchF {
         // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
         // RG_APPLY_SPEC=0 turns it off)
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
+        // lazy pass: the optimizer state loaded before the row decision (RG_LAZY_SPEC=1)
+        static const int lazy_spec = [] { const char *e = getenv("RG_LAZY_SPEC"); return e ? atoi(e) : 0; }();
         const OwnerArgs oa = own ? *own : OwnerArgs{};
         LaunchEvents &le = launch_events();
         const hipEvent_t e0 = le.start, e1 = le.stop;
@@ -1454,6 +1631,8 @@ struct BackLaunchF {
                 hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         };
         if (own) go(mf_back_kernel<L, 0, true, true>);
+        else if (lazy && lazy_spec) go(mf_back_kernel<L, 0, true, false, true, true>);
+        else if (lazy) go(mf_back_kernel<L, 0, true, false, true>);
         else if (spec && nt == 1) go(mf_back_kernel<L, 1, true>);
         else if (spec && nt == 3) go(mf_back_kernel<L, 3, true>);
         else if (spec) go(mf_back_kernel<L, 0, true>);
@@ -1492,6 +1671,114 @@ extern "C" int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *t, rg
         prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
     BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
+}
+
+namespace {
+struct PairsPrepLaunchF {
+    PairsArgs *a, *prep;
+    int2 *prep_out;
+    int64_t prep_blocks;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        const int64_t nb = pairs_blocks<L>(a->cols);
+        const dim3 grid((unsigned)(nb + prep_blocks));
+        if (a->n_neg <= 5)
+            hipLaunchKernelGGL((mf_pairs_prep_kernel<L, 5>), grid, dim3(kPairBlock), 0, s, *a, *prep, prep_out, nb);
+        else
+            hipLaunchKernelGGL((mf_pairs_prep_kernel<L, kNMax>), grid, dim3(kPairBlock), 0, s, *a, *prep, prep_out, nb);
+        return check_launch("rg_mf_pairs_prepare");
+    }
+};
+
+struct FlushLaunchF {
+    ApplyArgs *a;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        const int64_t waves = (a->num_users + L::UPW - 1) / L::UPW;
+        const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+        hipLaunchKernelGGL((mf_lazy_flush_kernel<L>), dim3(nb < 1 ? 1 : nb), dim3(kBlock), 0, s, *a);
+        return check_launch("rg_mf_lazy_flush");
+    }
+};
+
+int lazy_args(const rg_mf_lazy_t *lz, const rg_opt_t *opt, ApplyArgs &a) {
+    if (!lz || !lz->last_rel) return fail_arg("lazy dense pass: null rg_mf_lazy_t / last_rel");
+    if (lz->step < 1 || lz->base < 0 || lz->base > lz->step || lz->step >= ((int64_t)1 << 31))
+        return fail_arg("lazy dense pass: bad step / base");
+    if (opt && opt->kind == RG_OPT_ADAM && (!lz->step_consts || lz->n_consts <= lz->step))
+        return fail_arg("lazy dense pass: Adam needs the per-step constants up to this step");
+    a.last_rel = lz->last_rel;
+    a.umark = lz->umark;
+    a.step_consts = reinterpret_cast<const float2 *>(lz->step_consts);
+    a.lazy_base = lz->base;
+    a.lazy_t = (int32_t)lz->step;
+    a.lazy_full = lz->full;
+    a.lazy_rows = reinterpret_cast<unsigned long long *>(lz->rows_done);
+    return RG_OK;
+}
+}  // namespace
+
+extern "C" int rg_mf_pairs_prepare(void *stream, const rg_mf_tables_t *t, const rg_mf_batch_t *b, rg_mf_work_t *w,
+                                   const rg_mf_batch_t *next, const rg_mf_work_t *next_w, int32_t *umark,
+                                   int32_t umark_step) {
+    if (!next) return rg_mf_pairs(stream, t, b, w, 1);
+    PairsArgs prep{};
+    int rc = prepare_args(next, next_w, nullptr, prep);
+    if (rc) return rc;
+    prep.umark = umark;
+    prep.umark_step = umark_step;
+    prep.num_users = t ? t->num_users : 0;
+    const int64_t total = prepare_threads(next->cols, next->n_neg);
+    if (b && b->loss == RG_LOSS_ADAPTIVE_HINGE) {   // several launches: the global max first
+        if ((rc = rg_mf_pairs(stream, t, b, w, 1))) return rc;
+        hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                           (hipStream_t)stream, prep, reinterpret_cast<int2 *>(next->pairs), 0);
+        return check_launch("rg_mf_pairs_prepare(prepare)");
+    }
+    if (kPairBlock != kBlock) return fail_arg("rg_mf_pairs_prepare: built with a pair-pass workgroup != 256 threads");
+    PairsArgs a;
+    if ((rc = pairs_args(t, b, w, 1, a))) return rc;
+    PairsPrepLaunchF f{&a, &prep, reinterpret_cast<int2 *>(next->pairs), (total + kBlock - 1) / kBlock,
+                       (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_apply_lazy(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                                const rg_mf_loss_t *loss, const rg_mf_lazy_t *lazy, const rg_mt_gen_t *gen) {
+    MtGenArgs g{};
+    if (gen && gen->nwords > 0) {
+        if (!gen->state || !gen->out) return fail_arg("rg_mf_apply_lazy: null MT state / output");
+        g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
+    }
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, 0, -1, loss, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    if ((rc = lazy_args(lazy, opt, a))) return rc;
+    if (!lazy->full && !lazy->umark) return fail_arg("rg_mf_apply_lazy: a partial pass needs the user marks");
+    PairsArgs prep{};
+    BackLaunchF f{&a, &prep, nullptr, 0, g, (hipStream_t)stream};
+    f.lazy = true;
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_lazy_flush(void *stream, const rg_mf_tables_t *t, const rg_opt_t *opt, const rg_mf_lazy_t *lazy) {
+    int rc = check_tables(t);
+    if (rc) return rc;
+    if (!opt || opt->kind < RG_OPT_ADAM || opt->kind > RG_OPT_RMSPROP) return fail_arg("rg_mf_lazy_flush: bad opt");
+    if (!t->user_w_out || !t->user_b_out) return fail_arg("rg_mf_lazy_flush: null other-set user tables");
+    ApplyArgs a{};
+    a.w_in[0] = t->user_w; a.b_in[0] = t->user_b; a.w_out[0] = t->user_w_out; a.b_out[0] = t->user_b_out;
+    a.w_m[0] = t->user_w_m; a.w_v[0] = t->user_w_v; a.b_m[0] = t->user_b_m; a.b_v[0] = t->user_b_v;
+    if (opt->kind == RG_OPT_ADAM && (!a.w_m[0] || !a.b_m[0])) return fail_arg("rg_mf_lazy_flush: Adam needs m");
+    if (opt->kind != RG_OPT_SGD && (!a.w_v[0] || !a.b_v[0])) return fail_arg("rg_mf_lazy_flush: needs v");
+    a.num_users = t->num_users; a.num_items = t->num_items; a.dim = t->dim;
+    a.opt = *opt;
+    a.has_bias = true;
+    if ((rc = lazy_args(lazy, opt, a))) return rc;
+    FlushLaunchF f{&a, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
 

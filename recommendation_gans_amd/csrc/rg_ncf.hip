@@ -956,6 +956,132 @@ extern "C" int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *b, rg_ncf_work
     return check_launch("rg_ncf_adapt_dp");
 }
 
+// ---- adaptive hinge over several ranks (each holds its column slice of ONE global draw) ----
+// The global maximum negative (torch.max over the flat draw: the largest score, the first
+// draw index j = k * global_cols + column on ties) is found in three small launches around
+// two float SUM all-reduces of the caller: each rank's (score, j) goes into its own slot of a
+// zeroed [world][4] buffer (one writer per slot, x + 0 = x: the sum is an all-gather), every
+// rank picks the same winner, and the active-positive count is summed before the winner's
+// rank sets its row's dp (spotlight/losses.py:133-172, implicit.py:194-199).
+__device__ __forceinline__ bool adapt_better(float s, int64_t j, float bs, int64_t bj) {
+    return s > bs || (s == bs && j < bj);
+}
+
+__device__ __forceinline__ int adapt_winner(const float *slots, int world) {
+    int w = 0;
+    float bs = slots[0];
+    int64_t bj = ((int64_t)slots[1] << 16) | (int64_t)slots[2];
+    for (int r = 1; r < world; ++r) {
+        const float sc = slots[4 * r];
+        const int64_t j = ((int64_t)slots[4 * r + 1] << 16) | (int64_t)slots[4 * r + 2];
+        if (adapt_better(sc, j, bs, bj)) { w = r; bs = sc; bj = j; }
+    }
+    return w;
+}
+
+__global__ __launch_bounds__(256) void ncf_adapt_local_kernel(const float *scores, int64_t rows, int tc, int NP,
+                                                             int64_t cols, const int32_t *perm, int64_t global_cols,
+                                                             int64_t col_offset, float *slots, int rank, int world,
+                                                             int32_t *local_row) {
+    __shared__ float ss[256];
+    __shared__ int64_t sj[256], sr[256];
+    const int tid = threadIdx.x;
+    float best = -1.0f;
+    int64_t bj = INT64_MAX, br = -1;
+    for (int64_t r = tid; r < rows; r += 256) {
+        const int64_t tile = r / kRows, rr = r % kRows;
+        const int q = (int)(rr / tc);
+        const int64_t s = tile * tc + rr % tc;
+        if (q >= 1 && q < NP && s < cols) {
+            const int64_t col = perm ? (int64_t)perm[s] : s;
+            const int64_t j = (int64_t)(q - 1) * global_cols + col_offset + col;
+            if (adapt_better(scores[r], j, best, bj)) { best = scores[r]; bj = j; br = r; }
+        }
+    }
+    ss[tid] = best; sj[tid] = bj; sr[tid] = br;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w && adapt_better(ss[tid + w], sj[tid + w], ss[tid], sj[tid])) {
+            ss[tid] = ss[tid + w]; sj[tid] = sj[tid + w]; sr[tid] = sr[tid + w];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        for (int i = 0; i < 4 * world; ++i) slots[i] = 0.0f;
+        const int64_t j = sj[0] == INT64_MAX ? 0 : sj[0];
+        slots[4 * rank] = ss[0];
+        slots[4 * rank + 1] = (float)(j >> 16);
+        slots[4 * rank + 2] = (float)(j & 0xffff);
+        local_row[0] = (int32_t)sr[0];
+    }
+}
+
+__global__ __launch_bounds__(256) void ncf_adapt_global_kernel(const float *scores, float *dp, int64_t rows, int tc,
+                                                              int64_t n_pos_cols, float n_a, const float *slots,
+                                                              int world, float *count, float *loss_partial) {
+    __shared__ float scnt[256], sloss[256];
+    const int tid = threadIdx.x;
+    const float mx = slots[4 * adapt_winner(slots, world)];
+    float cnt = 0.0f, ls = 0.0f;
+    for (int64_t r = tid; r < rows; r += 256) {
+        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t s = tile * tc + rr % tc;
+        dp[r] = 0.0f;
+        if (rr < (int64_t)tc && s < n_pos_cols) {
+            const float x = (mx - scores[r]) + 1.0f;
+            ls += fmaxf(x, 0.0f);
+            if (x >= 0.0f) { dp[r] = -(1.0f / n_a); cnt += 1.0f; }
+        }
+    }
+    scnt[tid] = cnt;
+    sloss[tid] = ls;
+    __syncthreads();
+    if (tid == 0) {
+        float c = 0.0f, l = 0.0f;
+        for (int i = 0; i < 256; ++i) { c += scnt[i]; l += sloss[i]; }
+        count[0] = c;
+        loss_partial[0] = l;
+        loss_partial[1] = 0.0f;
+    }
+}
+
+__global__ void ncf_adapt_winner_kernel(float *dp, const float *slots, int world, int rank, const int32_t *local_row,
+                                        const float *count, float n_a) {
+    if (threadIdx.x == 0 && adapt_winner(slots, world) == rank && local_row[0] >= 0)
+        dp[local_row[0]] = count[0] * (1.0f / n_a);
+}
+
+extern "C" int rg_ncf_adapt_local(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w, rg_ncf_work_t *nw,
+                                  float *slots, int32_t rank, int32_t world, int32_t *local_row) {
+    if (!b || !w || !nw || !nw->scores || !slots || !local_row || world < 1 || rank < 0 || rank >= world)
+        return fail_arg("rg_ncf_adapt_local: bad argument");
+    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    hipLaunchKernelGGL(ncf_adapt_local_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, tiles * kRows,
+                       (int)rg_ncf_cols_per_tile(b->n_neg), b->n_neg + 1, b->cols, w->plan_perm, b->global_cols,
+                       b->col_offset, slots, rank, world, local_row);
+    return check_launch("rg_ncf_adapt_local");
+}
+
+extern "C" int rg_ncf_adapt_global(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, const float *slots,
+                                   int32_t world, float *count, float *loss_partials) {
+    if (!b || !nw || !nw->scores || !nw->dp || !slots || !count || !loss_partials || world < 1)
+        return fail_arg("rg_ncf_adapt_global: bad argument");
+    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    hipLaunchKernelGGL(ncf_adapt_global_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, nw->dp,
+                       tiles * kRows, (int)rg_ncf_cols_per_tile(b->n_neg), b->n_pos, (float)b->global_pos, slots,
+                       world, count, loss_partials);
+    return check_launch("rg_ncf_adapt_global");
+}
+
+extern "C" int rg_ncf_adapt_winner(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, const float *slots,
+                                   int32_t world, int32_t rank, const int32_t *local_row, const float *count) {
+    if (!b || !nw || !nw->dp || !slots || !local_row || !count || world < 1 || rank < 0 || rank >= world)
+        return fail_arg("rg_ncf_adapt_winner: bad argument");
+    hipLaunchKernelGGL(ncf_adapt_winner_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, nw->dp, slots, world, rank,
+                       local_row, count, (float)b->global_pos);
+    return check_launch("rg_ncf_adapt_winner");
+}
+
 extern "C" int rg_ncf_update(void *stream, const rg_ncf_model_t *m, const rg_ncf_work_t *nw, int64_t nparts,
                              const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss) {
     if (!m || !nw || !opt || !nw->mlp_partials || !m->mlp) return fail_arg("rg_ncf_update: null argument");

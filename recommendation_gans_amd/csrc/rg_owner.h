@@ -70,6 +70,9 @@ __device__ __forceinline__ void owner_prepare_block(const OwnerArgs &a, int64_t 
     for (int64_t i = b * z + tid; i < z1; i += kOwnSeg) a.scores[i] = 0.0f;
 }
 
+// adaptive hinge: the score buffer's extra slots after the exchanged (1 + n) * GC scores
+__device__ __forceinline__ int64_t adapt_slot(const OwnerArgs &a) { return (int64_t)(1 + a.n_neg) * a.gc; }
+
 // host: validated device view of a batch (rg_owner.hip)
 int owner_args(const rg_mf_owner_batch_t *b, OwnerArgs &a);
 // rg_mf_apply_prepare with the NEXT step's owner prepare in the extra workgroups (rg_mf.hip)

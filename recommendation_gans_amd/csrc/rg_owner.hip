@@ -129,7 +129,11 @@ __global__ __launch_bounds__(kBlk) void owner_back_kernel(OwnerArgs a, OwnTables
         L::load(ur, t.user_w, lu, D, sub);          // the planned item-side partial: dz * user row
         const float p0 = a.scores[c];
         float dp0 = 0.0f;
-        if (pairwise) {
+        if (a.loss == RG_LOSS_ADAPTIVE_HINGE) {   // hinge against the global max negative (owner_adapt_kernel)
+            const float x = (a.scores[adapt_slot(a)] - p0) + 1.0f;
+            la = fmaxf(x, 0.0f);
+            if (x >= 0.0f) dp0 = -(1.0f / a.n_a);
+        } else if (pairwise) {
 #pragma unroll
             for (int k = 0; k < NMAX; ++k) {
                 if (k < n) {
@@ -190,7 +194,12 @@ __global__ __launch_bounds__(kBlk) void owner_back_kernel(OwnerArgs a, OwnTables
             const int lu = r.y, i = r.z;
             const float pk = a.scores[gp];
             float dpk;
-            if (pairwise) {
+            if (a.loss == RG_LOSS_ADAPTIVE_HINGE) {
+                // only the global max negative has a gradient: the active positives' count / B
+                const float *ex = a.scores + adapt_slot(a);
+                if (gp != (int64_t)__float_as_int(ex[1])) continue;
+                dpk = ex[2] * (1.0f / a.n_a);
+            } else if (pairwise) {
                 const float p0 = a.scores[c];
                 if (a.loss == RG_LOSS_BPR) {
                     const float sg = sigmoidf_ref(p0 - pk);
@@ -227,6 +236,55 @@ __global__ __launch_bounds__(kBlk) void owner_back_kernel(OwnerArgs a, OwnTables
 
 __global__ __launch_bounds__(kBlk) void owner_prepare_kernel(OwnerArgs a) { owner_prepare_block(a, blockIdx.x); }
 
+// Adaptive hinge (implicit.py:194-199 'bpr' / 'adaptive_hinge', spotlight/losses.py:133-172)
+// on the owner layout: after the exchange every rank holds every score, so each finds the
+// global max negative (largest score, first draw on ties -- torch.max over the flat draw) and
+// the count of active positives itself, identically, with no further exchange; stored in
+// the score buffer's extra slots [(1 + n) * GC + {0, 1, 2}] = (max, its pair index gp, count)
+__device__ __forceinline__ void block_max_first(float &v, int64_t &i, float *sv, int64_t *si) {
+    const int tid = threadIdx.x;
+    sv[tid] = v;
+    si[tid] = i;
+    __syncthreads();
+    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+        if (tid < w && (sv[tid + w] > sv[tid] || (sv[tid + w] == sv[tid] && si[tid + w] < si[tid]))) {
+            sv[tid] = sv[tid + w];
+            si[tid] = si[tid + w];
+        }
+        __syncthreads();
+    }
+    v = sv[0];
+    i = si[0];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void owner_adapt_kernel(OwnerArgs a) {
+    __shared__ float sv[1024];
+    __shared__ int64_t si[1024];
+    const int64_t gc = a.gc, end = (int64_t)(1 + a.n_neg) * gc;
+    float best = -1.0f;
+    int64_t bi = INT64_MAX;
+    for (int64_t g = gc + threadIdx.x; g < end; g += 1024) {
+        const float v = a.scores[g];
+        if (v > best) { best = v; bi = g; }
+    }
+    block_max_first(best, bi, sv, si);
+    float cnt = 0.0f;
+    for (int64_t c = threadIdx.x; c < a.n_pos; c += 1024) cnt += ((best - a.scores[c]) + 1.0f >= 0.0f) ? 1.0f : 0.0f;
+    sv[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sv[threadIdx.x] += sv[threadIdx.x + w];   // integers: exact in any order
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float *ex = a.scores + end;
+        ex[0] = best;
+        ex[1] = __int_as_float((int)bi);
+        ex[2] = sv[0];
+    }
+}
+
 // run_val_iteration's loss (implicit.py:366-379) from the exchanged score vector: every
 // rank holds every score, so each computes the whole loss (one workgroup, fixed order,
 // double accumulators) -- identical on every rank
@@ -236,10 +294,23 @@ __global__ __launch_bounds__(1024) void owner_loss_kernel(OwnerArgs a, double in
     const int n = a.n_neg;
     const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
     double sa = 0.0, sb = 0.0;
+    float mx = 0.0f;
+    if (a.loss == RG_LOSS_ADAPTIVE_HINGE) {
+        __shared__ float sv[1024];
+        __shared__ int64_t si[1024];
+        float best = -1.0f;
+        int64_t bi = INT64_MAX;
+        for (int64_t g = gc + threadIdx.x; g < (int64_t)(1 + n) * gc; g += 1024)
+            if (a.scores[g] > best) { best = a.scores[g]; bi = g; }
+        block_max_first(best, bi, sv, si);
+        mx = best;
+    }
     for (int64_t c = threadIdx.x; c < gc; c += 1024) {
         const bool has = c < a.n_pos;
         const float p0 = a.scores[c];
-        if (pairwise) {
+        if (a.loss == RG_LOSS_ADAPTIVE_HINGE) {
+            if (has) sa += (double)fmaxf((mx - p0) + 1.0f, 0.0f);
+        } else if (pairwise) {
             if (!has) continue;
             for (int k = 0; k < n; ++k) {
                 const float pk = a.scores[(1 + k) * gc + c];
@@ -330,7 +401,7 @@ int owner_args(const rg_mf_owner_batch_t *b, OwnerArgs &a) {
     if (b->n_planned < 0 || b->n_planned > b->n_pos) return fail_arg("rg_mf_owner: bad n_planned");
     if (b->n_planned > 0 && (!b->plan_perm || !b->plan_pos_slot || !b->pos_user || !b->pos_item))
         return fail_arg("rg_mf_owner: null positives / plan");
-    if (b->loss < 0 || b->loss > RG_LOSS_HINGE) return fail_arg("rg_mf_owner: loss must be pointwise, bpr or hinge");
+    if (b->loss < 0 || b->loss > RG_LOSS_ADAPTIVE_HINGE) return fail_arg("rg_mf_owner: bad loss kind");
     if (b->loss != RG_LOSS_POINTWISE && b->n_pos <= 0) return fail_arg("rg_mf_owner: empty global batch");
     if (!b->words || !b->pool || b->pool_len <= 0) return fail_arg("rg_mf_owner: no words / empty pool");
     if (!b->neg_rec || !b->seg_count || !b->scores) return fail_arg("rg_mf_owner: null records / counts / scores");
@@ -348,6 +419,9 @@ int owner_args(const rg_mf_owner_batch_t *b, OwnerArgs &a) {
     if (b->loss == RG_LOSS_POINTWISE) {
         a.n_a = (float)(b->n_pos > 0 ? b->n_pos : 1);
         a.n_b = (float)((int64_t)b->n_neg * b->global_cols);
+    } else if (b->loss == RG_LOSS_ADAPTIVE_HINGE) {
+        a.n_a = (float)b->n_pos;
+        a.n_b = 1.0f;
     } else {
         a.n_a = (float)((int64_t)b->n_neg * b->n_pos);
         a.n_b = 1.0f;
@@ -394,10 +468,19 @@ extern "C" int rg_mf_owner_loss(void *stream, const rg_mf_owner_batch_t *b, floa
     if (rc) return rc;
     if (!loss_out) return fail_arg("rg_mf_owner_loss: null output");
     const double gp = (double)(b->n_pos > 0 ? b->n_pos : 1), n = (double)b->n_neg;
-    const double inv_a = b->loss == RG_LOSS_POINTWISE ? 1.0 / gp : 1.0 / (n * gp);
+    const double inv_a = (b->loss == RG_LOSS_POINTWISE || b->loss == RG_LOSS_ADAPTIVE_HINGE) ? 1.0 / gp : 1.0 / (n * gp);
     const double inv_b = b->loss == RG_LOSS_POINTWISE ? 1.0 / (n * (double)b->global_cols) : 0.0;
     hipLaunchKernelGGL(owner_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, inv_a, inv_b, loss_out);
     return check_launch("rg_mf_owner_loss");
+}
+
+extern "C" int rg_mf_owner_adapt(void *stream, const rg_mf_owner_batch_t *b) {
+    OwnerArgs a;
+    int rc = owner_args(b, a);
+    if (rc) return rc;
+    if (b->loss != RG_LOSS_ADAPTIVE_HINGE) return fail_arg("rg_mf_owner_adapt: adaptive hinge only");
+    hipLaunchKernelGGL(owner_adapt_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+    return check_launch("rg_mf_owner_adapt");
 }
 
 extern "C" int rg_mf_owner_scores(void *stream, const rg_mf_tables_t *t, const rg_mf_owner_batch_t *b) {

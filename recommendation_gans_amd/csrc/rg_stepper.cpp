@@ -105,6 +105,16 @@ struct Stepper {
     int64_t own_unit = -1;
     int own_stage = 0;                    // 0 idle, 1 after begin, 2 after mid
     hipEvent_t own_back = nullptr;        // after the owner backward (the item gradient may start)
+    // lazy dense pass (single-rank split step): deferred cold user-row updates
+    bool lazy = false;
+    bool lazy_pending = false;            // some user rows lag the current step
+    int64_t lazy_base = 0;                // absolute step of last_rel == 0
+    int32_t *last_rel = nullptr;          // [U]
+    int32_t *umark = nullptr;             // [U]
+    float *consts = nullptr;              // [2 * n_consts] Adam constants per absolute step
+    int64_t n_consts = 0;
+    uint64_t *rows_done = nullptr;        // diagnostic counter (rg_mf_stepper_lazy_count)
+    bool count_rows = false;
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -315,10 +325,14 @@ int release(Stepper &st, hipStream_t stream) {
     return st.inline_gen ? RG_OK : keep_ahead(st, st.taken);
 }
 
+int lazy_flush(Stepper &st, hipStream_t s);
+
 // words + pairs of unit `taken` for `in`, visible to `stream` (split-step consumers)
 int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t *unit_out) {
     const int64_t unit = st.taken;
-    int rc = keep_ahead(st, unit);
+    int rc = lazy_flush(st, stream);      // external consumers read every row
+    if (rc) return rc;
+    rc = keep_ahead(st, unit);
     if (rc) return rc;
     if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, in))) {
         if ((rc = prepare_side(st, stream, unit, in))) return rc;
@@ -356,6 +370,56 @@ rg_opt_t opt_at(const Stepper &st, int64_t t) {
         o.bias_correction2_sqrt = (float)std::pow(bc2, 0.5);
     }
     return o;
+}
+
+// Adam constants of every absolute step < upto on the device (grown by doubling; the
+// copy is synchronous and happens O(log steps) times in a run)
+int ensure_consts(Stepper &st, int64_t upto) {
+    if (upto < st.n_consts) return RG_OK;
+    int64_t cap = st.n_consts > 0 ? st.n_consts : 4096;
+    while (cap <= upto) cap *= 2;
+    float *host = static_cast<float *>(std::malloc((size_t)cap * 2 * sizeof(float)));
+    if (!host) { rg::set_error("stepper: out of host memory"); return RG_E_LAUNCH; }
+    for (int64_t s = 0; s < cap; ++s) {
+        const rg_opt_t o = opt_at(st, s > 0 ? s : 1);
+        host[2 * s] = o.step_size;
+        host[2 * s + 1] = o.bias_correction2_sqrt;
+    }
+    float *dev = nullptr;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMalloc(&dev, (size_t)cap * 2 * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(dev, host, (size_t)cap * 2 * sizeof(float), hipMemcpyHostToDevice);
+    std::free(host);
+    if (e != hipSuccess) return hip_fail("stepper: step constants", e);
+    if (st.consts) (void)hipFree(st.consts);
+    st.consts = dev;
+    st.n_consts = cap;
+    return RG_OK;
+}
+
+rg_mf_lazy_t lazy_of(const Stepper &st, int64_t step, bool full) {
+    rg_mf_lazy_t l{};
+    l.last_rel = st.last_rel;
+    l.umark = st.umark;
+    l.step_consts = st.consts;
+    l.n_consts = st.n_consts;
+    l.base = st.lazy_base;
+    l.step = step;
+    l.full = full ? 1 : 0;
+    l.rows_done = st.count_rows ? st.rows_done : nullptr;
+    return l;
+}
+
+// every user row up to the current step, into the current set (no-op when none lags)
+int lazy_flush(Stepper &st, hipStream_t s) {
+    if (!st.lazy || !st.lazy_pending) return RG_OK;
+    int rc = ensure_consts(st, st.cfg.step + 1);
+    if (rc) return rc;
+    const rg_opt_t o = opt_at(st, st.cfg.step > 0 ? st.cfg.step : 1);
+    const rg_mf_lazy_t l = lazy_of(st, st.cfg.step, true);
+    if ((rc = rg_mf_lazy_flush(s, &st.cfg.tables[st.set], &o, &l))) return rc;
+    st.lazy_pending = false;
+    return RG_OK;
 }
 
 bool env_flag(const char *name, bool dflt) {
@@ -441,6 +505,83 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         st.prep_in = *next;
         st.prep_serial = 0;
     }
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
+// Lazy split step (single rank):
+//   main  rg_mf_pairs_prepare (this step's pairs + the NEXT step's prepare, which marks the
+//         users that step reads) -> rg_mf_apply_lazy (items, and the users with a gradient
+//         or a mark; a full pass when no next step is known; + the inline MT walk)
+// Every row a kernel reads is current; rows nobody reads lag until rg_mf_stepper_flush /
+// the next full pass / an external consumer (acquire) catches them up.
+int train_lazy(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+               float *loss_out, void *ev0, void *ev1) {
+    const int64_t unit = st.taken;
+    int rc = st.inline_gen ? generate_upto(st, unit + 1, 0) : keep_ahead(st, unit);
+    if (rc) return rc;
+    rg_mf_work_t w = work_for(st, cur);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if ((rc = wait_side(st, s, (int)(unit % 2)))) return rc;
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
+        // the pairs were not prepared (with marks) by the previous lazy step: bring every row
+        // up to date first, so whatever this step reads is current
+        if ((rc = lazy_flush(st, s))) return rc;
+        if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+        st.prepared = true;
+        st.prep_unit = unit;
+        st.prep_in = cur;
+        st.prep_serial = 0;
+    }
+    if (!st.lazy_pending) {                    // every row current at cfg.step: restart the clock
+        hipError_t e = hipMemsetAsync(st.last_rel, 0, (size_t)st.cfg.tables[0].num_users * sizeof(int32_t), s);
+        if (e != hipSuccess) return hip_fail("stepper: reset last_rel", e);
+        st.lazy_base = st.cfg.step;
+    }
+    if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = wait_words(st, s, unit))) return rc;
+    const int64_t t = st.cfg.step + 1;
+    if ((rc = ensure_consts(st, t + 1))) return rc;
+    rg_mf_batch_t nbatch{};
+    rg_mf_work_t nw{};
+    if (next) {
+        if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
+        if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        nbatch = make_batch(st, *next, unit + 1);
+        nw = work_for(st, *next);
+    }
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    if ((rc = rg_mf_pairs_prepare(s, tb, &batch, &w, next ? &nbatch : nullptr, next ? &nw : nullptr, st.umark,
+                                  (int32_t)(t + 1))))
+        return rc;
+    if ((rc = release(st, s))) return rc;
+    rg_mt_gen_t gen{};
+    int gen_slot = -1;
+    if (st.inline_gen && st.gen_slots == rel_slot(st, unit + 2)) {
+        gen_slot = (int)(st.gen_slots % kSlots);
+        if ((rc = begin_production(st, s, gen_slot))) return rc;
+        gen.state = st.cfg.mt_state;
+        gen.out = st.words[gen_slot];
+        gen.state_before = st.start_state[gen_slot];
+        gen.nwords = st.G * st.W;
+    }
+    st.cfg.step = t;
+    const rg_opt_t o = opt_at(st, t);
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+    const rg_mf_lazy_t lz = lazy_of(st, t, next == nullptr);
+    rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};
+    rc = rg_mf_apply_lazy(s, tb, &w, &o, &l, &lz, gen_slot >= 0 ? &gen : nullptr);
+    rg::launch_events() = rg::LaunchEvents{};
+    if (rc) return rc;
+    if (gen_slot >= 0) end_production(st, s, gen_slot);
+    if (next) {
+        st.prepared = true;
+        st.prep_unit = unit + 1;
+        st.prep_in = *next;
+        st.prep_serial = 0;
+    }
+    st.lazy_pending = next != nullptr;
     st.set = 1 - st.set;
     return RG_OK;
 }
@@ -577,7 +718,9 @@ int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stre
     const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
     rg_mf_work_t w = work_for(st, st.own_in);
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
-    int rc = rg_mf_owner_back(s, tb, &b, &w);
+    int rc = RG_OK;
+    if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = rg_mf_owner_adapt(s, &b))) return rc;   // global max, count
+    rc = rg_mf_owner_back(s, tb, &b, &w);
     if (rc) return rc;
     if (grad_stream && grad_stream != s) {
         hipError_t e = hipSuccess;
@@ -743,6 +886,10 @@ void destroy(Stepper *st) {
         if (st->stamp[i]) hipFree(st->stamp[i]);
     }
     if (st->mark) hipEventDestroy(st->mark);
+    if (st->last_rel) hipFree(st->last_rel);
+    if (st->umark) hipFree(st->umark);
+    if (st->consts) hipFree(st->consts);
+    if (st->rows_done) hipFree(st->rows_done);
     if (st->own_back) hipEventDestroy(st->own_back);
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
@@ -761,8 +908,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     if (cfg->dp_mode == 2) {
         const int64_t segs = rg_mf_owner_segments(cfg->global_cols, cfg->n_neg);
         if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world || !cfg->item_grad ||
-            cfg->cols != cfg->global_cols || cfg->col_offset != 0 || segs <= 0 ||
-            cfg->loss == RG_LOSS_ADAPTIVE_HINGE || !cfg->owner_rec[0] || !cfg->owner_rec[1] ||
+            cfg->cols != cfg->global_cols || cfg->col_offset != 0 || segs <= 0 || !cfg->owner_rec[0] || !cfg->owner_rec[1] ||
             !cfg->owner_seg[0] || !cfg->owner_seg[1] || !cfg->owner_scores[0] || !cfg->owner_scores[1]) {
             rg::set_error("rg_mf_stepper_create: inconsistent owner-sharded data-parallel configuration");
             return nullptr;
@@ -834,6 +980,24 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         return nullptr;
     }
     st->cp_pos = (int32_t)pos;
+    // lazy dense pass: the single-rank split step (RG_LAZY=0: the eager pass, for A/B runs)
+    st->lazy = env_flag("RG_LAZY", true) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
+    if (st->lazy) {
+        const size_t ub = (size_t)cfg->tables[0].num_users * sizeof(int32_t);
+        e = hipMalloc(&st->last_rel, ub);
+        if (e == hipSuccess) e = hipMalloc(&st->umark, ub);
+        if (e == hipSuccess) e = hipMemset(st->umark, 0, ub);
+        if (e == hipSuccess) e = hipMemset(st->last_rel, 0, ub);
+        if (e == hipSuccess) e = hipMalloc(&st->rows_done, sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemset(st->rows_done, 0, sizeof(uint64_t));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            hip_fail("rg_mf_stepper_create: lazy state", e);
+            destroy(st);
+            return nullptr;
+        }
+        st->lazy_base = cfg->step;
+    }
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
     if (env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
@@ -863,6 +1027,7 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
     }
     if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
         return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+    if (st->lazy) return train_lazy(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     return train_split(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
 }
 
@@ -991,6 +1156,7 @@ extern "C" int rg_mf_stepper_state(void *h, int32_t *current_set, int64_t *step)
 extern "C" int rg_mf_stepper_advance(void *h, int32_t flip_sets, int64_t steps) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st) return rg::fail_arg("rg_mf_stepper_advance: null handle");
+    if (st->lazy_pending) return rg::fail_arg("rg_mf_stepper_advance: lazy rows pending (rg_mf_stepper_flush first)");
     if (flip_sets) st->set = 1 - st->set;
     st->cfg.step += steps;
     return RG_OK;
@@ -1031,4 +1197,26 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
     e = hipMemcpy(st->cfg.mt_state, host_state, 625 * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail("stepper: copy MT state", e);
     return RG_OK;
+}
+
+extern "C" int rg_mf_stepper_flush(void *h, void *stream) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_flush: null handle");
+    return lazy_flush(*st, (hipStream_t)stream);
+}
+
+extern "C" int rg_mf_stepper_lazy_count(void *h, int32_t enable, uint64_t *rows_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_lazy_count: null handle");
+    if (rows_out) {
+        *rows_out = 0;
+        if (st->rows_done) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipMemcpy(rows_out, st->rows_done, sizeof(uint64_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemset(st->rows_done, 0, sizeof(uint64_t));
+            if (e != hipSuccess) return hip_fail("rg_mf_stepper_lazy_count", e);
+        }
+    }
+    st->count_rows = enable != 0 && st->rows_done != nullptr;
+    return st->lazy ? 1 : 0;
 }

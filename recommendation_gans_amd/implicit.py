@@ -130,6 +130,14 @@ class ImplicitFactorizationModel:
         common = dict(loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
                       betas=o.get("betas", (0.9, 0.999)), eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
                       n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
+        ncf_dp = {}
+        if self._world > 1:
+            import torch.distributed as dist
+            comm = None
+            if dist.get_backend() == "nccl":           # RCCL: the exchanges run inside the native step
+                from .comm import RcclComm
+                comm = RcclComm(dev)
+            ncf_dp = dict(rank=self._rank, world_size=self._world, comm=comm)
         if hasattr(net, "embedding_user_mlp") and hasattr(net, "affine_output"):   # NeuMF (neuMF.py:7-55)
             self._kind = "ncf"
             self._params = [net.embedding_user_mlp.weight, net.embedding_item_mlp.weight,
@@ -140,7 +148,7 @@ class ImplicitFactorizationModel:
             w = [p.detach() for p in self._params]
             self._engine = NCFEngine(w[0], w[1], w[4:], self._pool.user_ids, self._pool.item_ids, _mtstate.current(),
                                      seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), mf_user_w=w[2],
-                                     mf_item_w=w[3], **common)
+                                     mf_item_w=w[3], **common, **ncf_dp)
         elif hasattr(net, "embedding_user") and hasattr(net, "layers"):          # NCF MLP (mlp.py:5-46)
             self._kind = "ncf"
             self._params = [net.embedding_user.weight, net.embedding_item.weight]
@@ -150,7 +158,7 @@ class ImplicitFactorizationModel:
             self._engine = NCFEngine(self._params[0].detach(), self._params[1].detach(),
                                      [p.detach() for p in self._params[2:]], self._pool.user_ids,
                                      self._pool.item_ids, _mtstate.current(),
-                                     seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), **common)
+                                     seed=int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), **common, **ncf_dp)
         elif hasattr(net, "user_embeddings") and hasattr(net, "item_biases"):   # BilinearNet
             self._kind = "mf"
             self._params = [net.user_embeddings.weight, net.item_embeddings.weight, net.user_biases.weight,
@@ -159,18 +167,11 @@ class ImplicitFactorizationModel:
             w = [p.detach() for p in self._params]
             dp = {}
             if self._world > 1:
-                import torch.distributed as dist
-                comm = None
-                if dist.get_backend() == "nccl":       # RCCL: the exchanges run inside the native step
-                    from .comm import RcclComm
-                    comm = RcclComm(dev)
-                dp = dict(rank=self._rank, world_size=self._world, dp="owner", comm=comm)
+                dp = dict(rank=self._rank, world_size=self._world, dp="owner", comm=ncf_dp["comm"])
             self._engine = MFEngine(w[0], w[1], w[2].reshape(-1), w[3].reshape(-1), self._pool.user_ids,
                                     self._pool.item_ids, _mtstate.current(), **common, **dp)
         else:
             raise NotImplementedError("the fused steps train BilinearNet, the NCF MLP and NeuMF representations")
-        if self._world > 1 and self._kind != "mf":
-            raise NotImplementedError("world_size > 1: data-parallel training is implemented for BilinearNet")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
@@ -197,10 +198,12 @@ class ImplicitFactorizationModel:
             self._initialize(train_set)
         self._check_input(train_set.user_ids, train_set.item_ids)
         e, dev = self._engine, self._engine.device
-        B = self._batch_size * self._world         # the global batch (one process at world * batch_size)
-        owner = self._world > 1
+        b = self._batch_size
+        B = b * self._world                        # the global batch (one process at world * batch_size)
+        R, r = self._world, self._rank
+        owner = R > 1 and self._kind == "mf"       # MF: owner-sharded; NCF / NeuMF: replicated columns
         allreduce = None
-        if owner and e.comm is None:               # gloo process group: exchanges through torch.distributed
+        if R > 1 and e.comm is None:               # gloo process group: exchanges through torch.distributed
             import torch.distributed as dist
             allreduce = dist.all_reduce
         e.set_mt_state(_mtstate.current())
@@ -213,8 +216,17 @@ class ImplicitFactorizationModel:
         total = {"train_loss": [], "validation_loss": [], "curr_epoch": []}
         # the batches repeat every epoch (one shuffle): plans (and MF step inputs) are built once
         # (one launch builds every batch's plan, rg_mf_plans_build)
-        plans = e.make_plans(ti, users=tu) if owner else e.make_plans(ti)
+        if owner:
+            plans = e.make_plans(ti, users=tu)
+        elif R > 1:                                # this rank's columns [r*b, (r+1)*b) of each global batch
+            plans = e.make_plans(ti, offset=r * b, stride=B)
+        else:
+            plans = e.make_plans(ti)
         vplans = e.make_plans(vi, users=vu) if owner else None
+
+        def cols(x, s):                            # this rank's columns of global batch s (NCF / NeuMF)
+            lo = min(s * B + r * b, len(x))
+            return x[lo:min(lo + b, (s + 1) * B, len(x))]
         if self._kind == "mf":
             inputs = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
         for epoch in range(self._n_iter):
@@ -225,10 +237,9 @@ class ImplicitFactorizationModel:
                 elif self._kind == "mf":
                     e.train_step_in(inputs[s], nxt, loss_out=losses[s:s + 1])
                 else:
-                    nxt = (tu[(s + 1) * B:(s + 2) * B], ti[(s + 1) * B:(s + 2) * B], plans[s + 1]) \
-                        if s + 1 < nb else None
-                    e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s],
-                                 loss_out=losses[s:s + 1], next_step=nxt)
+                    nxt = (cols(tu, s + 1), cols(ti, s + 1), plans[s + 1]) if s + 1 < nb else None
+                    e.train_step(cols(tu, s), cols(ti, s), global_pos=min(B, len(tu) - s * B), plan=plans[s],
+                                 loss_out=losses[s:s + 1], next_step=nxt, allreduce=allreduce)
             tl = [float(x) for x in losses.cpu().numpy()]          # loss.item() per batch
             train_epoch_loss = sum(tl) / nb
             if np.isnan(train_epoch_loss) or train_epoch_loss == 0.0:
@@ -236,6 +247,9 @@ class ImplicitFactorizationModel:
             if owner:
                 vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B], plan=vplans[s // B], allreduce=allreduce)[0])
                       for s in range(0, len(vu), B)]
+            elif R > 1:
+                vl = [float(e.val_loss(cols(vu, s), cols(vi, s), global_pos=min(B, len(vu) - s * B),
+                                       allreduce=allreduce)[0]) for s in range(-(-len(vu) // B))]
             else:
                 vl = [float(e.val_loss(vu[s:s + B], vi[s:s + B])[0]) for s in range(0, len(vu), B)]
             valid_epoch_loss = sum(vl) / len(vl)

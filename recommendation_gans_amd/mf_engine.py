@@ -204,8 +204,8 @@ class MFEngine:
         dp = dp or ("owner" if world_size > 1 or comm is not None else None)
         if dp not in (None, "user_shard", "global_stream", "owner"):
             raise ValueError(f"unknown data-parallel layout {dp!r}")
-        if loss == "adaptive_hinge" and (world_size != 1 or dp is not None):
-            raise NotImplementedError("adaptive_hinge is implemented for the single-rank step")
+        if loss == "adaptive_hinge" and dp in ("global_stream", "user_shard"):
+            raise NotImplementedError("adaptive_hinge over several ranks runs on the owner-sharded layout (dp='owner')")
         self.U_global = int(user_w.shape[0])
         if dp == "owner":
             user_w = user_w[rank::world_size]
@@ -301,7 +301,9 @@ class MFEngine:
             ns = int(self.lib.rg_mf_owner_segments(self.global_cols, self.n_neg))
             self.owner_rec = [torch.zeros(4 * rl, dtype=torch.int32, device=dev) for _ in range(2)]
             self.owner_seg = [torch.zeros(ns, dtype=torch.int32, device=dev) for _ in range(2)]
-            self.owner_scores = [torch.zeros((1 + self.n_neg) * self.global_cols, **f32) for _ in range(2)]
+            # adaptive hinge: 4 extra slots after the exchanged scores (rg_mf_owner_adapt)
+            extra = 4 if loss == "adaptive_hinge" else 0
+            self.owner_scores = [torch.zeros((1 + self.n_neg) * self.global_cols + extra, **f32) for _ in range(2)]
         self.chunk = 0
         if dp == "global_stream":
             self.chunk = int(self.lib.rg_mf_grad_chunk(self.shard_users, self.shard_items, self.dim))
@@ -386,8 +388,22 @@ class MFEngine:
     def t(self):
         return self._state()[1]
 
+    def flush(self):
+        """Lazy split step: bring every deferred user row up to the current step
+        (rg_mf_stepper_flush, on the current stream; a no-op when no row lags)."""
+        check(self.lib.rg_mf_stepper_flush(self._stepper, _lib.stream_handle()), "rg_mf_stepper_flush")
+
+    def lazy_rows(self, enable=False):
+        """Diagnostics of the lazy pass: user rows processed since the last call (synchronises);
+        ``enable`` switches the (contended) device counter on for the following steps.
+        Returns None when the stepper runs the eager pass."""
+        n = ctypes.c_uint64()
+        lazy = self.lib.rg_mf_stepper_lazy_count(self._stepper, int(bool(enable)), ctypes.byref(n))
+        return int(n.value) if lazy == 1 else None
+
     def params(self):
-        """Current (user_w, item_w, user_b, item_b) device tensors."""
+        """Current (user_w, item_w, user_b, item_b) device tensors (deferred rows flushed)."""
+        self.flush()
         return self.tabs[self.cur]
 
     def loss_scales(self, global_pos):
@@ -662,14 +678,14 @@ class MFEngine:
         users = users.to(self.device, torch.int64).contiguous()
         items = items.to(self.device, torch.int64).contiguous()
         out = torch.empty(users.numel(), dtype=torch.float32, device=self.device)
-        U, I, ub, ib = self.params()
+        U, I, ub, ib = self.params()      # flushes deferred rows
         check(self.lib.rg_mf_scores(_lib.stream_handle(), ptr(U), ptr(I), ptr(ub), ptr(ib), self.dim,
                                     ptr(users), ptr(items), users.numel(), ptr(out)), "rg_mf_scores")
         return out
 
     def set_params(self, user_w, item_w, user_b, item_b):
         """Overwrite the current tables (teacher forcing in tests, checkpoint load)."""
-        for dst, src in zip(self.tabs[self.cur], (user_w, item_w, user_b, item_b)):
+        for dst, src in zip(self.params(), (user_w, item_w, user_b, item_b)):
             dst.copy_(torch.as_tensor(src, dtype=torch.float32).reshape(dst.shape))
 
     def mt_state(self):
@@ -685,4 +701,5 @@ class MFEngine:
               "rg_mf_stepper_sync_mt")
 
     def optimizer_state(self):
+        self.flush()
         return {"step": self.t, "m": self.m, "v": self.v}

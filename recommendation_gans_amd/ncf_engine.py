@@ -39,8 +39,6 @@ class NCFEngine:
                  device="cuda", seed=0, mf_user_w=None, mf_item_w=None, rank=0, world_size=1, comm=None):
         _lib.require_gpu()
         self.rank, self.world, self.comm = int(rank), int(world_size), comm
-        if self.world > 1 and loss == "adaptive_hinge":
-            raise NotImplementedError("adaptive_hinge is implemented for world_size 1 (global max over all negatives)")
         if loss not in LOSS_KINDS:
             raise ValueError(f"unknown loss {loss!r}")
         if optimizer not in OPT_KINDS:
@@ -98,6 +96,11 @@ class NCFEngine:
         self.hot_bias = torch.zeros(rows, dtype=torch.int64, device=dev)
         self.partials = torch.zeros(2 * max(self.tiles, 1), **f32)
         self.adapt_partials = torch.zeros(2, **f32)
+        # adaptive hinge over several ranks: per-rank (score, draw index) slots, the active count,
+        # this rank's argmax row (rg_ncf_adapt_local / _global / _winner)
+        self.adapt_slots = torch.zeros(4 * max(self.world, 1), **f32)
+        self.adapt_count = torch.zeros(1, **f32)
+        self.adapt_row = torch.zeros(1, dtype=torch.int32, device=dev)
         self.part_row = torch.zeros(B * E, **f32)
         self.contrib = torch.zeros(self.rows * 2 * E, **f32)
         self.mlp_partials = torch.zeros(self.blocks * self.P, **f32)
@@ -209,12 +212,34 @@ class NCFEngine:
         np_ = 1 if self.loss == "adaptive_hinge" else self.tiles
         return _lib.MFLoss(np_, ia, ib, ptr(out))
 
-    def _forward_backward(self, batch, work, nw, stream):
+    def _exchange(self, t, allreduce):
+        if self.comm is not None:
+            self.comm.allreduce_(t)
+        else:
+            allreduce(t)
+
+    def _adapt_dp(self, batch, work, nw, stream, allreduce):
+        """dp of the adaptive hinge from this step's scores: one rank as a single kernel; over
+        several ranks the global maximum of ONE draw through two small SUM exchanges."""
+        if self.world == 1:
+            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
+                  "rg_ncf_adapt_dp")
+            return
+        ref = ctypes.byref
+        check(self.lib.rg_ncf_adapt_local(stream, ref(batch), ref(work), ref(nw), ptr(self.adapt_slots), self.rank,
+                                          self.world, ptr(self.adapt_row)), "rg_ncf_adapt_local")
+        self._exchange(self.adapt_slots, allreduce)
+        check(self.lib.rg_ncf_adapt_global(stream, ref(batch), ref(nw), ptr(self.adapt_slots), self.world,
+                                           ptr(self.adapt_count), ptr(self.adapt_partials)), "rg_ncf_adapt_global")
+        self._exchange(self.adapt_count, allreduce)
+        check(self.lib.rg_ncf_adapt_winner(stream, ref(batch), ref(nw), ptr(self.adapt_slots), self.world, self.rank,
+                                           ptr(self.adapt_row), ptr(self.adapt_count)), "rg_ncf_adapt_winner")
+
+    def _forward_backward(self, batch, work, nw, stream, allreduce=None):
         if self.loss == "adaptive_hinge":
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 1), "rg_ncf_pairs(scores)")
-            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
-                  "rg_ncf_adapt_dp")
+            self._adapt_dp(batch, work, nw, stream, allreduce)
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 2), "rg_ncf_pairs(given dp)")
         else:
@@ -253,7 +278,7 @@ class NCFEngine:
         nw = self._work(masks, True)
         if self.kernel_events is not None:
             self.kernel_events[0].record()
-        self._forward_backward(batch, work, nw, stream)
+        self._forward_backward(batch, work, nw, stream, allreduce)
         if self.kernel_events is not None:
             self.kernel_events[1].record()
         check(self.lib.rg_mf_stepper_release(self._stepper, stream), "rg_mf_stepper_release")
@@ -323,8 +348,7 @@ class NCFEngine:
         if self.loss == "adaptive_hinge":
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),
                                         ctypes.byref(nw), 1), "rg_ncf_pairs(scores)")
-            check(self.lib.rg_ncf_adapt_dp(stream, ctypes.byref(batch), ctypes.byref(nw), ptr(self.adapt_partials)),
-                  "rg_ncf_adapt_dp")
+            self._adapt_dp(batch, work, nw, stream, allreduce)
             parts = self.adapt_partials
         else:
             check(self.lib.rg_ncf_pairs(stream, ctypes.byref(self._model), ctypes.byref(batch), ctypes.byref(work),

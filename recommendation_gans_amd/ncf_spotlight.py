@@ -15,6 +15,7 @@ import torch
 from .implicit import ImplicitFactorizationModel
 from .spotlight import optimizers
 from .spotlight.dnn_models.mlp import MLP
+from .mf_spotlight import init_data_parallel
 from .utils.arg_extractor import get_args
 from .utils.data_provider import data_provider
 
@@ -27,6 +28,7 @@ def mlp_layers(embedding_dim):
 def main(argv=None):
     logging.basicConfig(format="%(message)s", level=logging.INFO)
     args = get_args(argv)
+    rank = init_data_parallel(args.world_size)     # additive --world_size (torchrun, one process per GPU)
     logging.info("DataSet MovieLens_%s will be used" % args.dataset)
     path = "/disk/scratch/s1877727/datasets/movielens/" if args.on_cluster else "datasets/movielens/"
     seed = 0
@@ -47,9 +49,12 @@ def main(argv=None):
                                        l2=args.l2_regularizer, representation=technique, random_state=random_state,
                                        batch_size=args.batch_size, use_cuda=bool(args.use_gpu),
                                        learning_rate=args.learning_rate, optimizer_func=optim,
-                                       experiment_name=args.experiment_name, loss=args.mf_loss)
+                                       experiment_name=args.experiment_name, loss=args.mf_loss,
+                                       world_size=args.world_size)
     logging.info("Model set, training begins")
-    model.fit(train, valid, verbose=True)
+    model.fit(train, valid, verbose=rank == 0)
+    if rank != 0:                       # replicated model: rank 0 evaluates and logs
+        return model
     logging.info("Model is ready, testing performance")
     model.test(test, item_popularity, args.k, rmse_flag=args.rmse, precision_recall=args.precision_recall,
                map_recall=args.map_recall)

@@ -123,7 +123,7 @@ def _worker_owner(rank, world, port, loss, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge"])
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge", "adaptive_hinge"])
 def test_owner_gloo_world2_equals_batch_2B(loss):
     """The owner-sharded layout (the default at R > 1, rg_owner.hip) at the oracle level: two
     ranks owning users u % 2, exchanging the pairs' scores and the item gradient, == one
@@ -136,7 +136,7 @@ def test_owner_gloo_world2_equals_batch_2B(loss):
                                                            loss)
     for s, (lo, hi) in enumerate(dc.global_batches(world)):
         owners = sum(out[r][3][s][2].astype(int) for r in range(world))
-        valid = world * dc.B if loss == "pointwise" else hi - lo
+        valid = world * dc.B if loss in ("pointwise", "adaptive_hinge") else hi - lo
         assert (owners[:, :valid] == 1).all() and (owners[:, valid:] == 0).all()
     for r in range(world):
         params, losses, states, negs = out[r]

@@ -288,6 +288,27 @@ def _worker_own_rccl(rank, world, port, loss, out):
         dist.destroy_process_group()
 
 
+def _worker_own_host(rank, world, port, loss, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommendation_gans_amd.comm import HostComm
+        comm = HostComm("cuda:0")
+        e, inputs = _own_engine(rank, world, loss, comm=comm)
+
+        def step(cur, nxt):
+            lv = e.train_step_in(cur, nxt)
+            comm.sync()            # the exchanges' host callbacks need the GIL: wait in a ctypes call
+            return lv
+        out[rank] = _own_collect(e, inputs, step)
+        comm.sync()
+        del e
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
 def _own_check(out, world, loss):
     """R owner-sharded ranks at batch B == one process at batch R*B (the oracle): losses 1e-5,
     MT state and every negative's ids bit-exact (each valid draw kept by exactly the rank
@@ -309,7 +330,7 @@ def _own_check(out, world, loss):
             assert (users == ref_negs[s][0][k1 - 1, c]).all(), (r, s, "negative users")
             assert (rec[:, 2] == ref_negs[s][1][k1 - 1, c]).all(), (r, s, "negative items")
             np.add.at(seen, (k1 - 1, c), 1)
-        valid_cols = GC if loss == "pointwise" else hi - lo
+        valid_cols = GC if loss in ("pointwise", "adaptive_hinge") else hi - lo
         assert (seen[:, :valid_cols] == 1).all() and (seen[:, valid_cols:] == 0).all(), (s, "draw ownership")
     for r in range(world):
         params, losses, states, _ = out[r]
@@ -327,7 +348,7 @@ def _own_check(out, world, loss):
         assert torch.equal(out[0][0][1], out[1][0][1]), "replicated items diverged"
 
 
-@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge"])
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge", "adaptive_hinge"])
 def test_owner_engine_gloo_world2(loss):
     """Two owner-sharded ranks at batch B (native parts, gloo all-reduces) == one process at 2B."""
     out = mp.Manager().dict()
@@ -340,3 +361,16 @@ def test_owner_native_rccl_world1():
     out = mp.Manager().dict()
     mp.spawn(_worker_own_rccl, args=(1, _free_port(), "bpr", out), nprocs=1, join=True)
     _own_check(out, 1, "bpr")
+
+
+@pytest.mark.parametrize("loss", ["bpr", "adaptive_hinge"])
+def test_owner_native_concurrent_step_world2(loss):
+    """The whole native owner step (rg_mf_stepper_train: the score all-reduce fenced on the main
+    stream, the item gradient and its all-reduce on the communicator stream beside the user
+    update and the next owner prepare) at world 2 -- two processes on cuda:0, the all-reduces
+    host-staged through gloo in stream order (comm.HostComm; RCCL refuses two ranks on one GPU)
+    -- == one process at batch 2B."""
+    out = mp.Manager().dict()
+    mp.spawn(_worker_own_host, args=(2, _free_port(), loss, out), nprocs=2, join=True)
+    _own_check(out, 2, loss)
+

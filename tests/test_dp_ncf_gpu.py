@@ -21,7 +21,8 @@ from oracle import ncf as oncf
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = ["mlp_pointwise_e16", "mlp_pointwise_e64", "mlp_bpr_e16", "neumf_pointwise_e16_m10", "neumf_bpr_e8_m5"]
+CASES = ["mlp_pointwise_e16", "mlp_pointwise_e64", "mlp_bpr_e16", "neumf_pointwise_e16_m10", "neumf_bpr_e8_m5",
+         "mlp_adaptive_hinge_e16", "neumf_adaptive_hinge_e16_m12"]   # adaptive: the global max over both ranks
 
 
 def _free_port():
