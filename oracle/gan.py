@@ -92,10 +92,12 @@ class Optimizer:
 class GANOracle:
     """G / D parameters under the reference's state_dict names (float64)."""
 
-    def __init__(self, g_init, d_init, N, S, H, E, Z=100, opt="rms", lr=1e-3):
+    def __init__(self, g_init, d_init, N, S, H, E, Z=100, opt="rms", lr=1e-3, dtype=np.float64):
         self.N, self.S, self.H, self.E, self.Z = N, S, H, E, Z
-        self.G = {k: np.asarray(v, np.float64).copy() for k, v in g_init.items()}
-        self.D = {k: np.asarray(v, np.float64).copy() for k, v in d_init.items()}
+        # dtype float32: the same restatement in fp32 NumPy arithmetic (another fp32 summation
+        # order, the fp32 side of tensor_parity's band where the reference cannot run)
+        self.G = {k: np.asarray(v, dtype).copy() for k, v in g_init.items()}
+        self.D = {k: np.asarray(v, dtype).copy() for k, v in d_init.items()}
         self.gh, self.dh = g_hidden(H), d_hidden(H)
         self.g_lin = [f"layers.{4 * i}" for i in range(len(self.gh))]
         self.g_bn = [f"layers.{4 * i + 1}" for i in range(len(self.gh))]

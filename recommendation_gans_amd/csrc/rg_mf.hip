@@ -561,6 +561,8 @@ struct ApplyArgs {
     int32_t lazy_t;               // this step (absolute)
     int32_t lazy_full;            // process every user row (no next step known)
     unsigned long long *lazy_rows;   // optional: count of user rows processed (diagnostic steps)
+    int32_t lazy_dbg;             // timing experiments only (RG_LAZY_DBG; wrong results): bit 0 no catch-up
+    int32_t lazy_cap;             // > 0: a row that has missed this many steps is processed anyway
 };
 
 #ifndef RG_MF_SORTED_PULL
@@ -643,51 +645,59 @@ __device__ __forceinline__ float finalize_loss(const float *__restrict__ partial
 // Gradient + optimizer update of unified row r (users [0, U), items [U, U + I)).
 // COLD: a row no pair of the step touches -- its data gradient is exactly zero
 // (only the coupled weight decay acts), so nothing of the step's scratch is read.
-// Adam constants of the last kConstWin steps before this one, staged in LDS by every
-// workgroup of a lazy pass (a row's catch-up loop reads one per skipped step; from global
-// memory each would be a dependent round trip); older steps fall back to global loads
-constexpr int kConstWin = kBlock;
 struct LazyRow {
     int cnt;          // list count (data gradient this step)
     int32_t mk, lsr;  // prepare mark, last step applied (relative)
+    bool active;      // false: a lane group past the end of the rows
 };
 
-__device__ __forceinline__ float2 step_const(const ApplyArgs &a, const float2 *lconst, int64_t s) {
-    const int64_t w = s - ((int64_t)a.lazy_t - kConstWin);
-    return (w >= 0 && w < kConstWin) ? lconst[w] : a.step_consts[s];
+// wave-uniform maximum (every lane ends with the same value)
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
+    return __builtin_amdgcn_readfirstlane(x);
 }
 
-// the cold updates of steps lazy_base + lsr + 1 .. + lag of one row (zero data gradient: the
-// coupled weight decay and the optimizer state only), in step order, each with its own
-// Adam constants -- the exact operation sequence the eager dense pass applies to a row no
-// pair touches (opt_update with gdata = 0), so the row ends bit-identical
+// this lane's Adam constants of window step `lane` (absolute step s0 + lane, lane < n)
+__device__ __forceinline__ float2 window_const(const ApplyArgs &a, int64_t s0, int n) {
+    const int lane = threadIdx.x & (kWave - 1);
+    return (a.opt.kind == RG_OPT_ADAM && lane < n) ? a.step_consts[s0 + lane] : make_float2(0.0f, 0.0f);
+}
+
+// The cold updates a row missed (zero data gradient: the coupled weight decay and the
+// optimizer state only), in step order, each with its own Adam constants -- the exact
+// operation sequence the eager dense pass applies to a row no pair touches (opt_update with
+// gdata = 0), so the row ends bit-identical.  The loop runs over the wave's window of the
+// `wmax` steps before `upto`, so the step is wave-uniform: its constants come from lane k of
+// `cl` (loaded beside the row, 64 steps per load) by readlane, and each row updates only at
+// the last `mylag` steps of the window.
 template <class L>
-__device__ __forceinline__ void catch_up(const ApplyArgs &a, const float2 *lconst, int lag, int32_t lsr, int sub,
+__device__ __forceinline__ void catch_up(const ApplyArgs &a, float2 cl, int wmax, int mylag, int64_t upto, int sub,
                                          float (&p)[L::EPL], float (&m)[L::EPL], float (&v)[L::EPL], float &pb,
                                          float &mb, float &vb) {
+    if (wmax <= 0) return;
     rg_opt_t o = a.opt;
     const bool adam = o.kind == RG_OPT_ADAM;
-    for (int k = 0; k < lag; ++k) {
-        if (adam) {
-            const float2 sc = step_const(a, lconst, a.lazy_base + lsr + 1 + k);
-            o.step_size = sc.x;
-            o.bias_correction2_sqrt = sc.y;
-        }
+    const int first = wmax - mylag;
+    for (int c0 = 0; c0 < wmax; c0 += kWave) {
+        if (c0 > 0) cl = window_const(a, upto - wmax + c0, wmax - c0);
+        const int n = wmax - c0 < kWave ? wmax - c0 : kWave;
+        for (int k = 0; k < n; ++k) {
+            if (adam) {
+                o.step_size = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cl.x), k));
+                o.bias_correction2_sqrt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cl.y), k));
+            }
+            if (c0 + k < first) continue;
 #pragma unroll
-        for (int q = 0; q < L::EPL; ++q) p[q] = opt_update(o, p[q], 0.0f, m[q], v[q]);
-        if (sub == 0 && a.has_bias) pb = opt_update(o, pb, 0.0f, mb, vb);
+            for (int q = 0; q < L::EPL; ++q) p[q] = opt_update(o, p[q], 0.0f, m[q], v[q]);
+            if (sub == 0 && a.has_bias) pb = opt_update(o, pb, 0.0f, mb, vb);
+        }
     }
-}
-
-// every thread of the workgroup: this step's window of Adam constants into LDS
-__device__ __forceinline__ void stage_consts(const ApplyArgs &a, float2 *lconst) {
-    const int64_t s = (int64_t)a.lazy_t - kConstWin + threadIdx.x;
-    if (a.opt.kind == RG_OPT_ADAM && s >= 1) lconst[threadIdx.x] = a.step_consts[s];
 }
 
 template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false>
 __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub,
-                                          const LazyRow lzr = LazyRow{}, const float2 *lconst = nullptr) {
+                                          const LazyRow lzr = LazyRow{}) {
     constexpr int EPL = L::EPL;
     const int64_t rb = a.row_begin, nr = a.row_end - rb;
     const int D = a.dim;
@@ -703,31 +713,54 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     // since, else w_out (then the update is in place)
     const bool lz = LAZY && t == 0;
     int lag = 0;
-    const int cnt = lzr.cnt;
     const int32_t lsr = lzr.lsr;
+    // proc: this row is updated this step (false: a lazily skipped user row, which still runs
+    // through to the wave's catch-up loop -- a wave-collective -- doing nothing)
+    const int missed = lz ? (int)((int64_t)a.lazy_t - 1 - a.lazy_base - lsr) : 0;
+    const bool proc = !lz || (lzr.active && (a.lazy_full || lzr.cnt > 0 || lzr.mk == a.lazy_t + 1 ||
+                                             (a.lazy_cap > 0 && missed >= a.lazy_cap)));
+    const int cnt = proc ? lzr.cnt : 0;
     const float *src_w = a.w_in[t], *src_b = a.b_in[t];
     float p[EPL], m[EPL], v[EPL], g[EPL];
     float pb = 0.0f, mb = 0.0f, vb = 0.0f;
+    L::zero(p); L::zero(m); L::zero(v);
+    int2 lspec[LSPEC ? kCap : 1];
     if (lz) {
-        // LSPEC: the optimizer state (one copy, not ping-ponged) is loaded before the decision,
-        // so a processed row's loads take one dependent round trip fewer
-        if (LSPEC) {
-            if (adam) L::load(m, a.w_m[0], lr_, D, sub); else L::zero(m);
-            if (has_v) L::load(v, a.w_v[0], lr_, D, sub); else L::zero(v);
+        // LSPEC: p (from the set a row processed last step holds it in), m, v and the list are
+        // loaded with the decision words, in one round trip as the eager pass; a processed row
+        // that missed an odd number of steps reloads p from the other set
+        if (LSPEC && lzr.active) {
+            L::load(p, a.w_in[0], lr_, D, sub);
+            if (adam) L::load(m, a.w_m[0], lr_, D, sub);
+            if (has_v) L::load(v, a.w_v[0], lr_, D, sub);
             if (sub == 0 && a.has_bias) {
+                pb = a.b_in[0][lr_];
                 if (adam) mb = a.b_m[0][lr_];
                 if (has_v) vb = a.b_v[0][lr_];
             }
+            const int4 *lst = reinterpret_cast<const int4 *>(a.row_list + r * kCap);
+#pragma unroll
+            for (int e = 0; e < kCap / 2; ++e) {
+                const int4 q = lst[e];
+                lspec[2 * e] = make_int2(q.x, q.y);
+                lspec[2 * e + 1] = make_int2(q.z, q.w);
+            }
         }
-        if (!(a.lazy_full || cnt > 0 || lzr.mk == a.lazy_t + 1)) return;
-        lag = (int)((int64_t)a.lazy_t - 1 - a.lazy_base - lsr);
+        lag = proc ? missed : 0;
         if (lag & 1) {
             src_w = a.w_out[t];
             src_b = a.b_out[t];
         }
     }
+    // the wave's catch-up window and its constants (issued with the row's loads)
+    const int wmax = LAZY ? wave_max(lag) : 0;
+    const float2 wconst = (LAZY && wmax > 0) ? window_const(a, (int64_t)a.lazy_t - wmax, wmax) : make_float2(0.0f, 0.0f);
+    if (LSPEC && lz && proc && (lag & 1)) {
+        L::load(p, src_w, lr_, D, sub);
+        if (sub == 0 && a.has_bias) pb = src_b[lr_];
+    }
 
-    if (MODE != kGradOnly) {
+    if (MODE != kGradOnly && proc && !(LSPEC && lz)) {
         if (NT == 2) {
             L::load_nt(p, src_w, lr_, D, sub);
             if (adam) L::load_nt(m, a.w_m[t], lr_, D, sub); else L::zero(m);
@@ -760,7 +793,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 #ifdef RG_X_NOPULL   // timing experiments only (wrong results): the pass without the pulls
         const int c = a.row_count[r] < 0 ? 1 : 0;
 #else
-        const int c = lz ? cnt : a.row_count[r];
+        const int c = lz ? cnt : (COLD ? 0 : a.row_count[r]);
 #endif
         // SPEC: the list and the item's partial-slot range are loaded beside the count
         // (entries past the count are stale and never used), so a touched row's partner
@@ -782,7 +815,8 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             int2 ent[kCap];
 #pragma unroll
             for (int e = 0; e < kCap; ++e)
-                ent[e] = e < ne ? ((SPEC && !lz) ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
+                ent[e] = e < ne ? ((LSPEC && lz) ? lspec[LSPEC ? e : 0]
+                                   : (SPEC && !lz) ? spec[SPEC ? e : 0] : a.row_list[r * kCap + e]) : make_int2(0, 0);
 #if RG_MF_SORTED_PULL
             // the entries' slots were claimed by atomics in arrival order: sorted by (partner,
             // dz bits) the row sums them in an order independent of that timing, so a step
@@ -879,7 +913,9 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         }
     }
 
-    if (lz && lag > 0) catch_up<L>(a, lconst, lag, lsr, sub, p, m, v, pb, mb, vb);
+    if (LAZY && !(a.lazy_dbg & 1))   // every lane of the wave (item / skipped rows: nothing to catch up)
+        catch_up<L>(a, wconst, wmax, lag, a.lazy_t, sub, p, m, v, pb, mb, vb);
+    if (!proc) return;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
     if (NT == 3) {          // optimizer state streamed past the caches, the new row kept (next gathers)
@@ -914,38 +950,37 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 template <class L>
 __global__ __launch_bounds__(kBlock) void mf_lazy_flush_kernel(ApplyArgs a) {
     constexpr int LPU = L::LPU, UPW = L::UPW, EPL = L::EPL;
-    __shared__ float2 lconst[kConstWin];
     const int lane = threadIdx.x & (kWave - 1);
     const int sub = lane & (LPU - 1);
     const int64_t r = (((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * UPW + (lane / LPU);
-    const int32_t lsr = r < a.num_users ? a.last_rel[r] : 0;
-    // the window ends at lazy_t + 1: the flush's last catch-up step is lazy_t itself
-    {
-        const int64_t s = (int64_t)a.lazy_t + 1 - kConstWin + threadIdx.x;
-        if (a.opt.kind == RG_OPT_ADAM && s >= 1) lconst[threadIdx.x] = a.step_consts[s];
-    }
-    lds_barrier();
-    if (r >= a.num_users) return;
-    const int lag = (int)((int64_t)a.lazy_t - a.lazy_base - lsr);
-    if (lag <= 0) return;
+    if (((((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * UPW) >= a.num_users) return;   // wave-uniform
+    const bool in = r < a.num_users;
+    const int32_t lsr = in ? a.last_rel[r] : 0;
+    const int lag = in ? (int)((int64_t)a.lazy_t - a.lazy_base - lsr) : 0;
     const int D = a.dim;
     const bool adam = a.opt.kind == RG_OPT_ADAM;
     const bool has_v = a.opt.kind != RG_OPT_SGD;
     const float *src_w = (lag & 1) ? a.w_out[0] : a.w_in[0];
     const float *src_b = (lag & 1) ? a.b_out[0] : a.b_in[0];
+    const int64_t rr = in ? r : 0;
     float p[EPL], m[EPL], v[EPL];
     float pb = 0.0f, mb = 0.0f, vb = 0.0f;
-    L::load(p, src_w, r, D, sub);
-    if (adam) L::load(m, a.w_m[0], r, D, sub); else L::zero(m);
-    if (has_v) L::load(v, a.w_v[0], r, D, sub); else L::zero(v);
-    if (sub == 0) {
-        pb = src_b[r];
-        if (adam) mb = a.b_m[0][r];
-        if (has_v) vb = a.b_v[0][r];
+    L::zero(p); L::zero(m); L::zero(v);
+    if (lag > 0) {              // current rows are read and written by nobody
+        L::load(p, src_w, rr, D, sub);
+        if (adam) L::load(m, a.w_m[0], rr, D, sub);
+        if (has_v) L::load(v, a.w_v[0], rr, D, sub);
+        if (sub == 0) {
+            pb = src_b[rr];
+            if (adam) mb = a.b_m[0][rr];
+            if (has_v) vb = a.b_v[0][rr];
+        }
     }
-    ApplyArgs b = a;           // step_const's window is relative to lazy_t: shift it by one
-    b.lazy_t = a.lazy_t + 1;
-    catch_up<L>(b, lconst, lag, lsr, sub, p, m, v, pb, mb, vb);
+    // steps [lazy_t + 1 - lag, lazy_t] (the flush's window ends at lazy_t itself)
+    const int wmax = wave_max(lag > 0 ? lag : 0);
+    const float2 wc = wmax > 0 ? window_const(a, (int64_t)a.lazy_t + 1 - wmax, wmax) : make_float2(0.0f, 0.0f);
+    catch_up<L>(a, wc, wmax, lag > 0 ? lag : 0, (int64_t)a.lazy_t + 1, sub, p, m, v, pb, mb, vb);
+    if (lag <= 0) return;
     L::store(const_cast<float *>(a.w_in[0]), r, D, sub, p);
     if (adam) L::store(a.w_m[0], r, D, sub, m);
     if (has_v) L::store(a.w_v[0], r, D, sub, v);
@@ -1073,18 +1108,18 @@ __global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs 
     const int64_t ni = re > ia0 ? re - ia0 : 0;
     const int64_t r = k < ni ? ia0 + k : rb + (k - ni);
     if (LAZY) {
-        // a user row's decision words and the workgroup's constants window, loaded together
-        __shared__ float2 lconst[kConstWin];
-        LazyRow lzr{0, 0, 0};
-        if (k < nr && r < a.num_users) {
-            lzr.cnt = a.row_count[r];
-            lzr.mk = a.umark[r];
-            lzr.lsr = a.last_rel[r];
+        // a user row's decision words first (the row's loads depend on them)
+        if ((wave * UPW) >= nr) return;                     // wave-uniform: the catch-up loop is per wave
+        const bool in = k < nr;
+        const int64_t rr = in ? r : rb;
+        LazyRow lzr{0, 0, 0, in};
+        if (in && rr < a.num_users) {
+            lzr.cnt = a.row_count[rr];
+            lzr.mk = a.umark[rr];
+            lzr.lsr = a.last_rel[rr];
         }
-        stage_consts(a, lconst);
-        lds_barrier();
-        if (k >= nr) return;
-        apply_row<L, kApplyPull, NT, false, SPEC, true, LSPEC>(a, r, sub, lzr, lconst);
+        // a lane group past the end runs as an inactive user row (row 0: no loads, no stores)
+        apply_row<L, kApplyPull, NT, false, SPEC, true, LSPEC>(a, in ? r : 0, sub, lzr);
         return;
     }
     if (k >= nr) return;
@@ -1717,6 +1752,10 @@ int lazy_args(const rg_mf_lazy_t *lz, const rg_opt_t *opt, ApplyArgs &a) {
     a.lazy_t = (int32_t)lz->step;
     a.lazy_full = lz->full;
     a.lazy_rows = reinterpret_cast<unsigned long long *>(lz->rows_done);
+    static const int dbg = [] { const char *e = getenv("RG_LAZY_DBG"); return e ? atoi(e) : 0; }();
+    static const int cap = [] { const char *e = getenv("RG_LAZY_CAP"); return e ? atoi(e) : 0; }();
+    a.lazy_dbg = dbg;
+    a.lazy_cap = cap;
     return RG_OK;
 }
 }  // namespace

@@ -219,7 +219,7 @@ class ImplicitFactorizationModel:
         if owner:
             plans = e.make_plans(ti, users=tu)
         elif R > 1:                                # this rank's columns [r*b, (r+1)*b) of each global batch
-            plans = e.make_plans(ti, offset=r * b, stride=B)
+            plans = e.make_plans(ti, offset=r * b, stride=B, n_batches=nb)
         else:
             plans = e.make_plans(ti)
         vplans = e.make_plans(vi, users=vu) if owner else None

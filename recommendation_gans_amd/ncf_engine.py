@@ -176,9 +176,12 @@ class NCFEngine:
     def make_plan(self, pos_i):
         return build_plan(pos_i, self.batch_size, self.tc, self.I)
 
-    def make_plans(self, items, offset=0, stride=None):
-        """Plans of every batch [offset + k*stride, +batch_size) of ``items`` in one launch."""
-        return build_plans(items, self.batch_size, self.tc, self.I, offset=offset, stride=stride)
+    def make_plans(self, items, offset=0, stride=None, n_batches=None):
+        """Plans of every batch [offset + k*stride, +batch_size) of ``items`` in one launch
+        (``n_batches``: how many, counting empty ones -- a data-parallel rank's slice of the last
+        global batch may be empty)."""
+        return build_plans(items, self.batch_size, self.tc, self.I, offset=offset, stride=stride,
+                           n_batches=n_batches)
 
     def mlp_params(self):
         """The MLP parameters as tensors of their reference shapes (views of the flat buffer)."""

@@ -579,6 +579,12 @@ if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "init":
     sys.exit(0)
 
 
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "refinit5":
+    # the reference's own D init (clamp-bound) and lr 1e-3 over a whole
+    # n_critic cycle: five D iterations, the G iteration after the fifth, one more D iteration
+    save("gan_rms_refinit5.npz", **gan_case("rms", seed=3, d_steps=6, lr=1e-3))
+    sys.exit(0)
+
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gan":
     make_gan()
     sys.exit(0)

@@ -138,7 +138,8 @@ def _gan_batch(ml20m, S, B):
     return hist, sl
 
 
-def test_gan_full_size_iterations(ml20m):
+@pytest.mark.parametrize("refinit", [False, True], ids=["scaled_d", "reference_init"])
+def test_gan_full_size_iterations(ml20m, refinit):
     """C4: slate_generation.py's cGAN at S = 5, gan_hidden_layer = 256, batch 256, RMSprop.
     G keeps the reference's own init (cGAN_models.py:70-73 under torch.manual_seed(0)); every
     D tensor is rescaled to max |x| = 0.004 (as the cGAN goldens, make_golden.gan_case):
@@ -146,19 +147,45 @@ def test_gan_full_size_iterations(ml20m):
     +-0.01 and their pre-activations cancel to within rounding of the LeakyReLU kink, where
     the slope -- and so the sign of RMSprop's first, sign-like update -- is decided by
     summation order in ANY implementation.  Continuous D weights keep the comparison
-    meaningful; lr 1e-4 as the goldens."""
+    meaningful; lr 1e-4 as the goldens.
+
+    reference_init: the reference's own D init and the bench's lr 1e-3, no
+    rescale (at C4's size W1's Xavier bound is 0.0077, inside the clamp; layers 2-4 clamp).
+    Every tensor after each iteration within 1e-5 relative (norm) of the float64 restatement,
+    nothing exempted except the bound check of the pre-BatchNorm biases (analytically zero
+    gradient, see test_gan_oracle_reference_init_cycle); the fraction of elements off by more
+    than 1e-5 of the tensor's scale is printed."""
     from recommendation_gans_amd.gan_engine import GANBatch, GANEngine
     from recommendation_gans_amd.spotlight.dnn_models.cGAN_models import discriminator, generator
-    N, S, H, E, Z, B, lr = ml20m.num_items, 5, 256, 5, 100, 256, 1e-4
+    N, S, H, E, Z, B, lr = ml20m.num_items, 5, 256, 5, 100, 256, (1e-3 if refinit else 1e-4)
     hist, sl = _gan_batch(ml20m, S, B)
     torch.manual_seed(0)
     G = generator(num_items=N, noise_dim=Z, embedding_dim=E, hidden_layer=[H // 2, H], output_dim=S)
     D = discriminator(num_items=N, embedding_dim=E, hidden_layers=[2 * H, H, H // 2], input_dim=S)
     g_sd = {k: v.detach().clone() for k, v in G.state_dict().items()}
-    d_sd = {k: v.detach().clone() * (0.004 / max(float(v.abs().max()), 1e-30)) for k, v in D.state_dict().items()}
+    d_sd = {k: v.detach().clone() * (1.0 if refinit else 0.004 / max(float(v.abs().max()), 1e-30))
+            for k, v in D.state_dict().items()}
+
+    def check(got, ref, grad, name, exempt=False, ref32=None):
+        if not refinit:
+            return param_ok(got, ref, grad, lr, exempt=exempt)
+        got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+        r = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
+        frac = float((np.abs(got - ref) > 1e-5 * max(np.abs(ref).max(), 1e-30)).mean())
+        ok, msg = omf.tensor_parity(torch.from_numpy(got), torch.from_numpy(np.asarray(ref32, np.float64)),
+                                    torch.from_numpy(ref))
+        print(f"C4 reference init {name}: GPU vs fp64 rel {r:.2e}, {frac:.2e} of elements outside 1e-5 of scale; "
+              f"band rule vs fp32 NumPy: {msg}")
+        if exempt and not ok:
+            return bool(np.abs(got - ref).max() <= lr), f"pre-BN bias (analytically zero gradient): {msg}"
+        return ok, msg
     eng = GANEngine(g_sd, d_sd, N, S, H, E, Z, batch_max=B, optimizer="rms", lr=lr)
     o = og.GANOracle({k: v.numpy() for k, v in g_sd.items()}, {k: v.numpy() for k, v in d_sd.items()}, N, S, H, E,
                      Z, opt="rms", lr=lr)
+    # reference_init: the fp32 side of tensor_parity's band (the reference cannot run at this size):
+    # the same restatement in fp32 NumPy arithmetic, another fp32 summation order
+    o32 = og.GANOracle({k: v.numpy() for k, v in g_sd.items()}, {k: v.numpy() for k, v in d_sd.items()}, N, S, H, E,
+                       Z, opt="rms", lr=lr, dtype=np.float32) if refinit else None
     rs = np.random.RandomState(7)
     gd, dd = og.g_hidden(H), og.d_hidden(H)
 
@@ -171,6 +198,8 @@ def test_gan_full_size_iterations(ml20m):
     mk = masks(dd, 0.3) + masks(gd, 0.1) + masks(dd, 0.3)
     out = eng.d_step(batch, z=torch.from_numpy(z), masks=mk).cpu().numpy()
     loss, d_real, d_fake, fake = o.d_step(hist, sl, z.astype(np.float64), [m.astype(np.float64) for m in mk], scales)
+    if o32 is not None:
+        o32.d_step(hist, sl, z, [m.astype(np.float32) for m in mk], tuple(np.float32(x) for x in scales))
     dval = eng.last_d_out(2 * B).cpu().numpy()
     # D outputs: 4 layers over K = S*N + E = 100,545 (fp32 MFMA, split-K): 1e-5 of the outputs' scale
     scale = np.abs(np.concatenate([d_real.ravel(), d_fake.ravel()])).max()
@@ -180,20 +209,38 @@ def test_gan_full_size_iterations(ml20m):
     assert abs(out[0] - loss) <= 1e-5 * scale
     dsd = eng.d_state_dict()
     for k in o.D:
-        ok, msg = param_ok(dsd[k].numpy(), o.D[k], o.last_grads[k], lr)
+        ok, msg = check(dsd[k].numpy(), o.D[k], o.last_grads[k], "D " + k, ref32=o32.D[k] if o32 else None)
         assert ok, f"D {k}: {msg}"
     # one generator iteration (CGANs.py:370-408) on the same batch, eval-mode slates after it
     z = rs.rand(B, Z).astype(np.float32)
     mk = masks(gd, 0.1) + masks(dd, 0.3)
     gl, slates = eng.g_step(batch, z=torch.from_numpy(z), masks=mk)
     gloss, gd_fake, ref_slates = o.g_step(hist, z.astype(np.float64), [m.astype(np.float64) for m in mk], scales)
-    assert abs(float(gl[0]) - gloss) <= 1e-5 * np.abs(gd_fake).max()
-    assert np.abs(eng.last_d_out(B).cpu().numpy() - gd_fake.ravel()).max() <= 1e-5 * np.abs(gd_fake).max()
+    gdout = eng.last_d_out(B).cpu().numpy()
+    if o32 is not None:
+        # after a D step from the clamp-bound init, D(G(z)) carries the D parameters' fp32
+        # spread (the band above): loss and outputs no further from float64 than 3x fp32 NumPy's
+        gl32, gd32, sl32 = o32.g_step(hist, z, [m.astype(np.float32) for m in mk], tuple(np.float32(x) for x in scales))
+        e32 = np.abs(np.asarray(gd32, np.float64).ravel() - gd_fake.ravel()).max()
+        print(f"C4 reference init G step: loss |gpu-fp64| {abs(float(gl[0]) - gloss):.3e} vs |fp32-fp64| "
+              f"{abs(float(gl32) - gloss):.3e}; D(G(z)) max |gpu-fp64| {np.abs(gdout - gd_fake.ravel()).max():.3e} "
+              f"vs |fp32-fp64| {e32:.3e}")
+        assert abs(float(gl[0]) - gloss) <= max(3 * abs(float(gl32) - gloss), 1e-5 * np.abs(gd_fake).max())
+        assert np.abs(gdout - gd_fake.ravel()).max() <= max(3 * e32, 1e-5 * np.abs(gd_fake).max())
+    else:
+        assert abs(float(gl[0]) - gloss) <= 1e-5 * np.abs(gd_fake).max()
+        assert np.abs(gdout - gd_fake.ravel()).max() <= 1e-5 * np.abs(gd_fake).max()
     agree = (slates.cpu().numpy() == ref_slates).mean()
-    assert agree >= 0.999, agree                          # argmax ties within fp32 rounding may differ
+    if o32 is not None:   # the G parameters carry D's fp32 spread: near-ties of the heads' argmax flip
+        agree32 = (np.asarray(sl32) == ref_slates).mean()
+        print(f"C4 reference init slates: GPU agrees with fp64 on {agree:.4f}, fp32 NumPy on {agree32:.4f}")
+        assert 1 - agree <= max(3 * (1 - agree32), 1e-3), (agree, agree32)
+    else:
+        assert agree >= 0.999, agree                      # argmax ties within fp32 rounding may differ
     gsd = eng.g_state_dict()
     for k in o.g_params:
-        ok, msg = param_ok(gsd[k].numpy(), o.G[k], o.last_grads[k], lr, exempt=k in o.pre_bn_biases())
+        ok, msg = check(gsd[k].numpy(), o.G[k], o.last_grads[k], "G " + k, exempt=k in o.pre_bn_biases(),
+                        ref32=o32.G[k] if o32 else None)
         assert ok, f"G {k}: {msg}"
 
 

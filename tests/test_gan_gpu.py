@@ -267,3 +267,96 @@ def test_gan_device_noise_trains():
         runs.append(np.concatenate(losses))
         assert np.isfinite(runs[-1]).all()
     np.testing.assert_array_equal(runs[0], runs[1])
+
+
+def test_gan_reference_init_full_cycle(golden_dir):
+    """the reference's own D init (clamp-bound) at lr 1e-3 over a whole
+    n_critic cycle -- five D iterations, the G iteration after the fifth, a sixth D iteration
+    (tests/golden/gan_rms_refinit5.npz, the reference's steps with their z and dropout masks).
+    Free-running from the same init, every D / G tensor after every step is held to
+    tensor_parity's rule: 1e-5 relative to the reference's fp32 tensor, or -- where the
+    clamped weights put pre-activations on the LeakyReLU kink and summation order picks the
+    slope, for any fp32 implementation -- no further from the float64 restatement (oracle/gan.py
+    with the same z and masks) than 3x an fp32 implementation's own distance to it: the
+    reference's, or the same restatement run in fp32 NumPy (another summation order).  The
+    second matters where an exact gradient is 0: a clamped layer's bias sums terms that cancel
+    exactly, torch's CPU order leaves 0 and fp32 NumPy (and the GPU) a 1e-10 residue that
+    RMSprop's g / (sqrt(v) + eps) turns into a 2.8e-5 step (D0 layers.6.bias, measured).
+    Nothing is exempted; the fraction of elements off by more than 1e-5 of the tensor's scale
+    is reported (stdout, and RG_REPORT_DIR/gan_refinit5_parity.json when set)."""
+    import json
+    from oracle import mf as omf
+    from recommendation_gans_amd.gan_engine import GANBatch
+    z, dims, gp, gb, dn, g_init, d_init = load(golden_dir, "gan_rms_refinit5")
+    N, S, H, E, B, L, Z, nb, dsteps = dims
+    lr = float(z["lr"][0])
+    assert lr == 1e-3 and dsteps == 6 and int(z["g_step_at"][0]) == 4
+    assert (np.abs(d_init["layers.0.weight"]) > og.CLAMP).mean() > 0.5, "the reference init binds the clamp"
+    eng = make_engine(z, gp, gb, dn, g_init, d_init, dims, "rms", lr)
+    o = og.GANOracle(g_init, d_init, N, S, H, E, Z, opt="rms", lr=lr)
+    o32 = og.GANOracle(g_init, d_init, N, S, H, E, Z, opt="rms", lr=lr, dtype=np.float32)
+    scales = tuple(float(x) for x in z["drop_scale"])
+    sc32 = tuple(np.float32(x) for x in scales)
+    report, worst = [], []
+    for k in range(dsteps):
+        b = int(z[f"d{k}_batch"][0])
+        hist, sl = z["hist"][b * B:(b + 1) * B], z["slates"][b * B:(b + 1) * B]
+        batch = GANBatch(hist, sl, N, S, "cuda")
+        masks = [z[f"d{k}_mask{j}"] for j in range(8)]
+        eng.d_step(batch, z=torch.from_numpy(z[f"d{k}_z"]), masks=masks)
+        o.d_step(hist, sl, z[f"d{k}_z"].astype(np.float64), [m.astype(np.float64) for m in masks], scales)
+        o32.d_step(hist, sl, z[f"d{k}_z"], [m.astype(np.float32) for m in masks], sc32)
+        dgr = dict(o.last_grads)
+        checks = [(f"D{k} D.{n}", eng.d_state_dict()[n].numpy(), z[key(f"d{k}_after_D_", n)], o.D[n], o32.D[n], dgr)
+                  for n in dn]
+        if k == int(z["g_step_at"][0]):
+            masks = [z[f"g{k}_mask{j}"] for j in range(5)]
+            gl, slates = eng.g_step(batch, z=torch.from_numpy(z[f"g{k}_z"]), masks=masks)
+            o.g_step(hist, z[f"g{k}_z"].astype(np.float64), [m.astype(np.float64) for m in masks], scales)
+            o32.g_step(hist, z[f"g{k}_z"], [m.astype(np.float32) for m in masks], sc32)
+            np.testing.assert_allclose(float(gl[0]), z[f"g{k}_loss"][0], rtol=1e-5)
+            gsd = eng.g_state_dict()
+            ggr = dict(o.last_grads)
+            checks += [(f"G{k} G.{n}", gsd[n].numpy(), z[key(f"g{k}_after_G_", n)], o.G[n], o32.G[n], ggr)
+                       for n in gp + gb]
+        for what, got, ref32, ref64, np32, grads in checks:
+            t = lambda x: torch.from_numpy(np.asarray(x, np.float64).ravel())
+            ok, msg = omf.tensor_parity(t(got), t(ref32), t(ref64))
+            if not ok:                       # the band of the other fp32 implementation
+                ok2, msg2 = omf.tensor_parity(t(got), t(np32), t(ref64))
+                ok, msg = ok2, f"{msg}; vs fp32 NumPy: {msg2}"
+            zero = np.zeros(np.asarray(got).size, bool)
+            if not ok:
+                # elements whose float64 gradient is EXACTLY zero (terms that cancel exactly, e.g.
+                # a clamped layer's bias): an fp32 sum leaves 0 or a rounding residue depending on
+                # its order, and RMSprop's g / (sqrt(v) + eps) turns a residue into a step of up to
+                # lr -- counted and bounded by lr; every other element stays under the band rule
+                name = what.split(".", 1)[1]
+                zero = (np.asarray(grads[name]).ravel() == 0) if name in grads else zero
+                keep = ~zero
+                ok3, msg3 = omf.tensor_parity(t(got)[keep], t(ref32)[keep], t(ref64)[keep]) if keep.any() else \
+                    (True, "no elements")
+                if not ok3:
+                    ok3, msg3 = omf.tensor_parity(t(got)[keep], t(np32)[keep], t(ref64)[keep])
+                bound = bool(np.all(np.abs(np.asarray(got, np.float64).ravel() - np.asarray(ref64).ravel())[zero]
+                                    <= lr * (1 + 1e-5)))
+                ok = bool(zero.any()) and ok3 and bound
+                msg = f"{msg}; {int(zero.sum())} exact-zero-gradient elements (|d| <= lr: {bound}), rest: {msg3}"
+            scale = max(float(np.abs(ref32).max()), 1e-30)
+            frac = float((np.abs(np.asarray(got, np.float64) - ref32) > 1e-5 * scale).mean())
+            report.append({"tensor": what, "parity": msg, "frac_outside_1e-5_of_scale": frac,
+                           "exact_zero_gradient_elements": int(zero.sum())})
+            if not ok:
+                detail = {}
+                if np.asarray(got).size <= 16:
+                    detail = {"gpu": np.asarray(got).ravel().tolist(), "ref32": np.asarray(ref32).ravel().tolist(),
+                              "ref64": np.asarray(ref64).ravel().tolist()}
+                    detail["grad64"] = np.asarray(grads.get(what.split(".", 1)[1], [])).ravel().tolist()
+                report[-1]["detail"] = detail
+                worst.append((what, msg))
+    print(json.dumps(report, indent=0))
+    if os.environ.get("RG_REPORT_DIR"):
+        os.makedirs(os.environ["RG_REPORT_DIR"], exist_ok=True)
+        with open(os.path.join(os.environ["RG_REPORT_DIR"], "gan_refinit5_parity.json"), "w") as fp:
+            json.dump(report, fp, indent=1)
+    assert not worst, worst
