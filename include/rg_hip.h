@@ -53,7 +53,9 @@ enum rg_loss_kind {
     RG_LOSS_POINTWISE = 0,       /* spotlight/losses.py:20   BCE(pos,1) + BCE(neg,0) */
     RG_LOSS_BPR = 1,             /* spotlight/losses.py:59   mean(1 - sigmoid(pos - neg)), neg.view(n,B) */
     RG_LOSS_HINGE = 2,           /* spotlight/losses.py:99   mean(clamp(neg - pos + 1, 0)), neg.view(n,B) */
-    RG_LOSS_ADAPTIVE_HINGE = 3   /* spotlight/losses.py:133  hinge against max over ALL negatives */
+    RG_LOSS_ADAPTIVE_HINGE = 3,  /* spotlight/losses.py:133  hinge against max over ALL negatives */
+    RG_LOSS_POINTWISE_POS = 4    /* implicit.py:359-360 (neg_examples=None): BCE(pos,1) only; the step's
+                                    negatives are drawn but take no part (single-rank MF step only) */
 };
 
 enum rg_opt_kind {

@@ -19,7 +19,8 @@ RG_MF_MAX_NEG = 8
 RG_COMM_ID_BYTES = 128
 RG_MT_PAD = 1280
 
-LOSS_KINDS = {"pointwise": 0, "bpr": 1, "hinge": 2, "adaptive_hinge": 3}
+LOSS_KINDS = {"pointwise": 0, "bpr": 1, "hinge": 2, "adaptive_hinge": 3,
+              "pointwise_pos": 4}   # implicit.py:359-360 (neg_examples=None): BCE on the positives only
 OPT_KINDS = {"adam": 0, "sgd": 1, "rms": 2}
 
 c_f32p = ctypes.POINTER(ctypes.c_float)

@@ -209,6 +209,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     const int D = a.dim;
     const int n = a.n_neg;
     const bool pairwise = (a.loss == RG_LOSS_BPR) || (a.loss == RG_LOSS_HINGE);
+    const bool negs = a.loss != RG_LOSS_POINTWISE_POS;   // no negative pool: positives only
     RG_STAMP(0);
 
     // ---- ids of every pair, prepared in processing order (one coalesced round trip) ----
@@ -217,7 +218,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     valid[0] = has_pos;
 #pragma unroll
     for (int k = 0; k < NMAX; ++k)   // flat negatives that pair with no positive only matter to pointwise / adaptive
-        valid[k + 1] = !kScoresFromBuf && active && k < n && (has_pos || !pairwise);
+        valid[k + 1] = !kScoresFromBuf && negs && active && k < n && (has_pos || !pairwise);
     // the column's record: every pair's ids and the positive's plan slot in one line
     // (the slot entry is loaded with the ids, unconditionally: issued after them it became a
     // second round trip that queued behind the gathers of the waves already past this point)
@@ -239,7 +240,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     for (int j = 0; j < TPL; ++j) {
         const int t = sub + j * LPU, q = t >> 1;
         const bool inb = t < 2 * NP && q <= n;
-        tv[j] = inb && (q == 0 ? has_pos : (!kScoresFromBuf && active && (has_pos || !pairwise)));
+        tv[j] = inb && (q == 0 ? has_pos : (!kScoresFromBuf && negs && active && (has_pos || !pairwise)));
         const int2 e = rec[inb ? q : 0];
         tu[j] = e.x & kIdMask;
         ti[j] = e.y & kIdMask;
@@ -320,7 +321,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                 if (PHASE == kAdaptBwd && sub == 0) atomicAdd(a.active_count, 1);
             }
         }
-    } else if (a.loss == RG_LOSS_POINTWISE) {
+    } else if (a.loss == RG_LOSS_POINTWISE || a.loss == RG_LOSS_POINTWISE_POS) {
         if (has_pos) {
             la = -fmaxf(logf(p[0]), -100.0f);
             dp[0] = ((p[0] - 1.0f) / fmaxf((1.0f - p[0]) * p[0], 1e-12f)) / a.n_a;
@@ -561,7 +562,8 @@ struct ApplyArgs {
     int32_t lazy_t;               // this step (absolute)
     int32_t lazy_full;            // process every user row (no next step known)
     unsigned long long *lazy_rows;   // optional: count of user rows processed (diagnostic steps)
-    int32_t lazy_dbg;             // timing experiments only (RG_LAZY_DBG; wrong results): bit 0 no catch-up
+    int32_t lazy_dbg;             // timing experiments only (RG_LAZY_DBG; wrong results): bit 0 no catch-up,
+                                  // 1 every user row processed, 2 no constants window, 3 no odd-lag reload
     int32_t lazy_cap;             // > 0: a row that has missed this many steps is processed anyway
 };
 
@@ -717,8 +719,8 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     // proc: this row is updated this step (false: a lazily skipped user row, which still runs
     // through to the wave's catch-up loop -- a wave-collective -- doing nothing)
     const int missed = lz ? (int)((int64_t)a.lazy_t - 1 - a.lazy_base - lsr) : 0;
-    const bool proc = !lz || (lzr.active && (a.lazy_full || lzr.cnt > 0 || lzr.mk == a.lazy_t + 1 ||
-                                             (a.lazy_cap > 0 && missed >= a.lazy_cap)));
+    const bool proc = !lz || (lzr.active && (a.lazy_full || (a.lazy_dbg & 2) || lzr.cnt > 0 ||
+                                             lzr.mk == a.lazy_t + 1 || (a.lazy_cap > 0 && missed >= a.lazy_cap)));
     const int cnt = proc ? lzr.cnt : 0;
     const float *src_w = a.w_in[t], *src_b = a.b_in[t];
     float p[EPL], m[EPL], v[EPL], g[EPL];
@@ -754,8 +756,9 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     }
     // the wave's catch-up window and its constants (issued with the row's loads)
     const int wmax = LAZY ? wave_max(lag) : 0;
-    const float2 wconst = (LAZY && wmax > 0) ? window_const(a, (int64_t)a.lazy_t - wmax, wmax) : make_float2(0.0f, 0.0f);
-    if (LSPEC && lz && proc && (lag & 1)) {
+    const float2 wconst = (LAZY && wmax > 0 && !(a.lazy_dbg & 4)) ? window_const(a, (int64_t)a.lazy_t - wmax, wmax)
+                                                                    : make_float2(0.0f, 0.0f);
+    if (LSPEC && lz && proc && (lag & 1) && !(a.lazy_dbg & 8)) {
         L::load(p, src_w, lr_, D, sub);
         if (sub == 0 && a.has_bias) pb = src_b[lr_];
     }
@@ -1407,10 +1410,11 @@ static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_
     if (b->n_neg < 1 || b->n_neg > kNMax) return fail_arg("rg_mf_pairs: n_neg must be in [1, 8]");
     if (b->cols <= 0 || b->n_pos < 0 || b->n_pos > b->cols) return fail_arg("rg_mf_pairs: bad n_pos/cols");
     if (b->col_offset < 0 || b->col_offset + b->cols > b->global_cols) return fail_arg("rg_mf_pairs: bad column slice");
-    if (b->global_pos <= 0 && b->loss != RG_LOSS_POINTWISE) return fail_arg("rg_mf_pairs: empty global batch");
+    if (b->global_pos <= 0 && b->loss != RG_LOSS_POINTWISE && b->loss != RG_LOSS_POINTWISE_POS)
+        return fail_arg("rg_mf_pairs: empty global batch");
     if (b->pool_len <= 0 || !b->pool || !b->words) return fail_arg("rg_mf_pairs: empty pool / no words");
     if (b->n_pos > 0 && (!b->pos_user || !b->pos_item)) return fail_arg("rg_mf_pairs: null positives");
-    if (b->loss < 0 || b->loss > RG_LOSS_ADAPTIVE_HINGE) return fail_arg("rg_mf_pairs: bad loss kind");
+    if (b->loss < 0 || b->loss > RG_LOSS_POINTWISE_POS) return fail_arg("rg_mf_pairs: bad loss kind");
     if (!w->loss_partials) return fail_arg("rg_mf_pairs: null loss_partials");
     if (backward && (!w->row_count || !w->row_list || !w->hot_grad || !w->hot_bias_grad))
         return fail_arg("rg_mf_pairs: null backward scratch");

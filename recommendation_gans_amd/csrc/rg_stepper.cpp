@@ -545,7 +545,10 @@ int train_lazy(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_
     rg_mf_batch_t nbatch{};
     rg_mf_work_t nw{};
     if (next) {
-        if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
+        // only the slot holding unit + 1: this unit is not released yet, and keeping two
+        // slots ahead of unit + 1 could overwrite its words under the adaptive-max kernel
+        // (release() below keeps the ring ahead once the pair pass is enqueued)
+        if (!st.inline_gen && (rc = generate_upto(st, unit + 1, 0))) return rc;
         if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
         if ((rc = wait_words(st, s, unit + 1))) return rc;
         nbatch = make_batch(st, *next, unit + 1);
@@ -980,8 +983,9 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         return nullptr;
     }
     st->cp_pos = (int32_t)pos;
-    // lazy dense pass: the single-rank split step (RG_LAZY=0: the eager pass, for A/B runs)
-    st->lazy = env_flag("RG_LAZY", true) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
+    // lazy dense pass (opt-in, RG_LAZY=1): the single-rank split step.  Bit-exact with the
+    // eager pass but measured slower on gfx950 (the catch-up is ALU-bound).
+    st->lazy = env_flag("RG_LAZY", false) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
     if (st->lazy) {
         const size_t ub = (size_t)cfg->tables[0].num_users * sizeof(int32_t);
         e = hipMalloc(&st->last_rel, ub);

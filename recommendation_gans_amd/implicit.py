@@ -123,11 +123,19 @@ class ImplicitFactorizationModel:
         # the reference's loss selection (implicit.py:194-199); the fused step computes the same
         # loss in its kernel, this is the function for callers that score pairs themselves
         self._loss_func = losses.bpr_loss if self._loss == "pairwise_bpr" else losses.loss_for(self._loss)
-        if not self.neg_examples:
-            raise NotImplementedError("training without a negative pool (neg_examples) is not supported")
-        self._pool = NegativePool.from_pairs(self.neg_examples)
+        # implicit.py:351-360: without a negative pool the loss sees the positives only --
+        # self._loss_func(positive_prediction) -- and no draw is taken from `random`
+        self._no_negatives = not self.neg_examples
+        if self._no_negatives:
+            if self._loss != "pointwise":   # the reference's pairwise losses need the negatives argument
+                raise TypeError(f"{self._loss_func.__name__}() missing 1 required positional argument: "
+                                f"'negative_predictions'")
+            if self._world > 1:
+                raise NotImplementedError("data-parallel training needs a negative pool")
+        self._pool = NegativePool.from_pairs([(0, 0)] if self._no_negatives else self.neg_examples)
+        engine_loss = "pointwise_pos" if self._no_negatives else _LOSS_MAP[self._loss]
         o = self._opt
-        common = dict(loss=_LOSS_MAP[self._loss], optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
+        common = dict(loss=engine_loss, optimizer=o["kind"], lr=o["lr"], weight_decay=o["weight_decay"],
                       betas=o.get("betas", (0.9, 0.999)), eps=o.get("eps", 1e-8), alpha=o.get("alpha", 0.99),
                       n_neg=self._num_negative_samples, batch_size=self._batch_size, device=dev)
         ncf_dp = {}
@@ -172,6 +180,8 @@ class ImplicitFactorizationModel:
                                     self._pool.item_ids, _mtstate.current(), **common, **dp)
         else:
             raise NotImplementedError("the fused steps train BilinearNet, the NCF MLP and NeuMF representations")
+        if self._no_negatives and self._kind != "mf":
+            raise NotImplementedError("training without a negative pool is implemented for BilinearNet")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,
@@ -266,7 +276,8 @@ class ImplicitFactorizationModel:
             if self._rank == 0:
                 save_statistics(experiment_log_dir=self.experiment_logs, filename="summary.csv", stats_dict=total,
                                 current_epoch=epoch, continue_from_mode=(self.starting_epoch != 0 or epoch > 0))
-        _mtstate.restore(e.mt_state())                 # the Python stream continues after fit
+        if not self._no_negatives:                     # the Python stream continues after fit
+            _mtstate.restore(e.mt_state())
         if self._kind == "mf":
             e.set_params(*self.best_model)
         else:

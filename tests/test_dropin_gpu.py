@@ -82,6 +82,52 @@ def test_fit_matches_reference_golden(golden_dir, tmp_path, monkeypatch, loss, i
     assert json.load(open(os.path.join(model.experiment_logs, "configuration.json")))["num_users"] == U
 
 
+def test_fit_without_negatives_matches_reference(golden_dir, tmp_path, monkeypatch):
+    """implicit.py:351-360's neg_examples=None branch (tests/golden/mf_fit_noneg_golden.npz, the
+    reference's own 2-epoch fit): the pointwise loss on the positives only (RG_LOSS_POINTWISE_POS),
+    summary.csv, best epoch, best tables, predict(3), and the `random` state untouched."""
+    from recommendation_gans_amd.implicit import ImplicitFactorizationModel
+    from recommendation_gans_amd.spotlight import optimizers
+    from recommendation_gans_amd.spotlight.factorization.representations import BilinearNet
+    from recommendation_gans_amd.spotlight.interactions import Interactions
+    f = np.load(os.path.join(golden_dir, "mf_fit_golden.npz"))
+    z = np.load(os.path.join(golden_dir, "mf_fit_noneg_golden.npz"))
+    U, I, d, B, n = (int(x) for x in z["meta"])
+    train = Interactions(f["train_u"].astype(np.int32), f["train_i"].astype(np.int32),
+                         ratings=np.ones(len(f["train_u"]), np.float32), num_users=U, num_items=I)
+    valid = Interactions(f["valid_u"].astype(np.int32), f["valid_i"].astype(np.int32),
+                         ratings=np.ones(len(f["valid_u"]), np.float32), num_users=U, num_items=I)
+    net = BilinearNet(U, I, d)
+    with torch.no_grad():
+        net.user_embeddings.weight.copy_(torch.from_numpy(z["init_U"]))
+        net.item_embeddings.weight.copy_(torch.from_numpy(z["init_I"]))
+    random.seed(0)
+    monkeypatch.chdir(tmp_path)
+    model = ImplicitFactorizationModel(loss="pointwise", embedding_dim=d, n_iter=2, batch_size=B, l2=1e-5,
+                                       learning_rate=1e-2, optimizer_func=optimizers.adam_optimizer,
+                                       representation=net, random_state=np.random.RandomState(0),
+                                       neg_examples=None, num_negative_samples=n, use_cuda=True)
+    model.fit(train, valid)
+    assert (np.array(random.getstate()[1], np.uint32) == z["mt_state_end"]).all()
+    assert (z["mt_state_end"] == z["mt_state"]).all()
+    assert model.best_epoch == int(z["best_epoch"][0])
+    got = list(csv.reader(open(os.path.join(model.experiment_logs, "summary.csv"))))
+    ref = list(csv.reader(io.StringIO(str(z["summary_csv"]))))
+    assert got[0] == ref[0] and len(got) == len(ref)
+    for g, r in zip(got[1:], ref[1:]):
+        np.testing.assert_allclose([float(x) for x in g], [float(x) for x in r], rtol=1e-5)
+    names = ["user_embeddings_weight", "item_embeddings_weight", "user_biases_weight", "item_biases_weight"]
+    for t, nm in zip(model.best_model, names):
+        ref_t = torch.from_numpy(z[f"best_{nm}"])
+        ok, msg = omf.tensor_parity(t.reshape(ref_t.shape), ref_t, rtol=1e-5)
+        assert ok, (nm, msg)
+    np.testing.assert_allclose(model.predict(3), z["predict_u3"], rtol=1e-5, atol=1e-7)
+    # the pairwise losses need the negatives argument, as in the reference
+    with pytest.raises(TypeError):
+        ImplicitFactorizationModel(loss="hinge", embedding_dim=d, n_iter=1, batch_size=B, representation=BilinearNet(
+            U, I, d), neg_examples=None, use_cuda=True).fit(train, valid)
+
+
 def test_mf_spotlight_cli_synthetic(tmp_path, monkeypatch):
     from recommendation_gans_amd import mf_spotlight
     monkeypatch.chdir(tmp_path)

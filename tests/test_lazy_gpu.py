@@ -84,7 +84,8 @@ def _same(a, b, what):
 
 @pytest.mark.parametrize("loss,opt,d", [("bpr", "adam", 64), ("pointwise", "adam", 32), ("hinge", "rms", 64),
                                         ("adaptive_hinge", "adam", 64), ("bpr", "sgd", 128),
-                                        ("pointwise", "adam", 50), ("bpr", "adam", 8)])
+                                        ("pointwise", "adam", 50), ("bpr", "adam", 8),
+                                        ("adaptive_hinge", "adam", 8)])
 def test_lazy_equals_eager_bitwise(dev, loss, opt, d):
     U, I, B, n = 3000, 400, 256, 5
     tabs, pool_u, pool_i, steps = _case(U, I, d, B, 14, 20000, seed=d + len(loss))
@@ -99,6 +100,56 @@ def test_lazy_equals_eager_bitwise(dev, loss, opt, d):
     assert (mtl == mte).all()
     # the lazy path really skipped rows: fewer user rows than U per step
     assert rows is not None and 0 < rows < U * len(steps), rows
+
+
+def _fit_like(dev, lazy, loss, epochs=3, val=True):
+    """implicit.py's fit loop on the fit golden's problem (U 30, I 20, d 8, B 32): the step
+    inputs built once and replayed every epoch, the last step of an epoch without a next
+    step, validation batches and a params() snapshot between epochs."""
+    from recommendation_gans_amd.mf_engine import MFEngine
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "mf_fit_golden.npz"))
+    U, I, d, B, n = (int(x) for x in z["meta"])
+    key = loss if f"{loss}_init_U" in z else "pointwise"
+    tabs = [torch.from_numpy(z[f"{key}_init_U"]), torch.from_numpy(z[f"{key}_init_I"]), torch.zeros(U),
+            torch.zeros(I)]
+    old = os.environ.get("RG_LAZY")
+    os.environ["RG_LAZY"] = "1" if lazy else "0"
+    try:
+        e = MFEngine(*tabs, z["pool_u"], z["pool_i"], z[f"{key}_mt_state"].copy(), loss=loss, optimizer="adam",
+                     lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev)
+    finally:
+        if old is None:
+            del os.environ["RG_LAZY"]
+        else:
+            os.environ["RG_LAZY"] = old
+    tu, ti = (torch.from_numpy(z[k].astype(np.int64)).to(dev) for k in ("train_u", "train_i"))
+    vu, vi = (torch.from_numpy(z[k].astype(np.int64)).to(dev) for k in ("valid_u", "valid_i"))
+    nb = (len(tu) + B - 1) // B
+    plans = e.make_plans(ti)
+    ins = [e.step_input(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], None, plans[s]) for s in range(nb)]
+    losses, vals, snaps = [], [], []
+    for _ in range(epochs):
+        for s in range(nb):
+            out = torch.zeros(1, dtype=torch.float32, device=dev)
+            e.train_step_in(ins[s], ins[s + 1] if s + 1 < nb else None, loss_out=out)
+            losses.append(out)
+        if val:
+            vals += [float(e.val_loss(vu[s:s + B], vi[s:s + B])[0]) for s in range(0, len(vu), B)]
+        snaps.append([t.clone().cpu() for t in e.params()])
+    return torch.cat(losses).cpu(), vals, snaps, e.mt_state()
+
+
+@pytest.mark.parametrize("loss", ["pointwise", "adaptive_hinge"])
+def test_lazy_fit_loop_equals_eager(dev, loss):
+    le, ve, se, mte = _fit_like(dev, False, loss)
+    ll, vl, sl, mtl = _fit_like(dev, True, loss)
+    bad = [k for k in range(len(le)) if le[k] != ll[k]]
+    assert not bad, f"steps {bad} differ: eager {le.tolist()} lazy {ll.tolist()}"
+    assert vl == ve, (vl, ve)
+    for ep, (a, b) in enumerate(zip(sl, se)):
+        for k in range(4):
+            _same(a[k], b[k], f"epoch {ep} table {k}")
+    assert (mtl == mte).all()
 
 
 def test_lazy_without_plan_and_two_flushes(dev):
