@@ -118,7 +118,15 @@ typedef struct rg_mf_batch {
  *                         item inside one block of U positions share a slot; slots are
  *                         numbered in position order
  *   plan_item_slot_off[i] item i's slots are [off[i], off[i+1])  (num_items + 1 entries)
- * part_row / part_bias: [slots * dim] / [slots] partial sums (slots <= cols). */
+ * part_row / part_bias: [slots * dim] / [slots] partial sums (slots <= cols).
+ *
+ * claim_num_users > 0 (= the tables' num_users; split step, not the adaptive hinge;
+ * num_users, num_items < 2^27):
+ * rg_mf_prepare claims every valid pair's list slots in row_count (one atomic per row
+ * side) and stores them in bits 27-30 of the prepared ids, so rg_mf_pairs writes its
+ * list entries at those slots without returning atomics.  The prepare of step t + 1
+ * runs inside step t's dense pass, which resets step t's counts: consecutive steps
+ * then need separate row_count arrays (the stepper alternates two). */
 typedef struct rg_mf_work {
     int32_t *row_count;      /* [num_users + num_items] */
     int32_t *row_list;       /* [(num_users + num_items) * RG_MF_LIST_CAP * 2] {other row, dz bits} */
@@ -131,6 +139,7 @@ typedef struct rg_mf_work {
     int32_t *active_count;   /* [1] (adaptive hinge only) */
     const int32_t *plan_perm, *plan_pos_slot, *plan_item_slot_off;
     float *part_row, *part_bias;
+    int64_t claim_num_users; /* see above; 0: the pair pass claims list slots itself */
 } rg_mf_work_t;
 
 /* Loss reduction requested from rg_mf_apply / rg_mf_grads:

@@ -54,7 +54,7 @@ class MFWork(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "row_count", "row_list", "hot_grad", "hot_bias_grad", "loss_partials", "scores",
         "max_key", "active_count", "plan_perm", "plan_pos_slot", "plan_item_slot_off",
-        "part_row", "part_bias")]
+        "part_row", "part_bias")] + [("claim_num_users", ctypes.c_int64)]
 
 
 class MFMark(ctypes.Structure):

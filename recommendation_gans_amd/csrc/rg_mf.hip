@@ -75,6 +75,9 @@ struct PairsArgs {
     int32_t serial;
     int32_t *umark;            // prepare (lazy dense pass): umark[user] = umark_step for every pair's user
     int32_t umark_step;
+    // claimed list slots (rg_mf_work_t claim_num_users): the prepare claims them in row_count and
+    // stores them in the ids' bits 27-30; the pair pass reads them instead of claiming
+    int32_t claimed;
 };
 
 // Prepared ids carry ownership flags in bit 31 when the prepare pass stamped rows:
@@ -82,6 +85,9 @@ struct PairsArgs {
 // the hot-row apply (mf_hot_kernel) updates each touched row through its owner only.
 constexpr int32_t kOwnerBit = (int32_t)0x80000000;
 constexpr int32_t kIdMask = 0x7fffffff;
+// claimed records: slot min(slot, kCap) of the row side in bits 27-30 of its id
+constexpr int kSlotShift = 27;
+constexpr int32_t kClaimIdMask = (1 << kSlotShift) - 1;
 
 // Diagnostic build only (RG_DIAG_STAMPS, librg_hip_diag.so; scripts/mf_pairs_stamps.py):
 // per-wave s_memrealtime stamps at the pair pass's phase boundaries, each after a full
@@ -137,6 +143,20 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         r = a.pool[choice_index(w.x, w.y, a.pool_len)];
     }
     if (a.umark != nullptr) a.umark[r.x] = a.umark_step;   // plain store: every writer stores the same value
+    if (a.claimed) {
+        // the list slots the pair pass would claim (pairs_body's validity): the positive if the
+        // position has one, a negative if its column pairs with a positive or the loss is
+        // pointwise; the planned positives' item side is reduced in LDS instead
+        const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
+        const bool v = q == 0 ? s < a.n_pos : (a.loss != RG_LOSS_POINTWISE_POS && (s < a.n_pos || !pairwise));
+        if (v) {
+            const int su = atomicAdd(a.row_count + r.x, 1);
+            const bool item_side = !(q == 0 && a.pos_slot != nullptr);
+            const int si = item_side ? atomicAdd(a.row_count + a.num_users + r.y, 1) : 0;
+            r.x |= (su < kCap ? su : kCap) << kSlotShift;
+            r.y |= (si < kCap ? si : kCap) << kSlotShift;
+        }
+    }
     if (a.stamp != nullptr) {
         const int32_t ou = atomicExch(a.stamp + r.x, a.serial);
         const int32_t oi = atomicExch(a.stamp + a.num_users + r.y, a.serial);
@@ -224,11 +244,13 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     // second round trip that queued behind the gathers of the waves already past this point)
     const int2 *rec = a.pairs + (active ? s : 0) * (int64_t)pair_stride(n);
     const int2 slot_entry = rec[n + 1];
+    const bool claimed = kBackward && a.claimed;
+    const int32_t idm = a.claimed ? kClaimIdMask : kIdMask;   // drop the ownership flags / slots
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const int2 pr = rec[(valid[q] || q == 0) ? q : 0];
-        uid[q] = pr.x & kIdMask;     // drop the ownership flags
-        iid[q] = pr.y & kIdMask;
+        uid[q] = pr.x & idm;
+        iid[q] = pr.y & idm;
     }
     const int myslot = (kBackward && plan && has_pos) ? slot_entry.x : -1;
     // each list task's own pair, loaded from the record beside the ids: indexing uid[] /
@@ -236,25 +258,25 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     // per-thread LDS array (18 KB per workgroup), which slowed this whole phase ~10x
     int tu[TPL], ti[TPL];
     bool tv[TPL];
+    int slot[TPL];
 #pragma unroll
     for (int j = 0; j < TPL; ++j) {
         const int t = sub + j * LPU, q = t >> 1;
         const bool inb = t < 2 * NP && q <= n;
         tv[j] = inb && (q == 0 ? has_pos : (!kScoresFromBuf && negs && active && (has_pos || !pairwise)));
         const int2 e = rec[inb ? q : 0];
-        tu[j] = e.x & kIdMask;
-        ti[j] = e.y & kIdMask;
+        tu[j] = e.x & idm;
+        ti[j] = e.y & idm;
+        slot[j] = claimed ? (int)(((uint32_t)((t & 1) ? e.y : e.x) >> kSlotShift) & 15u) : 0;
     }
     RG_STAMP(1);
     if (RG_DIAG_FLAG(3)) return;
 
     // ---- claim list slots early (their latency hides under the gathers) -------
-    int slot[TPL];
 #pragma unroll
     for (int j = 0; j < TPL; ++j) {
-        slot[j] = 0;
         const int t = sub + j * LPU;
-        if (kBackward && t < 2 * NP && !(plan && t == 1)) {
+        if (kBackward && !claimed && t < 2 * NP && !(plan && t == 1)) {
             if (tv[j] && !RG_DIAG_FLAG(0)) {
                 const int64_t row = (t & 1) ? a.num_users + ti[j] : (int64_t)tu[j];
                 slot[j] = atomicAdd(a.row_count + row, 1);
@@ -1458,6 +1480,12 @@ static int pairs_args(const rg_mf_tables_t *t, const rg_mf_batch_t *b, const rg_
     a.perm = w->plan_perm;
     a.pos_slot = backward ? w->plan_pos_slot : nullptr;   // partials only in the backward pass
     a.part_row = w->part_row; a.part_bias = w->part_bias;
+    if (w->claim_num_users > 0) {
+        if (w->claim_num_users != t->num_users || t->num_users >= kClaimIdMask || t->num_items >= kClaimIdMask)
+            return fail_arg("rg_mf_pairs: claimed slots need claim_num_users == num_users and ids < 2^27");
+        if (adaptive) return fail_arg("rg_mf_pairs: no claimed slots for the adaptive hinge");
+        a.claimed = 1;
+    }
     return RG_OK;
 }
 
@@ -1487,10 +1515,21 @@ static int prepare_args(const rg_mf_batch_t *b, const rg_mf_work_t *w, const rg_
     a.pool_len = b->pool_len; a.n_neg = b->n_neg;
     a.perm = w ? w->plan_perm : nullptr;
     a.pos_slot = w ? w->plan_pos_slot : nullptr;
+    a.loss = b->loss;
     if (mark) {
         a.stamp = mark->stamp;
         a.serial = mark->serial;
         a.num_users = mark->num_users;
+    }
+    if (w && w->claim_num_users > 0) {
+        if (mark) return fail_arg("rg_mf_prepare: claimed slots and row marks are exclusive");
+        if (!w->row_count) return fail_arg("rg_mf_prepare: claimed slots need row_count");
+        if (b->loss == RG_LOSS_ADAPTIVE_HINGE)
+            return fail_arg("rg_mf_prepare: no claimed slots for the adaptive hinge (its lists follow the max)");
+        a.claimed = 1;
+        a.row_count = w->row_count;
+        if (w->claim_num_users >= kClaimIdMask) return fail_arg("rg_mf_prepare: claimed slots need ids < 2^27");
+        a.num_users = w->claim_num_users;
     }
     return RG_OK;
 }

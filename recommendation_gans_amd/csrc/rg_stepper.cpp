@@ -115,6 +115,14 @@ struct Stepper {
     int64_t n_consts = 0;
     uint64_t *rows_done = nullptr;        // diagnostic counter (rg_mf_stepper_lazy_count)
     bool count_rows = false;
+    // claimed list slots (single-rank split step, rg_mf_work_t claim_num_users): the prepare of
+    // unit u claims in counts[u % 2] (cfg.work.row_count and a second array owned here), so the
+    // next unit's claims never meet the dense pass that reads and resets this unit's counts
+    bool claim = false;
+    int32_t *counts[2] = {nullptr, nullptr};
+    int32_t *own_counts = nullptr;
+    bool count_dirty[2] = {false, false};  // counts[b] hold claims no dense pass consumed yet
+    bool prep_claimed = false;             // the prepared pairs carry claimed slots
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -158,6 +166,27 @@ rg_mf_work_t work_for(const Stepper &st, const rg_mf_step_in_t &in) {
     rg_mf_work_t w = st.cfg.work;
     set_plan(w, in);
     return w;
+}
+
+// the scratch of training unit `unit` (claimed slots: its parity's count array)
+rg_mf_work_t train_work(const Stepper &st, const rg_mf_step_in_t &in, int64_t unit) {
+    rg_mf_work_t w = work_for(st, in);
+    if (st.claim) {
+        w.row_count = st.counts[unit % 2];
+        w.claim_num_users = st.cfg.tables[0].num_users;
+    }
+    return w;
+}
+
+// before a claiming prepare into counts[b]: drop claims a dense pass never consumed (a
+// prefetched step that did not run, or ran as validation)
+int clean_counts(Stepper &st, hipStream_t s, int b) {
+    if (!st.claim || !st.count_dirty[b]) return RG_OK;
+    const rg_mf_tables_t &t = st.cfg.tables[0];
+    hipError_t e = hipMemsetAsync(st.counts[b], 0, (size_t)(t.num_users + t.num_items) * sizeof(int32_t), s);
+    if (e != hipSuccess) return hip_fail("stepper: reset claimed counts", e);
+    st.count_dirty[b] = false;
+    return RG_OK;
 }
 
 bool same_input(const rg_mf_step_in_t &a, const rg_mf_step_in_t &b) {
@@ -282,6 +311,7 @@ int prepare_side(Stepper &st, hipStream_t consumer, int64_t unit, const rg_mf_st
     st.prep_unit = unit;
     st.prep_in = in;
     st.prep_serial = 0;
+    st.prep_claimed = false;
     return RG_OK;
 }
 
@@ -334,7 +364,9 @@ int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t 
     if (rc) return rc;
     rc = keep_ahead(st, unit);
     if (rc) return rc;
-    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, in))) {
+    // an external consumer's pair pass claims in cfg.work.row_count (= counts[0]) by itself
+    if ((rc = clean_counts(st, stream, 0))) return rc;
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, in) && !st.prep_claimed)) {
         if ((rc = prepare_side(st, stream, unit, in))) return rc;
     }
     if ((rc = wait_side(st, stream, (int)(unit % 2)))) return rc;
@@ -445,16 +477,19 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     // validation pass); unit t+2 is walked inside this step's dense pass
     int rc = st.inline_gen ? generate_upto(st, unit + 1, 0) : keep_ahead(st, unit);
     if (rc) return rc;
-    rg_mf_work_t w = work_for(st, cur);
+    rg_mf_work_t w = train_work(st, cur, unit);
     const rg_mf_batch_t batch = make_batch(st, cur, unit);
     if ((rc = wait_side(st, s, (int)(unit % 2)))) return rc;      // a side prepare (acquire path) of this buffer
-    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
+    if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur) && st.prep_claimed == st.claim)) {
         if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = clean_counts(st, s, (int)(unit % 2)))) return rc;
         if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+        st.count_dirty[unit % 2] = st.claim;
         st.prepared = true;
         st.prep_unit = unit;
         st.prep_in = cur;
         st.prep_serial = 0;
+        st.prep_claimed = st.claim;
     }
     if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = wait_words(st, s, unit))) return rc;   // adapt-max reads them
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
@@ -466,8 +501,9 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
         if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
         if ((rc = wait_words(st, s, unit + 1))) return rc;
+        if ((rc = clean_counts(st, s, (int)((unit + 1) % 2)))) return rc;
         nbatch = make_batch(st, *next, unit + 1);
-        nw = work_for(st, *next);
+        nw = train_work(st, *next, unit + 1);
     }
     rg_mt_gen_t gen{};
     int gen_slot = -1;
@@ -499,11 +535,14 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
         if ((rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out))) return rc;
     }
+    st.count_dirty[unit % 2] = false;           // the dense pass consumed (and reset) this unit's claims
     if (next) {
+        st.count_dirty[(unit + 1) % 2] = st.claim;
         st.prepared = true;
         st.prep_unit = unit + 1;
         st.prep_in = *next;
         st.prep_serial = 0;
+        st.prep_claimed = st.claim;
     }
     st.set = 1 - st.set;
     return RG_OK;
@@ -893,6 +932,7 @@ void destroy(Stepper *st) {
     if (st->umark) hipFree(st->umark);
     if (st->consts) hipFree(st->consts);
     if (st->rows_done) hipFree(st->rows_done);
+    if (st->own_counts) hipFree(st->own_counts);
     if (st->own_back) hipEventDestroy(st->own_back);
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
@@ -1001,6 +1041,25 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
             return nullptr;
         }
         st->lazy_base = cfg->step;
+    }
+    // claimed list slots: the single-rank eager split step (RG_MF_CLAIM=0: the pair pass
+    // claims its slots with returning atomics, as before)
+    const rg_mf_tables_t &t0 = cfg->tables[0];
+    st->claim = env_flag("RG_MF_CLAIM", true) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused && !st->lazy &&
+                cfg->loss != RG_LOSS_ADAPTIVE_HINGE && cfg->work.row_count != nullptr &&
+                t0.num_users < ((int64_t)1 << 27) && t0.num_items < ((int64_t)1 << 27);
+    if (st->claim) {
+        const size_t cb = (size_t)(t0.num_users + t0.num_items) * sizeof(int32_t);
+        e = hipMalloc(&st->own_counts, cb);
+        if (e == hipSuccess) e = hipMemset(st->own_counts, 0, cb);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            hip_fail("rg_mf_stepper_create: claimed counts", e);
+            destroy(st);
+            return nullptr;
+        }
+        st->counts[0] = cfg->work.row_count;
+        st->counts[1] = st->own_counts;
     }
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
@@ -1138,7 +1197,8 @@ extern "C" int rg_mf_stepper_release(void *h, void *stream) {
 extern "C" int rg_mf_stepper_prefetch(void *h, void *stream, const rg_mf_step_in_t *next) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !next) return rg::fail_arg("rg_mf_stepper_prefetch: null argument");
-    if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next)) return RG_OK;
+    if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next) && !st->prep_claimed)
+        return RG_OK;
     return prepare_side(*st, (hipStream_t)stream, st->taken, *next);
 }
 

@@ -73,7 +73,7 @@ def test_mf_full_size_steps(ml20m, d, loss):
         assert (e.mt_state() == o.state).all(), f"d{d} step {s}: MT state"
         # the consumed pairs (item-plan order): negatives as a multiset per column = random.choices' draw
         perm = ins[s]._keep[2].perm.cpu().numpy()
-        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].cpu().numpy() & 0x7FFFFFFF      # [position][q]
+        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].cpu().numpy() & 0x07FFFFFF      # [position][q], minus flags / claimed slots
         nu = out["neg_u"].numpy().reshape(n, B)[:, perm].T
         ni = out["neg_i"].numpy().reshape(n, B)[:, perm].T
         assert (pr[..., 0] == nu).all() and (pr[..., 1] == ni).all(), f"d{d} step {s}: negatives"

@@ -116,7 +116,7 @@ def _gs_collect(e, inputs, rank, step_fn):
         if planned:
             negs.append(None)
         else:                                                    # the buffer this step consumed
-            pr = e.pairs[k % 2].view(dc.B, S, 2)[:, 1:1 + dc.N_NEG].transpose(0, 1).cpu().numpy() & 0x7FFFFFFF
+            pr = e.pairs[k % 2].view(dc.B, S, 2)[:, 1:1 + dc.N_NEG].transpose(0, 1).cpu().numpy() & 0x07FFFFFF
             negs.append((pr[..., 0], pr[..., 1]))
     torch.cuda.synchronize()
     return [p.cpu().clone() for p in e.params()], losses, states, negs

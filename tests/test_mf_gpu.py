@@ -474,7 +474,7 @@ def test_full_size_sampler_steps(dev, n, jump, monkeypatch):
         found = False
         for buf in e.pairs:
             S = 8 if n + 2 <= 8 else 16                              # per-column records (rg_mf_pairs_len)
-            pr = buf.view(B, S, 2)[:, :1 + n].transpose(0, 1).cpu().numpy() & 0x7FFFFFFF   # minus ownership flags
+            pr = buf.view(B, S, 2)[:, :1 + n].transpose(0, 1).cpu().numpy() & 0x07FFFFFF   # minus ownership flags / claimed slots (bits 27-31)
             if (pr[1:, :, 0].reshape(-1) == out["neg_u"].numpy()).all() and \
                (pr[1:, :, 1].reshape(-1) == out["neg_i"].numpy()).all():
                 found = True
@@ -518,7 +518,7 @@ def test_dp_rank_slice_sampler_full_size(dev, rank):
     for s in range(9):
         e.train_step_exchange(ins[s], ins[s + 1], none, none)
         idx = orng.py_choices_indices(ref, len(pool_u), n * B * world).reshape(n, B * world)[:, rank * B:(rank + 1) * B]
-        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].transpose(0, 1).cpu().numpy() & 0x7FFFFFFF
+        pr = e.pairs[s % 2].view(B, 8, 2)[:, 1:1 + n].transpose(0, 1).cpu().numpy() & 0x07FFFFFF
         assert (pr[..., 0] == pool_u[idx]).all() and (pr[..., 1] == pool_i[idx]).all(), f"step {s} negatives"
         assert (e.mt_state() == ref).all(), f"step {s} MT state"
 
