@@ -764,7 +764,7 @@ def main():
         eng.flush()
 
     if emu is not None:
-        return report_emulated(args, emu, eng, evs, el, U, I, d, B, n)
+        return report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq)
     if rank == 0:
         value = args.steps * B * world / el
         # per rank: its user shard + every item go through the dense optimizer pass
@@ -863,7 +863,7 @@ def main():
         dist.destroy_process_group()
 
 
-def report_emulated(args, emu, eng, evs, el, U, I, d, B, n):
+def report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq):
     """--emulate-rank: one JSON line for rank R's step at W-rank geometry (NOT the driver's
     metric line): its time per step, the user-update kernel's events, and what W ranks each
     taking this step time would process (exchange time over xGMI NOT included: the
@@ -884,6 +884,9 @@ def report_emulated(args, emu, eng, evs, el, U, I, d, B, n):
            "exchange_floats_per_step": {"scores": (1 + n) * B * w_ if args.loss != "pointwise" else 0,
                                         "item_grad": I * (d + 1) + 1},
            "user_update_us": float(np.mean(ev)) * 1e3 if ev else None,
+           # host time to enqueue a step (Python + the stepper's HIP calls): close to the step
+           # time means the GPU waits for the host
+           "host_enqueue_us_per_step": t_enq / args.steps * 1e6,
            "final_loss": float(eng.loss_out[0])}
     print(json.dumps(out), flush=True)
     eng.comm.close()

@@ -118,6 +118,19 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
 
 hipStream_t comm_stream(void *h) { return h ? static_cast<Comm *>(h)->stream : nullptr; }
 
+int comm_allreduce_on(void *h, hipStream_t stream, float *buf, int64_t n) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c || !buf || n < 0) return fail_arg("rg_comm allreduce: bad argument");
+    if (c->host_fn) {                      // staged through the host on the communicator stream
+        const int rc = comm_begin(h, stream, buf, n);
+        return rc ? rc : comm_end(h, stream);
+    }
+    if (c->local) return local_roundtrip(c, stream, buf, n);
+    if (c->world == 1) return RG_OK;       // a one-rank sum is the buffer itself: no RCCL launch
+    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, stream);
+    return r == ncclSuccess ? RG_OK : nccl_fail("ncclAllReduce", r);
+}
+
 int comm_end(void *h, hipStream_t stream) {
     Comm *c = static_cast<Comm *>(h);
     if (!c) return fail_arg("rg_comm_allreduce_end: null communicator");

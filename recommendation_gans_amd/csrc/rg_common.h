@@ -28,6 +28,8 @@ int comm_end(void *comm, hipStream_t stream);
 int comm_reduce_scatter(void *comm, hipStream_t stream, float *buf, int64_t chunk);
 int comm_allgather(void *comm, hipStream_t stream, int n, float *const *bufs, const int64_t *counts);
 hipStream_t comm_stream(void *comm);   // the communicator's own stream
+// the all-reduce enqueued on `stream` itself (no cross-stream events; host mode: begin + end)
+int comm_allreduce_on(void *comm, hipStream_t stream, float *buf, int64_t n);
 
 // ---------------------------------------------------------------- MT jump-ahead
 // One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,

@@ -666,6 +666,47 @@ __device__ __forceinline__ float finalize_loss(const float *__restrict__ partial
     return (float)(sa * inv_a + sb * inv_b);
 }
 
+// The same loss over a whole workgroup (every thread of it calls this; every thread gets
+// the value): a data-parallel step's backward leaves thousands of partials, which one wave
+// reads in ~6 dependent rounds -- a floor under the short launch that finalizes them.
+// Fixed partition and combine order: deterministic.
+template <int NT>
+__device__ __forceinline__ float finalize_loss_wg(const float *__restrict__ partials, int64_t np_, double inv_a,
+                                                  double inv_b) {
+    constexpr int kU = 8, NW = NT / kWave;
+    __shared__ double red[2][NW];
+    __shared__ float out;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    double sa = 0.0, sb = 0.0;
+    for (int64_t i0 = tid; i0 < np_; i0 += (int64_t)kU * NT) {
+        float2 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + (int64_t)u * NT;
+            v[u] = i < np_ ? reinterpret_cast<const float2 *>(partials)[i] : make_float2(0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            sa += (double)v[u].x;
+            sb += (double)v[u].y;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sa += __shfl_xor(sa, off);
+        sb += __shfl_xor(sb, off);
+    }
+    if (lane == 0) { red[0][w] = sa; red[1][w] = sb; }
+    __syncthreads();
+    if (tid == 0) {
+        double ta = 0.0, tb = 0.0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) { ta += red[0][k]; tb += red[1][k]; }
+        out = (float)(ta * inv_a + tb * inv_b);
+    }
+    __syncthreads();
+    return out;
+}
+
 // Gradient + optimizer update of unified row r (users [0, U), items [U, U + I)).
 // COLD: a row no pair of the step touches -- its data gradient is exactly zero
 // (only the coupled weight decay acts), so nothing of the step's scratch is read.
@@ -835,6 +876,22 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             }
             if (t == 1 && a.item_slot_off != nullptr) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
         }
+        // kGradOnly (the data-parallel item gradient: a short, latency-bound launch over rows
+        // that are nearly all touched): every load of the row -- all partner rows, the
+        // overflow accumulators, the first planned partials -- issues in ONE round trip after
+        // the list instead of a dependent chain; the sums keep their order (same bits)
+        constexpr bool kOneTrip = MODE == kGradOnly && SPEC;
+        float h0[kOneTrip ? 4 : 1][EPL];
+        float hb0[kOneTrip ? 4 : 1];
+        const bool parts = t == 1 && a.item_slot_off != nullptr;
+        if (kOneTrip && parts && s1 > s0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ss = s0 + u < s1 ? s0 + u : s0;
+                L::load(h0[kOneTrip ? u : 0], a.part_row, ss, D, sub);
+                hb0[kOneTrip ? u : 0] = a.has_bias ? a.part_bias[ss] : 0.0f;
+            }
+        }
         if (c > 0) {
             const int ne = c < kCap ? c : kCap;
             int2 ent[kCap];
@@ -854,13 +911,23 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             // partner rows in groups of PG list entries (RG_MF_PULL_GROUP; most touched rows have
             // 1-2 entries): a later group's gathers issue only when some row of the wave needs them,
             // and the smaller register footprint raises occupancy
-            constexpr int PG = RG_MF_PULL_GROUP;
+            constexpr int PG = kOneTrip ? kCap : RG_MF_PULL_GROUP;
             // an overflowed row (c > kCap) sums list and surplus in fixed point (see fix_add)
             const bool fixp = c > kCap;
             long long gf[EPL];
             long long gbf = 0;
 #pragma unroll
             for (int q = 0; q < EPL; ++q) gf[q] = 0;
+            long long hv[kOneTrip ? EPL : 1];
+            long long hbv = 0;
+            if (kOneTrip && fixp) {     // the surplus' accumulators, loaded with the partner rows
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int cc = L::elem(sub, e);
+                    hv[kOneTrip ? e : 0] = (L::VEC || cc < D) ? a.hot_grad[r * (int64_t)D + cc] : 0;
+                }
+                if (sub == 0 && a.has_bias) hbv = a.hot_bias_grad[r];
+            }
 #pragma unroll
             for (int h = 0; h < kCap / PG; ++h) {
                 if (h > 0 && !__any(ne > h * PG)) break;
@@ -886,34 +953,48 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
                     }
                 }
             }
+#ifdef RG_X_NOOVF   // timing experiments only (wrong results): overflowed rows skip their accumulators
+            if (false) {
+#else
             if (fixp) {
+#endif
                 // the surplus' accumulators (fixed point), read and reset
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
                     const int cc = L::elem(sub, e);
                     if (L::VEC || cc < D) {
                         long long *hp = a.hot_grad + r * (int64_t)D + cc;
-                        gf[e] += *hp;
+                        gf[e] += kOneTrip ? hv[kOneTrip ? e : 0] : *hp;
                         *hp = 0;
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < EPL; ++q) g[q] = from_fix(gf[q]);
                 if (sub == 0 && a.has_bias) {
-                    gbf += a.hot_bias_grad[r];
+                    gbf += kOneTrip ? hbv : a.hot_bias_grad[r];
                     a.hot_bias_grad[r] = 0;
                 }
                 gb = from_fix(gbf);
             }
             if (sub == 0 && !a.keep_count) a.row_count[r] = 0;
         }
-        if (t == 1 && a.item_slot_off != nullptr) {   // planned positive partials of this item
+#ifdef RG_X_NOPART  // timing experiments only (wrong results): no planned partials
+        if (false) {
+#else
+        if (parts) {   // planned positive partials of this item
+#endif
             if (!SPEC || lz) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
             for (int sl = s0; sl < s1; sl += 4) {
                 float h[4][EPL];
                 float hb[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
+                    if (kOneTrip && sl == s0) {        // the first four, loaded beside the partner rows
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q) h[u][q] = h0[kOneTrip ? u : 0][q];
+                        hb[u] = hb0[kOneTrip ? u : 0];
+                        continue;
+                    }
                     const int ss = sl + u < s1 ? sl + u : s0;
                     L::load(h[u], a.part_row, ss, D, sub);
                     hb[u] = a.has_bias ? a.part_bias[ss] : 0.0f;
@@ -1032,13 +1113,15 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
     const int D = a.dim;
 
     const int64_t slot_off = (a.shard_users + a.shard_items) * (int64_t)(D + 1);   // loss slot in a chunk
-    if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x < kWave) {
-        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
-        if (lane == 0) *a.loss_out = lv;
-        if (MODE == kGradOnly && a.shard_users > 0) {
-            for (int s = lane; s < a.world; s += kWave) a.grad[s * a.chunk + slot_off] = lv;   // summed by the RS
-        } else if (MODE == kGradOnly && lane == 0) {
-            a.grad[nr * (int64_t)(D + 1)] = lv;
+    if (MODE != kApplyDense && a.loss_out != nullptr && blockIdx.x == 0) {
+        const float lv = finalize_loss_wg<kBlock>(a.partials, a.n_partials, a.inv_a, a.inv_b);
+        if (threadIdx.x < kWave) {
+            if (lane == 0) *a.loss_out = lv;
+            if (MODE == kGradOnly && a.shard_users > 0) {
+                for (int s = lane; s < a.world; s += kWave) a.grad[s * a.chunk + slot_off] = lv;   // summed by the RS
+            } else if (MODE == kGradOnly && lane == 0) {
+                a.grad[nr * (int64_t)(D + 1)] = lv;
+            }
         }
     }
     if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)

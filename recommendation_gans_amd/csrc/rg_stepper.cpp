@@ -105,6 +105,8 @@ struct Stepper {
     int64_t own_unit = -1;
     int own_stage = 0;                    // 0 idle, 1 after begin, 2 after mid
     hipEvent_t own_back = nullptr;        // after the owner backward (the item gradient may start)
+    hipEvent_t own_grads = nullptr;       // train_owner: the lists are pulled (the user update may start)
+    hipEvent_t own_users = nullptr;       // train_owner: the user update is done (the next step may start)
     // lazy dense pass (single-rank split step): deferred cold user-row updates
     bool lazy = false;
     bool lazy_pending = false;            // some user rows lag the current step
@@ -815,9 +817,12 @@ int owner_item_update(Stepper &st, hipStream_t s, const rg_opt_t &o, float *loss
     return RG_OK;
 }
 
-// the whole owner-sharded step with the communicator: begin -> score all-reduce (not for
-// pointwise: no pairing) -> backward; then the item gradient and its all-reduce on the
-// communicator stream beside the user update (+ next prepare) -> item update
+// the whole owner-sharded step with the communicator.  The critical path stays on the
+// caller's stream s with the collectives enqueued on s itself (no cross-stream hop):
+//   s: scores -> score all-reduce (not for pointwise: no pairing) -> backward -> item
+//      gradient -> item-gradient all-reduce -> item update -> [wait for the user update]
+//   u: (after the item gradient) the user update + the next step's owner prepare
+// The user update (communicator stream u) runs beside the item-gradient exchange.
 int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next, float *loss_out,
                 void *ev0, void *ev1) {
     int rc = owner_begin(st, s, cur);
@@ -825,20 +830,32 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     if (st.cfg.loss != RG_LOSS_POINTWISE) {
         const int64_t len = (int64_t)(1 + st.cfg.n_neg) * st.cfg.global_cols;
-        if ((rc = rg::comm_begin(st.cfg.comm, s, st.cfg.owner_scores[st.own_unit % 2], len))) return rc;
-        if ((rc = rg::comm_end(st.cfg.comm, s))) return rc;
+        if ((rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.owner_scores[st.own_unit % 2], len))) return rc;
     }
-    hipStream_t cs = rg::comm_stream(st.cfg.comm);
-    if ((rc = owner_mid(st, s, loss_out, cs))) return rc;
-    if ((rc = rg::comm_begin(st.cfg.comm, cs, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
+    if ((rc = owner_mid(st, s, loss_out))) return rc;
+    // one rank: nothing to overlap (the exchanges are no-ops), so no cross-stream hops
+    const bool side = st.cfg.world > 1;
+    hipStream_t u = side ? rg::comm_stream(st.cfg.comm) : s;
+    hipError_t e = hipSuccess;
+    if (side) {
+        if (!st.own_grads) e = hipEventCreateWithFlags(&st.own_grads, hipEventDisableTiming);
+        if (e == hipSuccess && !st.own_users) e = hipEventCreateWithFlags(&st.own_users, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(st.own_grads, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(u, st.own_grads, 0);
+        if (e != hipSuccess) return hip_fail("stepper: order the user update", e);
+    }
+    if ((rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
         return rc;
     st.cfg.step += 1;
     const rg_opt_t o = opt_at(st, st.cfg.step);
-    if ((rc = record(ev0, s))) return rc;
-    if ((rc = owner_user_update(st, s, next, o))) return rc;
-    if ((rc = record(ev1, s))) return rc;
-    if ((rc = rg::comm_end(st.cfg.comm, s))) return rc;
-    return owner_item_update(st, s, o, loss_out);
+    if ((rc = record(ev0, u))) return rc;
+    if ((rc = owner_user_update(st, u, next, o))) return rc;
+    if ((rc = record(ev1, u))) return rc;
+    if (side && (e = hipEventRecord(st.own_users, u)) != hipSuccess) return hip_fail("stepper: record the user update", e);
+    if ((rc = owner_item_update(st, s, o, loss_out))) return rc;
+    if (side && (e = hipStreamWaitEvent(s, st.own_users, 0)) != hipSuccess)
+        return hip_fail("stepper: wait the user update", e);
+    return RG_OK;
 }
 
 // the touched rows of the hot pass: a stamp scan (RG_HOT_SCAN=1, default) or the owner flags
@@ -934,6 +951,8 @@ void destroy(Stepper *st) {
     if (st->rows_done) hipFree(st->rows_done);
     if (st->own_counts) hipFree(st->own_counts);
     if (st->own_back) hipEventDestroy(st->own_back);
+    if (st->own_grads) hipEventDestroy(st->own_grads);
+    if (st->own_users) hipEventDestroy(st->own_users);
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
     rg::mt_jump_plan_destroy(st->jump);
