@@ -1043,7 +1043,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     }
     st->cp_pos = (int32_t)pos;
     // lazy dense pass (opt-in, RG_LAZY=1): the single-rank split step.  Bit-exact with the
-    // eager pass but measured slower on gfx950 (the catch-up is ALU-bound; DESIGN.md §3.6).
+    // eager pass but measured slower on gfx950 (the catch-up is ALU-bound; DESIGN.md §4.1).
     st->lazy = env_flag("RG_LAZY", false) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
     if (st->lazy) {
         const size_t ub = (size_t)cfg->tables[0].num_users * sizeof(int32_t);
