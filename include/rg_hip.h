@@ -373,6 +373,13 @@ typedef struct rg_mf_owner_batch {
     int32_t *seg_count;                  /* [rg_mf_owner_segments(GC, n_neg)] */
     float *scores;                       /* [(1 + n_neg) * GC] (+ 4 for the adaptive hinge: max, its
                                             pair, the active count -- rg_mf_owner_adapt) */
+    int32_t *claim_count;                /* non-null (not the adaptive hinge): rg_mf_owner_prepare claims
+                                            each kept draw's two list slots here (local user row, and
+                                            claim_num_users + item) and keeps them in its record, and
+                                            rg_mf_owner_back appends there without atomics; the work's
+                                            row_count of the step must be this array (alternate two
+                                            between consecutive steps, as rg_mf_work_t claim_num_users) */
+    int64_t claim_num_users;             /* this rank's user rows */
 } rg_mf_owner_batch_t;
 
 int64_t rg_mf_owner_segments(int64_t global_cols, int32_t n_neg);

@@ -159,7 +159,8 @@ class MFOwnerBatch(ctypes.Structure):
                 ("n_planned", ctypes.c_int64), ("words", ctypes.c_void_p), ("pool", ctypes.c_void_p),
                 ("pool_len", ctypes.c_int64), ("n_neg", ctypes.c_int32), ("loss", ctypes.c_int32),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("neg_rec", ctypes.c_void_p),
-                ("seg_count", ctypes.c_void_p), ("scores", ctypes.c_void_p)]
+                ("seg_count", ctypes.c_void_p), ("scores", ctypes.c_void_p), ("claim_count", ctypes.c_void_p),
+                ("claim_num_users", ctypes.c_int64)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/rg_hip.h

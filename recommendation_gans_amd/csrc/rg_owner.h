@@ -28,6 +28,10 @@ struct OwnerArgs {
     float *scores;                        // [(1 + n) * gc]
     int64_t segs;
     float n_a, n_b;                       // loss mean denominators (global batch)
+    // claimed list slots (rg_mf_owner_batch_t claim_count): the prepare claims both row sides of
+    // every kept draw and stores them in rec.w (user slot | item slot << 8, each min(slot, cap))
+    int32_t *claim;
+    int64_t claim_users;
 };
 
 // One prepare workgroup: draws [b * kOwnSeg, (b + 1) * kOwnSeg) -> pool pairs (CPython
@@ -49,6 +53,11 @@ __device__ __forceinline__ void owner_prepare_block(const OwnerArgs &a, int64_t 
             const int2 pr = a.pool[choice_index(wd.x, wd.y, a.pool_len)];
             own = (pr.x % a.world) == a.rank;
             r = make_int4((int)((1 + k) * a.gc + c), pr.x / a.world, pr.y, 0);
+            if (own && a.claim != nullptr) {
+                const int su = atomicAdd(a.claim + r.y, 1);
+                const int si = atomicAdd(a.claim + a.claim_users + r.z, 1);
+                r.w = (su < RG_MF_LIST_CAP ? su : RG_MF_LIST_CAP) | ((si < RG_MF_LIST_CAP ? si : RG_MF_LIST_CAP) << 8);
+            }
         }
     }
     __shared__ int wcount[kOwnSeg / kWave];

@@ -60,6 +60,20 @@ __device__ __forceinline__ void append(const OwnWork &w, const OwnTables &t, int
     }
 }
 
+// append at a slot the prepare claimed (no atomic; the overflow path as append's)
+template <class L>
+__device__ __forceinline__ void append_at(const OwnWork &w, const OwnTables &t, int64_t row, int other,
+                                          const float *partner_table, float dz, int sub, int sl) {
+    if (sl < kCapO) {
+        if (sub == 0) w.row_list[row * kCapO + sl] = make_int2(other, __float_as_int(dz));
+    } else {
+        float o[L::EPL];
+        L::load(o, partner_table, other, t.dim, sub);
+        overflow_row<L>(w.hot_grad, row, t.dim, sub, dz, o);
+        if (sub == 0) fix_add(w.hot_bias + row, dz);
+    }
+}
+
 template <class L>
 __device__ __forceinline__ float score(const OwnTables &t, int lu, int i, int sub) {
     constexpr int EPL = L::EPL;
@@ -214,8 +228,13 @@ __global__ __launch_bounds__(kBlk) void owner_back_kernel(OwnerArgs a, OwnTables
                 dpk = (pk / fmaxf((1.0f - pk) * pk, 1e-12f)) / a.n_b;
             }
             const float dz = (dpk * (1.0f - pk)) * pk;
-            append<L>(w, t, lu, i, t.item_w, dz, sub, ubase);
-            append<L>(w, t, U + i, lu, t.user_w, dz, sub, ubase);
+            if (a.claim != nullptr) {
+                append_at<L>(w, t, lu, i, t.item_w, dz, sub, r.w & 0xff);
+                append_at<L>(w, t, U + i, lu, t.user_w, dz, sub, (r.w >> 8) & 0xff);
+            } else {
+                append<L>(w, t, lu, i, t.item_w, dz, sub, ubase);
+                append<L>(w, t, U + i, lu, t.user_w, dz, sub, ubase);
+            }
         }
     }
     // ---- deterministic loss partials: wave DPP sum -> block -> partials[block] --------
@@ -415,6 +434,13 @@ int owner_args(const rg_mf_owner_batch_t *b, OwnerArgs &a) {
     a.seg_count = b->seg_count;
     a.scores = b->scores;
     a.segs = segs_of(b->global_cols, b->n_neg);
+    if (b->claim_count) {
+        if (b->loss == RG_LOSS_ADAPTIVE_HINGE)
+            return fail_arg("rg_mf_owner: no claimed slots for the adaptive hinge (only the max negative is listed)");
+        if (b->claim_num_users <= 0) return fail_arg("rg_mf_owner: claimed slots need claim_num_users");
+        a.claim = b->claim_count;
+        a.claim_users = b->claim_num_users;
+    }
     // mean denominators as the pair pass: BCE means over B and n*B, bpr / hinge over n*B
     if (b->loss == RG_LOSS_POINTWISE) {
         a.n_a = (float)(b->n_pos > 0 ? b->n_pos : 1);
@@ -502,6 +528,9 @@ extern "C" int rg_mf_owner_back(void *stream, const rg_mf_tables_t *t, const rg_
         return fail_arg("rg_mf_owner_back: null scratch");
     if (a.n_planned > 0 && (!w->part_row || !w->part_bias || !w->plan_item_slot_off))
         return fail_arg("rg_mf_owner_back: planned positives need part_row / part_bias / plan_item_slot_off");
+    if (a.claim && (a.claim != w->row_count || a.claim_users != t->num_users))
+        return fail_arg("rg_mf_owner_back: claimed slots need the claim array as row_count and claim_num_users == "
+                        "num_users");
     OwnWork ow{};
     ow.row_count = w->row_count;
     ow.row_list = reinterpret_cast<int2 *>(w->row_list);

@@ -722,7 +722,18 @@ rg_mf_owner_batch_t owner_batch(const Stepper &st, const rg_mf_step_in_t &in, in
     b.neg_rec = st.cfg.owner_rec[unit % 2];
     b.seg_count = st.cfg.owner_seg[unit % 2];
     b.scores = st.cfg.owner_scores[unit % 2];
+    if (st.claim) {                       // the owner prepare claims the kept draws' list slots
+        b.claim_count = st.counts[unit % 2];
+        b.claim_num_users = st.cfg.tables[0].num_users;
+    }
     return b;
+}
+
+// the owner step's scratch for `unit` (claimed slots: that unit's count array)
+rg_mf_work_t owner_work(const Stepper &st, const rg_mf_step_in_t &in, int64_t unit) {
+    rg_mf_work_t w = work_for(st, in);
+    if (st.claim) w.row_count = st.counts[unit % 2];
+    return w;
 }
 
 int owner_check_in(const Stepper &st, const rg_mf_step_in_t &in) {
@@ -743,7 +754,9 @@ int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
     const rg_mf_owner_batch_t b = owner_batch(st, cur, unit);
     if (!(st.prepared && st.prep_unit == unit && same_input(st.prep_in, cur))) {
         if ((rc = wait_words(st, s, unit))) return rc;
+        if ((rc = clean_counts(st, s, (int)(unit % 2)))) return rc;
         if ((rc = rg_mf_owner_prepare(s, &b))) return rc;
+        st.count_dirty[unit % 2] = st.claim;
     }
     st.prepared = false;
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
@@ -760,7 +773,7 @@ int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
 int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr) {
     if (st.own_stage != 1) return rg::fail_arg("rg_mf_stepper_owner_mid: owner_begin must come first");
     const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
-    rg_mf_work_t w = work_for(st, st.own_in);
+    rg_mf_work_t w = owner_work(st, st.own_in, st.own_unit);
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     int rc = RG_OK;
     if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = rg_mf_owner_adapt(s, &b))) return rc;   // global max, count
@@ -793,12 +806,15 @@ int owner_user_update(Stepper &st, hipStream_t s, const rg_mf_step_in_t *next, c
         if ((rc = owner_check_in(st, *next))) return rc;
         if ((rc = keep_ahead(st, unit + 1))) return rc;
         if ((rc = wait_words(st, s, unit + 1))) return rc;
+        if ((rc = clean_counts(st, s, (int)((unit + 1) % 2)))) return rc;
         nb = owner_batch(st, *next, unit + 1);
     }
-    rg_mf_work_t w = work_for(st, st.own_in);
+    rg_mf_work_t w = owner_work(st, st.own_in, unit);
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     if ((rc = rg::apply_prepare_owner(s, tb, &w, &o, 0, tb->num_users, nullptr, next ? &nb : nullptr))) return rc;
+    st.count_dirty[unit % 2] = false;     // the item gradient and this pass consumed (reset) its claims
     if (next) {
+        st.count_dirty[(unit + 1) % 2] = st.claim;
         st.prepared = true;
         st.prep_unit = unit + 1;
         st.prep_in = *next;
@@ -1064,9 +1080,11 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     // claimed list slots: the single-rank eager split step (RG_MF_CLAIM=0: the pair pass
     // claims its slots with returning atomics, as before)
     const rg_mf_tables_t &t0 = cfg->tables[0];
-    st->claim = env_flag("RG_MF_CLAIM", true) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused && !st->lazy &&
+    // (the owner-sharded step claims in its owner prepare, records keep the slots beside the ids)
+    st->claim = env_flag("RG_MF_CLAIM", true) && !cfg->item_grad && !st->fused && !st->lazy &&
                 cfg->loss != RG_LOSS_ADAPTIVE_HINGE && cfg->work.row_count != nullptr &&
-                t0.num_users < ((int64_t)1 << 27) && t0.num_items < ((int64_t)1 << 27);
+                (cfg->dp_mode == 2 ||
+                 (cfg->dp_mode == 0 && t0.num_users < ((int64_t)1 << 27) && t0.num_items < ((int64_t)1 << 27)));
     if (st->claim) {
         const size_t cb = (size_t)(t0.num_users + t0.num_items) * sizeof(int32_t);
         e = hipMalloc(&st->own_counts, cb);

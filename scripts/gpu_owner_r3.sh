@@ -5,7 +5,7 @@ TAG=${1:-run}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
-  tests/test_dp_gpu.py tests/test_dp_fit_gpu.py > gpurun_out/gpu_tests_$TAG.log 2>&1
+  tests/test_dp_gpu.py tests/test_dp_fit_gpu.py tests/test_configs_gpu.py -k "dp or owner or rank or Dp or Owner or world" > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "tests exit=$rc"; grep -E "passed|failed" gpurun_out/gpu_tests_$TAG.log | tail -2
 [ $rc -eq 0 ] || exit $rc
 for k in 1 2; do

@@ -121,6 +121,88 @@ def test_mf_dp_rank_gradient_d128(ml20m):
         assert abs(float(buf[s, nb + Us + Is]) - lv) <= 1e-5 * abs(lv)
 
 
+@pytest.mark.parametrize("loss", ["bpr", "pointwise"])
+def test_mf_owner_full_size_8_ranks_d128(ml20m, loss):
+    """C5 in the owner-sharded layout (the default at R > 1): all 8 ranks of the step at
+    d = 128, full size, on this one GPU -- 8 engines, one thread each, their score and
+    item-gradient all-reduces summed across the threads -- against the single process at
+    batch 8 * 8192 (the oracle): loss 1e-5, MT state exact, every rank's user rows and the
+    replicated items by tensor parity, two steps (the second's draws prepared, with claimed
+    list slots, inside the first's user update)."""
+    import threading
+    from recommendation_gans_amd import sharding
+    from recommendation_gans_amd.mf_engine import MFEngine
+    dev = torch.device("cuda:0")
+    U, I, d, B, n, world = ml20m.num_users, ml20m.num_items, 128, 8192, 5, 8
+    gb = B * world
+    tabs = _tables(U, I, d)
+    st = orng.py_seed_state(0)
+    kw = dict(loss=loss, optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    tu = torch.from_numpy(ml20m.train_u[:3 * gb].astype(np.int64)).to(dev)
+    ti = torch.from_numpy(ml20m.train_i[:3 * gb].astype(np.int64)).to(dev)
+    engines, inputs = [], []
+    for r in range(world):
+        e = MFEngine(tabs[0], tabs[1], tabs[2].reshape(-1), tabs[3].reshape(-1), ml20m.pool_u, ml20m.pool_i,
+                     st.copy(), device=dev, rank=r, world_size=world, dp="owner", **kw)
+        plans = e.make_plans(ti, users=tu)
+        engines.append(e)
+        inputs.append([e.step_input(tu[g * gb:(g + 1) * gb], ti[g * gb:(g + 1) * gb], gb, plans[g]) for g in range(3)])
+    bar = threading.Barrier(world)
+    bufs = [None] * world
+    losses = [[None] * 2 for _ in range(world)]
+    errors = []
+
+    def allreduce(r, buf):
+        bufs[r] = buf
+        bar.wait()
+        if r == 0:
+            tot = bufs[0].clone()
+            for b in bufs[1:]:
+                tot += b
+            for b in bufs:
+                b.copy_(tot)
+        bar.wait()
+
+    def run(r):
+        try:
+            for s in range(2):
+                lv = engines[r].train_step_owner_exchange(inputs[r][s], inputs[r][s + 1],
+                                                          lambda buf: allreduce(r, buf))
+                losses[r][s] = lv.clone()
+        except Exception as ex:       # noqa: BLE001 -- reported below
+            errors.append((r, repr(ex)))
+            bar.abort()
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    o = omf.MFOracle(*[t.clone() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(), **{**kw, "batch_size": gb})
+    o64 = omf.MFOracle(*[t.clone().double() for t in tabs], ml20m.pool_u, ml20m.pool_i, st.copy(),
+                       **{**kw, "batch_size": gb})
+    ref = []
+    for s in range(2):
+        ref.append(o.step(ml20m.train_u[s * gb:(s + 1) * gb], ml20m.train_i[s * gb:(s + 1) * gb]))
+        o64.step(ml20m.train_u[s * gb:(s + 1) * gb], ml20m.train_i[s * gb:(s + 1) * gb])
+    params = [[p.cpu() for p in e.params()] for e in engines]
+    for r in range(world):
+        for s in range(2):
+            got = float(losses[r][s][0])
+            assert abs(got - ref[s]) <= 1e-5 * abs(ref[s]), (r, s, got, ref[s])
+        assert (engines[r].mt_state() == o.state).all(), (r, "MT state")
+        for k in (1, 3):                                  # replicated items
+            ok, msg = omf.tensor_parity(params[r][k].reshape(o.params[k].shape), o.params[k], o64.params[k])
+            assert ok, (loss, r, k, msg)
+    for k in (0, 2):                                      # every rank's user rows, unsharded
+        full = torch.from_numpy(sharding.unshard_rows([params[r][k].numpy() for r in range(world)], U))
+        ok, msg = omf.tensor_parity(full.reshape(o.params[k].shape), o.params[k], o64.params[k])
+        assert ok, (loss, k, msg)
+    assert all(torch.equal(params[0][1], params[r][1]) for r in range(world)), "replicated items diverged"
+
+
 def _gan_batch(ml20m, S, B):
     order = np.argsort(ml20m.train_u, kind="stable")
     uu, ii = ml20m.train_u[order], ml20m.train_i[order]
