@@ -125,6 +125,7 @@ struct Stepper {
     int32_t *own_counts = nullptr;
     bool count_dirty[2] = {false, false};  // counts[b] hold claims no dense pass consumed yet
     bool prep_claimed = false;             // the prepared pairs carry claimed slots
+    bool prep_in_pairs = false;            // split step: the next prepare rides in the pair pass
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -495,11 +496,25 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     }
     if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = wait_words(st, s, unit))) return rc;   // adapt-max reads them
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
-    if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) return rc;
-    if ((rc = release(st, s))) return rc;
     rg_mf_batch_t nbatch{};
     rg_mf_work_t nw{};
-    if (next) {
+    // RG_PREP_IN_PAIRS: the next step's prepare (pool lookups, claims) in extra workgroups of
+    // this pair pass, beside its latency-bound gathers, instead of in the dense pass
+    const bool pip = st.prep_in_pairs && next && st.cfg.loss != RG_LOSS_ADAPTIVE_HINGE && !st.cfg.item_grad;
+    if (pip) {
+        // only the slot of unit + 1 (this unit is not released yet; see train_lazy)
+        if (!st.inline_gen && (rc = generate_upto(st, unit + 1, 0))) return rc;
+        if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
+        if ((rc = wait_words(st, s, unit + 1))) return rc;
+        if ((rc = clean_counts(st, s, (int)((unit + 1) % 2)))) return rc;
+        nbatch = make_batch(st, *next, unit + 1);
+        nw = train_work(st, *next, unit + 1);
+        if ((rc = rg_mf_pairs_prepare(s, tb, &batch, &w, &nbatch, &nw, nullptr, 0))) return rc;
+    } else if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
+        return rc;
+    }
+    if ((rc = release(st, s))) return rc;
+    if (next && !pip) {
         if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
         if ((rc = wait_side(st, s, (int)((unit + 1) % 2)))) return rc;
         if ((rc = wait_words(st, s, unit + 1))) return rc;
@@ -529,7 +544,8 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     }
     rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // timed by the dispatch itself
     rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
-                                 next ? &nbatch : nullptr, next ? &nw : nullptr, gen_slot >= 0 ? &gen : nullptr);
+                                 next && !pip ? &nbatch : nullptr, next && !pip ? &nw : nullptr,
+                                 gen_slot >= 0 ? &gen : nullptr);
     rg::launch_events() = rg::LaunchEvents{};
     if (rc) return rc;
     if (gen_slot >= 0) end_production(st, s, gen_slot);
@@ -1098,6 +1114,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         st->counts[0] = cfg->work.row_count;
         st->counts[1] = st->own_counts;
     }
+    st->prep_in_pairs = env_flag("RG_PREP_IN_PAIRS", false);
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
     if (env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
