@@ -797,6 +797,732 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
     }
 }
 
+// ============================================================================================
+// E = 64 tower (C3, mf_dim = 0): one WAVE per 32-row tile, activations in registers.
+//
+// The tile kernel above keeps every activation in LDS and spreads a tile's MFMA tiles over 8
+// waves: ~12 workgroup barriers and an LDS -> MFMA -> LDS round trip per layer, 14 % of the
+// fp32 MFMA peak.  Here a wave owns a whole tile (the same 32 rows, so scores / dp / contrib
+// / list entries / plan partials keep their layouts) and runs the chain with no barrier:
+//
+//   * "T layout": a 16x16 MFMA C tile of a layer's output transposed, Y^T[feature][example]
+//     -- lane (g, j) holds features 16t + 4g + r (r = 0..3) of example j.  Fed back as the
+//     B operand of the next product, k-step r of tile t takes feature 16t + 4g + r from lane
+//     group g, so  Y_{k+1}^T = W_{k+1} Y_k^T  and  dA_k^T = W_k^T delta_k^T  consume the
+//     previous result straight from registers (the A operand, a weight, is read from LDS in
+//     the same permuted k order: one ds_read_b128 per 4 k-steps forward).
+//   * the weight gradients dW_k = sum_e delta_k[e] X_k[e]^T contract over EXAMPLES, which the
+//     T layout keeps on lanes; X_k and delta_k are staged once into the wave's own LDS rows
+//     ([example][feature], float4 stores) and read back with examples on the k axis.  X_0 (the
+//     gathered embeddings) is re-read from L2 in that layout, issued at the start of the
+//     backward.  The wave accumulates dW in MFMA accumulators across its tiles; bias
+//     gradients are per-lane sums of the T-layout deltas.
+//   * one workgroup of 4 waves per CU (135 KB of LDS, 512 registers per lane); at the end the
+//     4 waves' gradients are summed in wave order in LDS into the workgroup's partial.
+// Every sum is a fixed-order f32 chain (MFMA = k-ordered fmaf chain), so results are
+// deterministic; the order differs from the tile kernel's, so the two agree to fp32 rounding.
+// ============================================================================================
+namespace ncfw {
+constexpr int kWaves = 4, kThreads = 64 * kWaves, kR = kRows;   // 32 rows = 2 example blocks of 16
+// weights in LDS (floats): W_k row-major [out][in + 4] (b128 rows land on distinct 16-B slots),
+// W4 and the output row padded to 16 rows of zeros, biases padded with zeros
+constexpr int S1 = 132, S2 = 68, S3 = 36, S4 = 20, SO = 20;
+constexpr int oW1 = 0, oW2 = oW1 + 64 * S1, oW3 = oW2 + 32 * S2, oW4 = oW3 + 16 * S3, oWo = oW4 + 16 * S4;
+constexpr int oB1 = oWo + 16 * SO, oB2 = oB1 + 64, oB3 = oB2 + 32, oB4 = oB3 + 16, oBo = oB4 + 16;
+constexpr int kWFloats = oBo + 4;
+// per wave: staged activations / deltas [32][stride], stride = 16 mod 64 floats (the
+// example-on-k reads of lane (g, x) hit bank 16g + x), then the tile's small per-row arrays
+constexpr int R1S = 80, R2S = 48, R3S = 16, R4S = 16;
+constexpr int oR1 = 0, oR2 = oR1 + kR * R1S, oR3 = oR2 + kR * R2S, oR4 = oR3 + kR * R3S, oSm = oR4 + kR * R4S;
+constexpr int kSmall = 11;
+constexpr int kWaveFloats = oSm + kSmall * kR;
+constexpr int kLdsFloats = kWFloats + kWaves * kWaveFloats;
+constexpr int P = NcfShape<64>::P;
+static_assert(kLdsFloats <= kLdsMax, "LDS");
+static_assert(16 * 64 <= kR * R2S, "planned item halves fit the delta2 rows");
+static_assert(kWFloats % 4 == 0 && kWaveFloats % 4 == 0, "16-B alignment");
+
+// orders this wave's LDS traffic for the compiler: DS instructions of one wave execute in
+// order, so a wavefront-scope fence (no wait instruction) is all a cross-lane LDS hand-off
+// inside the wave needs
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+__device__ __forceinline__ v4f mfma(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// Y^T (TO tiles) = W X^T: W [16 TO][16 TI] (row stride S), X^T T-layout (TI tiles)
+template <int TI, int TO>
+__device__ __forceinline__ void fwd(const v4f (&x)[TI][2], v4f (&y)[TO][2], const float *W, int S, int g, int m) {
+#pragma unroll
+    for (int t = 0; t < TO; ++t) y[t][0] = y[t][1] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti) {
+        v4f a[TO];
+#pragma unroll
+        for (int t = 0; t < TO; ++t) a[t] = *reinterpret_cast<const v4f *>(W + (16 * t + m) * S + 16 * ti + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TO; ++t)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) y[t][nb] = mfma(a[t][r], x[ti][nb][r], y[t][nb]);
+    }
+}
+
+// dA^T (TI tiles) = W^T delta^T: W [16 TO][16 TI] row-major (stride S), delta^T T-layout (TO
+// tiles); W may point at a column block of a wider matrix (its first of TI column tiles)
+template <int TI, int TO>
+__device__ __forceinline__ void bwd(const v4f (&d)[TO][2], v4f (&da)[TI][2], const float *W, int S, int g, int x) {
+#pragma unroll
+    for (int t = 0; t < TI; ++t) da[t][0] = da[t][1] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int to = 0; to < TO; ++to)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a[TI];
+#pragma unroll
+            for (int ti = 0; ti < TI; ++ti) a[ti] = W[(16 * to + 4 * g + r) * S + 16 * ti + x];
+#pragma unroll
+            for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) da[ti][nb] = mfma(a[ti], d[to][nb][r], da[ti][nb]);
+        }
+}
+
+// dW[16 TOo][16 TIi] += sum_e D[e][o] X[e][i] over the tile's 32 examples (staged rows), and the
+// bias gradient sum_e D[e][o] as the same product with a ones operand (every column of gb)
+template <int TOo, int TIi>
+__device__ __forceinline__ void dw(v4f (&acc)[TOo][TIi], v4f (&gb)[TOo], const float *D, int SD, const float *X,
+                                   int SX, int g, int x) {
+#pragma unroll
+    for (int s = 0; s < kR / 4; ++s) {
+        float a[TOo], b[TIi];
+#pragma unroll
+        for (int to = 0; to < TOo; ++to) a[to] = D[(4 * s + g) * SD + 16 * to + x];
+#pragma unroll
+        for (int ti = 0; ti < TIi; ++ti) b[ti] = X[(4 * s + g) * SX + 16 * ti + x];
+#pragma unroll
+        for (int to = 0; to < TOo; ++to) {
+#pragma unroll
+            for (int ti = 0; ti < TIi; ++ti) acc[to][ti] = mfma(a[to], b[ti], acc[to][ti]);
+            gb[to] = mfma(a[to], 1.0f, gb[to]);
+        }
+    }
+}
+
+// staged rows -> T-layout tiles (the inverse of stage)
+template <int T>
+__device__ __forceinline__ void unstage(v4f (&y)[T][2], const float *R, int RS, int g, int j) {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) y[t][nb] = *reinterpret_cast<const v4f *>(R + (nb * 16 + j) * RS + 16 * t + 4 * g);
+}
+
+// T-layout tiles -> staged rows [example][feature] (float4 per lane)
+template <int T>
+__device__ __forceinline__ void stage(const v4f (&y)[T][2], float *R, int RS, int g, int j) {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<v4f *>(R + (nb * 16 + j) * RS + 16 * t + 4 * g) = y[t][nb];
+}
+
+// torch's LeakyReLU(0.1) -> Dropout(0.5) multiplier from the kept bit and the sign of the
+// output (A = z m with m > 0 keeps the sign of z; a dropped unit's delta is 0)
+__device__ __forceinline__ float mult(float y, bool keep, bool training) {
+    const float m1 = y > 0.0f ? 1.0f : 0.1f;
+    return training ? (keep ? 2.0f * m1 : 0.0f) : m1;
+}
+}  // namespace ncfw
+
+// Diagnostic build only: per-wave phase stamps of its first two tiles (16 slots per tile),
+// each draining the wave's loads and LDS traffic first (scripts/ncf_stamps.py --wave)
+#ifdef RG_DIAG_STAMPS
+#define WS(k)                                                                                              \
+    do {                                                                                                   \
+        if (g_ncf_stamps && tl_ < 2) {                                                                     \
+            unsigned long long t_;                                                                         \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)"      \
+                         : "=s"(t_)::"memory");                                                            \
+            if (lane == 0) g_ncf_stamps[(((int64_t)blockIdx.x * ncfw::kWaves + wave) * 2 + tl_) * 16 + (k)] = t_; \
+        }                                                                                                  \
+    } while (0)
+#else
+#define WS(k) \
+    do {      \
+    } while (0)
+#endif
+
+template <int PHASE>
+__global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void ncf_wave_kernel(NcfArgs a) {
+    using namespace ncfw;
+    using S64 = NcfShape<64>;
+    constexpr bool kBackward = PHASE != kNcfScores && PHASE != kNcfLossOnly;
+    constexpr int WO = S64::w_off(4);
+    extern __shared__ float lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, j = lane & 15;
+    float *sw = lds;
+    float *ws = lds + kWFloats + wave * kWaveFloats;
+    float *R1 = ws + oR1, *R2 = ws + oR2, *R3 = ws + oR3, *R4 = ws + oR4;
+    int *sU = reinterpret_cast<int *>(ws + oSm), *sI = sU + kR, *sR = sI + kR;
+    uint32_t *sK = reinterpret_cast<uint32_t *>(sR + kR);
+    float *sP = reinterpret_cast<float *>(sK + kR), *sDz = sP + kR, *sLa = sDz + kR, *sLb = sLa + kR;
+    int *sLu = reinterpret_cast<int *>(sLb + kR), *sLi = sLu + kR, *sPs = sLi + kR;
+
+    // ---- parameters into LDS: every thread's float4 loads issued before its LDS stores ----
+    {
+        auto copy = [&](auto cnt, int dst, int S, const float *src, int cols) {   // rows x cols (cols % 4 == 0)
+            constexpr int N4 = decltype(cnt)::value;
+            constexpr int PT = (N4 + kThreads - 1) / kThreads;
+            const int c4 = cols / 4;
+            float4 v[PT];
+#pragma unroll
+            for (int k = 0; k < PT; ++k) {
+                const int e = tid + k * kThreads;
+                if (e < N4) v[k] = reinterpret_cast<const float4 *>(src)[e];
+            }
+#pragma unroll
+            for (int k = 0; k < PT; ++k) {
+                const int e = tid + k * kThreads;
+                if (e < N4) *reinterpret_cast<float4 *>(sw + dst + (e / c4) * S + (e % c4) * 4) = v[k];
+            }
+        };
+        const float *W1 = a.mlp + S64::w_off(0), *W2 = a.mlp + S64::w_off(1), *W3 = a.mlp + S64::w_off(2),
+                    *W4 = a.mlp + S64::w_off(3);
+        copy(std::integral_constant<int, 64 * 128 / 4>{}, oW1, S1, W1, 128);
+        copy(std::integral_constant<int, 32 * 64 / 4>{}, oW2, S2, W2, 64);
+        copy(std::integral_constant<int, 16 * 32 / 4>{}, oW3, S3, W3, 32);
+        // the small tail [oW4, kWFloats): W4 rows 0..7 (rows 8..15 zero), the output row, biases
+        for (int e = tid; e < kWFloats - oW4; e += kThreads) {
+            const int o = oW4 + e;
+            float v = 0.0f;
+            if (o < oWo) {
+                const int row = (o - oW4) / S4, col = (o - oW4) % S4;
+                if (row < 8 && col < 16) v = W4[row * 16 + col];
+            } else if (o < oB1) {
+                if (o - oWo < 8) v = a.mlp[WO + (o - oWo)];
+            } else if (o < oB2) {
+                v = W1[64 * 128 + (o - oB1)];
+            } else if (o < oB3) {
+                v = W2[32 * 64 + (o - oB2)];
+            } else if (o < oB4) {
+                v = W3[16 * 32 + (o - oB3)];
+            } else if (o < oBo) {
+                if (o - oB4 < 8) v = W4[8 * 16 + (o - oB4)];
+            } else if (o == oBo) {
+                v = a.mlp[WO + 8];
+            }
+            sw[o] = v;
+        }
+    }
+    __syncthreads();
+    const float *W1s = sw + oW1, *W2s = sw + oW2, *W3s = sw + oW3, *W4s = sw + oW4, *Wos = sw + oWo;
+    const bool training = a.training != 0;
+    const int n = a.n_neg, NP = n + 1, tc = a.tc;
+    constexpr int units = S64::mask_units();
+    const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
+
+    // running gradients of this wave, all MFMA accumulators: weight tiles, bias tiles (every
+    // column holds the bias sum) and the output layer's [w_out | b_out] tile
+    v4f gW1[4][8], gW2[2][4], gW3[1][2], gW4[1][1], gB1[4], gB2[2], gB3[1], gB4[1], gO;
+    const v4f z4 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) gW1[p][q] = z4;
+        gB1[p] = z4;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gW2[p][q] = z4;
+        gB2[p] = z4;
+    }
+    gW3[0][0] = gW3[0][1] = gW4[0][0] = gB3[0] = gB4[0] = gO = z4;
+
+    // a column's pair record for row r = q * tc + cl of `tile` (lanes 0..31): the loads are
+    // issued unconditionally from clamped indices (fetch) and resolved when the values are
+    // needed, a tile later (finish), so no wait sits in between
+    struct RowRaw {
+        int2 pr;
+        int ps, perm;
+        int64_t s;
+        int q;
+        bool valid;
+    };
+    auto fetch_row = [&](int64_t tile, int r) {
+        RowRaw w;
+        w.q = r / tc;
+        const int cl = r % tc;
+        w.s = tile * tc + cl;
+        bool valid = tile < a.tiles && w.q < NP && w.s < a.cols;
+        if (valid && w.q == 0) valid = w.s < a.n_pos;
+        if (valid && w.q > 0 && pairwise) valid = w.s < a.n_pos;
+        w.valid = valid;
+        const int64_t sc = w.s < a.cols ? w.s : a.cols - 1;
+        w.pr = a.pairs[sc * pair_stride(a.n_neg) + min(w.q, n)];
+        w.ps = a.pos_slot != nullptr ? a.pos_slot[sc] : -1;
+        w.perm = a.perm ? a.perm[sc] : 0;
+        return w;
+    };
+    auto finish_row = [&](const RowRaw &w, int &u, int &i, int &ps, int64_t &gj) {
+        u = w.valid ? w.pr.x : -1;
+        i = w.valid ? w.pr.y : -1;
+        ps = (kBackward && w.valid && w.q == 0) ? w.ps : -1;
+        const int64_t colid = a.perm && w.s < a.cols ? (int64_t)w.perm : w.s;
+        gj = w.q == 0 ? a.col_offset + colid : (int64_t)(w.q - 1) * a.global_cols + a.col_offset + colid;
+    };
+
+    const int64_t waves_total = (int64_t)gridDim.x * kWaves;
+    const int64_t first = (int64_t)blockIdx.x * kWaves + wave;
+    RowRaw nxt{};   // the next tile's record (lanes 0..31), in flight during this tile
+    if (lane < kR) nxt = fetch_row(first, lane);
+    for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
+        int tc = a.tc;   // opaque per tile: keeps the loss / row addresses from being hoisted (and spilled)
+        asm volatile("" : "+s"(tc));
+        const int tl_ = (int)((tile - first) / waves_total);
+        (void)tl_;
+        WS(0);
+        // ---- row ids (lanes 0..31: row r = q * tc + cl), as the tile kernel ----
+        int ru = -1, ri = -1, rps = -1;
+        int64_t ngj = 0;
+        if (lane < kR) finish_row(nxt, ru, ri, rps, ngj);
+        if (lane < kR) {
+            const int r = lane, q = r / tc;
+            sU[r] = ru;
+            sI[r] = ri;
+            sR[r] = (int)ngj;
+            sK[r] = hash32(a.seed ^ ((uint64_t)(q == 0 ? 0 : 1) << 40) ^ ((uint64_t)ngj * 0x9E3779B97F4A7C15ULL));
+            sDz[r] = 0.0f;
+            sPs[r] = rps;
+        }
+        wave_sync();
+        WS(1);
+        int ue[2], ie[2], re[2];
+        uint32_t ke[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            ue[nb] = sU[nb * 16 + j];
+            ie[nb] = sI[nb * 16 + j];
+            re[nb] = sR[nb * 16 + j];
+            ke[nb] = sK[nb * 16 + j];
+        }
+        // ---- gather X0^T (T layout): features 16 t + 4 g .. + 3 of example nb * 16 + j; a row
+        // that is not a valid pair reads row 0 (its dz is 0, so none of its values reach a
+        // gradient, and its score is never used) ----
+        v4f x0[8][2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const float *pu = a.user_w + (int64_t)(ue[nb] >= 0 ? ue[nb] : 0) * 64 + 4 * g;
+            const float *pi = a.item_w + (int64_t)(ue[nb] >= 0 ? ie[nb] : 0) * 64 + 4 * g;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) x0[t][nb] = *reinterpret_cast<const v4f *>(t < 4 ? pu + 16 * t : pi + 16 * (t - 4));
+        }
+        // dropout bits of every unit of the tile, computed while the gather is in flight
+        // (bit (t * 2 + nb) * 4 + r of a layer's word: feature 16 t + 4 g + r, example nb * 16 + j)
+        auto keep_bits = [&](auto tc_, int out, int mask_base) -> uint32_t {
+            constexpr int T = decltype(tc_)::value;
+            uint32_t keep = 0;
+            if (!training) return keep;
+            if (a.mask_pos) {   // recorded masks (parity tests): every byte load first
+                uint8_t mv[T][2][4];
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const uint8_t *mk = (nb * 16 + j < tc ? a.mask_pos : a.mask_neg) +
+                                        (int64_t)(ue[nb] >= 0 ? re[nb] : 0) * units + mask_base;
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) mv[t][nb][r] = mk[min(16 * t + 4 * g + r, out - 1)];
+                }
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            keep |= (uint32_t)(mv[t][nb][r] != 0 && ue[nb] >= 0 && 16 * t + 4 * g + r < out)
+                                    << ((t * 2 + nb) * 4 + r);
+            } else {
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int f = 16 * t + 4 * g + r;
+                            const uint32_t h = mix32(ke[nb] + (uint32_t)(mask_base + f) * 0x85EBCA6BU);
+                            keep |= (((h >> 7) & 1U) & (uint32_t)(f < out)) << ((t * 2 + nb) * 4 + r);
+                        }
+            }
+            return keep;
+        };
+        const uint64_t kb = (uint64_t)keep_bits(std::integral_constant<int, 4>{}, 64, S64::mask_off(0)) |
+                            (uint64_t)keep_bits(std::integral_constant<int, 2>{}, 32, S64::mask_off(1)) << 32 |
+                            (uint64_t)keep_bits(std::integral_constant<int, 1>{}, 16, S64::mask_off(2)) << 48 |
+                            (uint64_t)keep_bits(std::integral_constant<int, 1>{}, 8, S64::mask_off(3)) << 56;
+        // list slots claimed behind the gather (their round trip overlaps it and the first layer;
+        // the entries are written after it)
+        int lu = -1, li = -1;
+        if (kBackward && lane < kR && ru >= 0) {
+            lu = atomicAdd(a.row_count + ru, 1);
+            if (rps < 0 && !(lane < tc && a.pos_slot != nullptr)) li = atomicAdd(a.row_count + a.num_users + ri, 1);
+        }
+        WS(2);
+        // ---- forward ----
+        // bias, LeakyReLU(0.1), Dropout(0.5) as one multiplier per unit
+        auto activate = [&](auto &y, const float *b, int bit0) {
+            constexpr int T = sizeof(y) / sizeof(y[0]);
+            v4f bv[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t) bv[t] = *reinterpret_cast<const v4f *>(b + 16 * t + 4 * g);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float z = y[t][nb][r] + bv[t][r];
+                        const float m1 = z > 0.0f ? 1.0f : 0.1f;
+                        const float m = training ? (((kb >> (bit0 + (t * 2 + nb) * 4 + r)) & 1U) ? 2.0f * m1 : 0.0f) : m1;
+                        y[t][nb][r] = z * m;
+                    }
+        };
+        v4f y1[4][2], y2[2][2], y3[1][2], y4[1][2];
+        fwd<8, 4>(x0, y1, W1s, S1, g, j);
+        WS(3);
+        activate(y1, sw + oB1, 0);
+        stage<4>(y1, R1, R1S, g, j);
+        fwd<4, 2>(y1, y2, W2s, S2, g, j);
+        activate(y2, sw + oB2, 32);
+        stage<2>(y2, R2, R2S, g, j);
+        fwd<2, 1>(y2, y3, W3s, S3, g, j);
+        activate(y3, sw + oB3, 48);
+        stage<1>(y3, R3, R3S, g, j);
+        fwd<1, 1>(y3, y4, W4s, S4, g, j);
+        activate(y4, sw + oB4, 56);
+        if (kBackward) {   // A_4 rows with a ones feature (8) for the output layer's bias gradient
+            v4f y4s[1][2] = {{y4[0][0], y4[0][1]}};
+            if (g == 2) y4s[0][0][0] = y4s[0][1][0] = 1.0f;
+            stage<1>(y4s, R4, R4S, g, j);
+        }
+        v4f zo[1][2];
+        fwd<1, 1>(y4, zo, Wos, SO, g, j);
+        if (g == 0) {
+            const float bo = sw[oBo];
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const float p = sigmoidf_ref(zo[0][nb][0] + bo);
+                sP[nb * 16 + j] = p;
+                if (PHASE == kNcfScores) a.scores[tile * kR + nb * 16 + j] = ue[nb] >= 0 ? p : 0.0f;
+            }
+        }
+        // list entries of the claimed slots (the atomics have returned by now)
+        if (kBackward && lane < kR) {
+            const int64_t ex = tile * kR + lane;
+            if (lu >= 0 && lu < kNcfCap) a.row_list[(int64_t)ru * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+            if (li >= 0 && li < kNcfCap)
+                a.row_list[(a.num_users + ri) * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+            sLu[lane] = lu;
+            sLi[lane] = li;
+        }
+        // the next tile's record, in flight during this tile's loss and backward
+        if (lane < kR) nxt = fetch_row(tile + waves_total, lane);
+        wave_sync();
+        WS(4);
+        if (PHASE == kNcfScores) continue;
+        // ---- loss: one lane per row, then the positives' lanes sum their column in q order
+        // (the tile kernel's arithmetic and summation order) ----
+        float *sT = reinterpret_cast<float *>(sK);   // row -> the positive's dL/dp term (sK is dead here)
+        if (lane < kR) {
+            const int r = lane, q = r / tc, cl = r % tc;
+            const bool v = q < NP && sU[r] >= 0, vp = sU[cl] >= 0;
+            const float p = sP[r], pp = sP[cl];
+            float dpr = 0.0f, ta = 0.0f, tb = 0.0f, t0 = 0.0f;
+            if (PHASE == kNcfGivenDp) {
+                if (v) dpr = a.dp_in[tile * kR + r];
+            } else if (a.loss == RG_LOSS_POINTWISE) {
+                if (v && q == 0) {
+                    ta = -fmaxf(logf(p), -100.0f);
+                    dpr = ((p - 1.0f) / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_a;
+                } else if (v) {
+                    tb = -fmaxf(logf(1.0f - p), -100.0f);
+                    dpr = (p / fmaxf((1.0f - p) * p, 1e-12f)) / a.n_b;
+                }
+            } else if (v && vp && q > 0) {   // bpr / hinge on the neg.view(n, B) pairing
+                const float gg = 1.0f / a.n_a;
+                if (a.loss == RG_LOSS_BPR) {
+                    const float sg = sigmoidf_ref(pp - p);
+                    ta = 1.0f - sg;
+                    const float dx = (-gg) * (1.0f - sg) * sg;
+                    t0 = dx;
+                    dpr = -dx;
+                } else {
+                    const float xx = (p - pp) + 1.0f;
+                    ta = fmaxf(xx, 0.0f);
+                    const float dx = xx >= 0.0f ? gg : 0.0f;
+                    t0 = -dx;
+                    dpr = dx;
+                }
+            }
+            sLa[r] = ta;
+            sLb[r] = tb;
+            sT[r] = t0;
+            wave_sync();
+            if (q == 0 && PHASE != kNcfGivenDp) {   // the positive: its column's sums in q order
+                constexpr int QM = RG_MF_MAX_NEG + 1;
+                float la = ta, lb = 0.0f;
+                float ca[QM], cb[QM], c0[QM];
+                bool cv[QM];
+#pragma unroll
+                for (int k = 1; k < QM; ++k) {
+                    const int rr = min(k * tc + cl, kR - 1);
+                    ca[k] = sLa[rr];
+                    cb[k] = sLb[rr];
+                    c0[k] = sT[rr];
+                    cv[k] = k < NP && sU[rr] >= 0;
+                }
+                if (a.loss == RG_LOSS_POINTWISE) {
+#pragma unroll
+                    for (int k = 1; k < QM; ++k)
+                        if (cv[k]) lb += cb[k];
+                } else {
+                    la = 0.0f;
+                    float d0 = 0.0f;
+#pragma unroll
+                    for (int k = 1; k < QM; ++k)
+                        if (cv[k] && v) { la += ca[k]; d0 += c0[k]; }
+                    dpr = d0;
+                }
+                wave_sync();
+                sLa[cl] = la;   // column totals (row cl is this lane's own row)
+                sLb[cl] = lb;
+            }
+            sDz[r] = v ? (dpr * (1.0f - p)) * p : 0.0f;
+        }
+        wave_sync();
+        if (lane == 0) {   // column order, as the one-thread loop summed them
+            float va[16], vb[16];
+#pragma unroll
+            for (int cl = 0; cl < 16; ++cl) {
+                va[cl] = cl < tc ? sLa[cl] : 0.0f;
+                vb[cl] = cl < tc ? sLb[cl] : 0.0f;
+            }
+            float la = 0.0f, lb = 0.0f;
+#pragma unroll
+            for (int cl = 0; cl < 16; ++cl)
+                if (cl < tc) { la += va[cl]; lb += vb[cl]; }
+            a.loss_partials[2 * tile] = la;
+            a.loss_partials[2 * tile + 1] = lb;
+        }
+        if (PHASE == kNcfLossOnly) { wave_sync(); continue; }
+        WS(5);
+        // ---- backward ----
+        float dz[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) dz[nb] = sDz[nb * 16 + j];
+        // output layer: [dW_out | db_out] += sum_e [A_4 | 1][e] dz[e]; delta_4 = (dz w_out) m_4
+#pragma unroll
+        for (int s = 0; s < kR / 4; ++s) gO = mfma(R4[(4 * s + g) * R4S + j], sDz[4 * s + g], gO);
+        v4f d4[1][2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                d4[0][nb][r] = (dz[nb] * Wos[4 * g + r]) * mult(y4[0][nb][r], (kb >> (56 + nb * 4 + r)) & 1, training);
+        auto apply_mult = [&](auto &da, const auto &y, int bit0) {
+            constexpr int T = sizeof(da) / sizeof(da[0]);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        da[t][nb][r] = da[t][nb][r] * mult(y[t][nb][r], (kb >> (bit0 + (t * 2 + nb) * 4 + r)) & 1, training);
+        };
+        v4f d3[1][2];
+        bwd<1, 1>(d4, d3, W4s, S4, g, j);
+        wave_sync();                                           // A_4 reads done before delta_4 lands there
+        stage<1>(d4, R4, R4S, g, j);
+        unstage<1>(y3, R3, R3S, g, j);                         // A_3 back from its staged rows
+        apply_mult(d3, y3, 48);
+        wave_sync();
+        dw<1, 1>(gW4, gB4, R4, R4S, R3, R3S, g, j);            // dW4 += delta4^T A_3
+        v4f d2[2][2];
+        bwd<2, 1>(d3, d2, W3s, S3, g, j);
+        wave_sync();                                           // A_3 reads done before delta_3 lands there
+        stage<1>(d3, R3, R3S, g, j);
+        unstage<2>(y2, R2, R2S, g, j);
+        apply_mult(d2, y2, 32);
+        wave_sync();
+        dw<1, 2>(gW3, gB3, R3, R3S, R2, R2S, g, j);
+        WS(6);
+        // X0 with examples on the k axis for dW1 (lane (g, x): X0[4 s + g][16 t + x]), re-read
+        // from L2 in two halves (user columns now, item columns behind the first half of dW1);
+        // rows that are not valid pairs read row 0 (their delta is 0)
+        auto load_xn = [&](float (&xv)[8][4], int h) {
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) {
+                const int e = 4 * s2 + g, u = sU[e], i = sI[e];
+                const float *p = h == 0 ? a.user_w + (int64_t)(u >= 0 ? u : 0) * 64 + j
+                                        : a.item_w + (int64_t)(u >= 0 ? i : 0) * 64 + j;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xv[s2][t] = p[16 * t];
+            }
+        };
+        float xn[8][4];
+        load_xn(xn, 0);
+        v4f d1[4][2];
+        bwd<4, 2>(d2, d1, W2s, S2, g, j);
+        wave_sync();
+        stage<2>(d2, R2, R2S, g, j);
+        unstage<4>(y1, R1, R1S, g, j);
+        apply_mult(d1, y1, 0);
+        wave_sync();
+        WS(7);
+        dw<2, 4>(gW2, gB2, R2, R2S, R1, R1S, g, j);
+        WS(8);
+        wave_sync();
+        stage<4>(d1, R1, R1S, g, j);
+        wave_sync();
+        WS(9);
+        // dW1 += delta1^T X0 (X0 rows from the registers loaded above), db1 alongside
+        auto dw1_half = [&](int h) {
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) {
+                float av[4];
+#pragma unroll
+                for (int to = 0; to < 4; ++to) av[to] = R1[(4 * s2 + g) * R1S + 16 * to + j];
+#pragma unroll
+                for (int to = 0; to < 4; ++to) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) gW1[to][4 * h + t] = mfma(av[to], xn[s2][t], gW1[to][4 * h + t]);
+                    if (h == 0) gB1[to] = mfma(av[to], 1.0f, gB1[to]);
+                }
+            }
+        };
+        dw1_half(0);
+        load_xn(xn, 1);   // item columns, in flight during the dX0 halves
+        WS(10);
+        // dX0^T = W1^T delta1^T: the per-example input gradient rows, in two halves (user
+        // columns, item columns: 32 accumulators each beside the gradient accumulators), each
+        // stored at once, overflow rows (lists full) in fixed point
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            v4f dx[4][2];
+            bwd<4, 4>(d1, dx, W1s + 64 * h, S1, g, j);
+            if (h == 0) WS(11);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const int e = nb * 16 + j;
+                    *reinterpret_cast<v4f *>(a.contrib + (tile * kR + e) * (int64_t)128 + 64 * h + 16 * t + 4 * g) = dx[t][nb];
+                }
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int e = nb * 16 + j;
+                if ((h == 0 ? sLu[e] : sLi[e]) >= kNcfCap) {
+                    const int64_t row = h == 0 ? (int64_t)ue[nb] : a.num_users + ie[nb];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) fix_add(a.hot_grad + row * 64 + 16 * t + 4 * g + r, dx[t][nb][r]);
+                }
+            }
+            if (h == 1 && a.pos_slot != nullptr && j < tc) {
+                // the positives' (rows 0..tc-1, example block 0) item halves into R2 as [16][64]
+                // (delta2 is consumed; R1 still holds delta1 for the second half of dW1)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) *reinterpret_cast<v4f *>(R2 + j * 64 + 16 * t + 4 * g) = dx[t][0];
+            }
+        }
+        dw1_half(1);
+        WS(12);
+        if (a.pos_slot != nullptr) {
+            // planned positives: lane c runs the segments of equal plan slots in column order (the
+            // same sums as a per-segment loop)
+            wave_sync();
+            float acc = 0.0f;
+            int prev = -2;
+            for (int cl = 0; cl < tc; ++cl) {
+                const int slot = sPs[cl];
+                if (slot != prev) acc = 0.0f;
+                acc += R2[cl * 64 + lane];
+                prev = slot;
+                if (slot >= 0 && (cl + 1 == tc || sPs[cl + 1] != slot)) a.part_row[(int64_t)slot * 64 + lane] = acc;
+            }
+        }
+        wave_sync();
+        WS(13);
+    }
+    if constexpr (!kBackward) return;
+    // ---- the workgroup's weight-gradient partial: ((w0 + w2) + (w1 + w3)) -- waves 0 and 1 store
+    // into two LDS images, then waves 2 and 3 add into them (each address has one adder, so the
+    // sums are deterministic), and the global write adds the two images ----
+    float *red = lds;   // every wave is past its tiles (barrier below): weights and scratch are free
+    static_assert(2 * P <= kLdsFloats, "two gradient images");
+    __syncthreads();
+    for (int round = 0; round < 2; ++round) {
+        if ((wave >> 1) == round) {
+            float *img = red + (wave & 1) * P;
+            // this lane's values and their flat indices, in a fixed order
+            auto each = [&](auto &&f) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int orow = 4 * g + r;   // row of a 16x16 tile held in register r
+#pragma unroll
+                    for (int to = 0; to < 4; ++to)
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) f(S64::w_off(0) + (16 * to + orow) * 128 + 16 * t + j, gW1[to][t][r], true);
+#pragma unroll
+                    for (int to = 0; to < 2; ++to)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) f(S64::w_off(1) + (16 * to + orow) * 64 + 16 * t + j, gW2[to][t][r], true);
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) f(S64::w_off(2) + orow * 32 + 16 * t + j, gW3[0][t][r], true);
+                    f(S64::w_off(3) + min(orow, 7) * 16 + j, gW4[0][0][r], orow < 8);
+                    // bias tiles: every column holds the sum (taken from column 0)
+#pragma unroll
+                    for (int to = 0; to < 4; ++to) f(S64::w_off(0) + 64 * 128 + 16 * to + orow, gB1[to][r], j == 0);
+#pragma unroll
+                    for (int to = 0; to < 2; ++to) f(S64::w_off(1) + 32 * 64 + 16 * to + orow, gB2[to][r], j == 0);
+                    f(S64::w_off(2) + 16 * 32 + orow, gB3[0][r], j == 0);
+                    f(S64::w_off(3) + 8 * 16 + min(orow, 7), gB4[0][r], j == 0 && orow < 8);
+                    f(WO + min(orow, 8), gO[r], j == 0 && orow <= 8);   // w_out (8), then b_out
+                }
+            };
+            if (round == 0) {
+                each([&](int idx, float v, bool ok) { if (ok) img[idx] = v; });
+            } else {   // one adder per image and address: an LDS add with no return (fire and forget)
+                each([&](int idx, float v, bool ok) {
+                    if (ok) __hip_atomic_fetch_add(img + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                });
+            }
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < P; e += kThreads) a.wpart[(int64_t)blockIdx.x * P + e] = red[e] + red[P + e];
+}
+
+static bool ncf_use_wave(int E, int M) {
+    static const bool off = [] {
+        const char *s = getenv("RG_NCF_TILE");
+        return s && s[0] == '1';
+    }();
+    return E == 64 && M == 0 && !off;
+}
+
+template <int PHASE>
+static int ncf_wave_launch(NcfArgs &a, hipStream_t s, int blocks) {
+    const size_t lds = (size_t)ncfw::kLdsFloats * sizeof(float);
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(ncf_wave_kernel<PHASE>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+    if (!attr) return fail_arg("ncf_wave_kernel: cannot reserve LDS");
+    hipLaunchKernelGGL((ncf_wave_kernel<PHASE>), dim3(blocks), dim3(ncfw::kThreads), lds, s, a);
+    return check_launch("rg_ncf_pairs");
+}
+
 template <int PHASE>
 struct NcfLaunchF {
     NcfArgs *a;
@@ -882,6 +1608,10 @@ extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32
     const int64_t t = rg_ncf_tiles(cols, n_neg);
     const int lds = ncf_lds_floats(dim, mf_dim);
     if (t <= 0 || lds <= 0 || lds > kLdsMax || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
+    if (ncf_use_wave(dim, mf_dim)) {   // one wave per tile, 4 waves per workgroup, one workgroup per CU
+        const int64_t w = (t + ncfw::kWaves - 1) / ncfw::kWaves;
+        return w < 256 ? w : 256;
+    }
     int per_cu = kLdsMax / lds;
     if (per_cu > 4) per_cu = 4;
     const int64_t cap = 256 * (int64_t)per_cu;
@@ -940,6 +1670,14 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     a.mf_part_row = nw->mf_part_row;
     const int blocks = (int)rg_ncf_blocks(b->cols, b->n_neg, m->dim, m->mf_dim);
     if (blocks <= 0) return fail_arg("rg_ncf_pairs: no launch shape for this dim / mf_dim");
+    if (ncf_use_wave(m->dim, m->mf_dim)) {
+        hipStream_t st = (hipStream_t)stream;
+        if (phase == kNcfFused) return ncf_wave_launch<kNcfFused>(a, st, blocks);
+        if (phase == kNcfScores) return ncf_wave_launch<kNcfScores>(a, st, blocks);
+        if (phase == kNcfGivenDp) return ncf_wave_launch<kNcfGivenDp>(a, st, blocks);
+        if (phase == kNcfLossOnly) return ncf_wave_launch<kNcfLossOnly>(a, st, blocks);
+        return fail_arg("rg_ncf_pairs: bad phase");
+    }
     if (phase == kNcfFused) { NcfLaunchF<kNcfFused> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfScores) { NcfLaunchF<kNcfScores> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }
     if (phase == kNcfGivenDp) { NcfLaunchF<kNcfGivenDp> f{&a, (hipStream_t)stream, blocks}; return f(m->dim); }

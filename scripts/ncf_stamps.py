@@ -20,6 +20,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from recommendation_gans_amd import _lib, build  # noqa: E402
 
+WAVE_PHASES = ["ids+slots", "gather issue", "gather + fwd layer 1", "fwd rest + output", "loss", "dW4 dA3 dW3",
+               "X0 re-read issue + dA2", "dW2", "dA1 + stage", "dW1", "dX0", "contrib stores", "overflow + planned"]
 PHASES = ["ids+slots", "gather", "forward layer 0", "forward rest + output", "loss", "backward first layer", "backward rest + rows"]
 
 
@@ -28,6 +30,7 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--mf-dim", type=int, default=0)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--wave", action="store_true", help="the E = 64 wave-per-tile kernel (16 stamps per wave tile)")
     args = ap.parse_args()
     lib = _lib.load(build.DIAG_LIB)
     lib.rg_diag_set_ncf_stamps.argtypes = [ctypes.c_void_p]
@@ -51,6 +54,8 @@ def main():
                   weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=0, **extra)
     tu, ti = torch.from_numpy(data.train_u).to(dev), torch.from_numpy(data.train_i).to(dev)
     plans = [e.make_plan(ti[s * B:(s + 1) * B]) for s in range(args.steps)]
+    if args.wave:
+        return wave_main(lib, e, tu, ti, plans, args, B)
     buf = torch.zeros(e.blocks * 2 * 8, dtype=torch.int64, device=dev)
     res = {p: [] for p in PHASES}
     tile_us, starts = [], []
@@ -69,6 +74,36 @@ def main():
     _lib.check(lib.rg_diag_set_ncf_stamps(None), "stamps")
     print(json.dumps({"dim": E, "mf_dim": M, "blocks": e.blocks, "tile_us_median": round(float(np.median(tile_us)), 2),
                       "block_start_p90_us": round(float(np.median(starts)), 2),
+                      "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()}}, indent=1))
+
+
+def wave_main(lib, e, tu, ti, plans, args, B):
+    nw = e.blocks * 4
+    buf = torch.zeros(nw * 2 * 16, dtype=torch.int64, device=tu.device)
+    res = {p: [] for p in WAVE_PHASES}
+    tile_us, first_us, kern_us = [], [], []
+    for s in range(args.steps):
+        on = s >= args.steps // 2
+        buf.zero_()
+        _lib.check(lib.rg_diag_set_ncf_stamps(buf.data_ptr() if on else None), "stamps")
+        e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s])
+        torch.cuda.synchronize()
+        if on:
+            st = buf.view(nw, 2, 16).cpu().numpy().astype(np.int64)
+            t0 = st[:, 0, 0][st[:, 0, 0] > 0].min()
+            t = (st - t0) * 0.01
+            ok0 = st[:, 0, 13] > 0
+            for k, p in enumerate(WAVE_PHASES):
+                res[p].append(float(np.median(t[ok0, 0, k + 1] - t[ok0, 0, k])))
+            tile_us.append(float(np.median(t[ok0, 0, 13] - t[ok0, 0, 0])))
+            first_us.append(float(np.percentile(t[ok0, 0, 0], 90)))
+            ok1 = st[:, 1, 13] > 0
+            kern_us.append(float(max(t[ok0, 0, 13].max(), t[ok1, 1, 13].max() if ok1.any() else 0)))
+    _lib.check(lib.rg_diag_set_ncf_stamps(None), "stamps")
+    print(json.dumps({"kernel": "ncf_wave_kernel", "blocks": e.blocks, "waves": nw,
+                      "tile_us_median": round(float(np.median(tile_us)), 2),
+                      "wave_start_p90_us": round(float(np.median(first_us)), 2),
+                      "last_stamp_us": round(float(np.median(kern_us)), 2),
                       "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()}}, indent=1))
 
 
