@@ -944,11 +944,23 @@ __device__ __forceinline__ float mult(float y, bool keep, bool training) {
             unsigned long long t_;                                                                         \
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)"      \
                          : "=s"(t_)::"memory");                                                            \
-            if (lane == 0) g_ncf_stamps[(((int64_t)blockIdx.x * ncfw::kWaves + wave) * 2 + tl_) * 16 + (k)] = t_; \
+            if (lane == 0) g_ncf_stamps[(((int64_t)blockIdx.x * ncfw::kWaves + wave) * 3 + tl_) * 16 + (k)] = t_; \
+        }                                                                                                  \
+    } while (0)
+#define WSK(k)                                                                                             \
+    do {                                                                                                   \
+        if (g_ncf_stamps) {                                                                                \
+            unsigned long long t_;                                                                         \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)"      \
+                         : "=s"(t_)::"memory");                                                            \
+            if (lane == 0) g_ncf_stamps[(((int64_t)blockIdx.x * ncfw::kWaves + wave) * 3 + 2) * 16 + (k)] = t_; \
         }                                                                                                  \
     } while (0)
 #else
 #define WS(k) \
+    do {      \
+    } while (0)
+#define WSK(k) \
     do {      \
     } while (0)
 #endif
@@ -968,54 +980,70 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     uint32_t *sK = reinterpret_cast<uint32_t *>(sR + kR);
     float *sP = reinterpret_cast<float *>(sK + kR), *sDz = sP + kR, *sLa = sDz + kR, *sLb = sLa + kR;
     int *sLu = reinterpret_cast<int *>(sLb + kR), *sLi = sLu + kR, *sPs = sLi + kR;
+    WSK(0);   // kernel entry (diag: kernel-level record 2)
 
-    // ---- parameters into LDS: every thread's float4 loads issued before its LDS stores ----
+    // ---- parameters: every load issued first, then the LDS stores (the first tile's record is
+    // fetched in between), then one barrier ----
+    constexpr int kTail = kWFloats - oW4;   // W4 rows (8..15 zero), the output row, the biases
+    constexpr int PT1 = 64 * 128 / 4 / kThreads, PT2 = 32 * 64 / 4 / kThreads, PT3 = (16 * 32 / 4 + kThreads - 1) / kThreads;
+    constexpr int PTT = (kTail + kThreads - 1) / kThreads;
+    static_assert(64 * 128 / 4 % kThreads == 0 && 32 * 64 / 4 % kThreads == 0, "weight copy shape");
+    float4 wv1[PT1], wv2[PT2], wv3[PT3];
+    float wvt[PTT];
     {
-        auto copy = [&](auto cnt, int dst, int S, const float *src, int cols) {   // rows x cols (cols % 4 == 0)
-            constexpr int N4 = decltype(cnt)::value;
-            constexpr int PT = (N4 + kThreads - 1) / kThreads;
-            const int c4 = cols / 4;
-            float4 v[PT];
+        const float4 *W1 = reinterpret_cast<const float4 *>(a.mlp + S64::w_off(0));
+        const float4 *W2 = reinterpret_cast<const float4 *>(a.mlp + S64::w_off(1));
+        const float4 *W3 = reinterpret_cast<const float4 *>(a.mlp + S64::w_off(2));
 #pragma unroll
-            for (int k = 0; k < PT; ++k) {
-                const int e = tid + k * kThreads;
-                if (e < N4) v[k] = reinterpret_cast<const float4 *>(src)[e];
-            }
+        for (int k = 0; k < PT1; ++k) wv1[k] = W1[tid + k * kThreads];
 #pragma unroll
-            for (int k = 0; k < PT; ++k) {
-                const int e = tid + k * kThreads;
-                if (e < N4) *reinterpret_cast<float4 *>(sw + dst + (e / c4) * S + (e % c4) * 4) = v[k];
-            }
-        };
-        const float *W1 = a.mlp + S64::w_off(0), *W2 = a.mlp + S64::w_off(1), *W3 = a.mlp + S64::w_off(2),
-                    *W4 = a.mlp + S64::w_off(3);
-        copy(std::integral_constant<int, 64 * 128 / 4>{}, oW1, S1, W1, 128);
-        copy(std::integral_constant<int, 32 * 64 / 4>{}, oW2, S2, W2, 64);
-        copy(std::integral_constant<int, 16 * 32 / 4>{}, oW3, S3, W3, 32);
-        // the small tail [oW4, kWFloats): W4 rows 0..7 (rows 8..15 zero), the output row, biases
-        for (int e = tid; e < kWFloats - oW4; e += kThreads) {
-            const int o = oW4 + e;
-            float v = 0.0f;
+        for (int k = 0; k < PT2; ++k) wv2[k] = W2[tid + k * kThreads];
+#pragma unroll
+        for (int k = 0; k < PT3; ++k) wv3[k] = W3[min(tid + k * kThreads, 16 * 32 / 4 - 1)];
+#pragma unroll
+        for (int k = 0; k < PTT; ++k) {   // flat source index of LDS float oW4 + e (or -1: zero)
+            const int o = oW4 + min(tid + k * kThreads, kTail - 1);
+            int src = -1;
             if (o < oWo) {
                 const int row = (o - oW4) / S4, col = (o - oW4) % S4;
-                if (row < 8 && col < 16) v = W4[row * 16 + col];
+                if (row < 8 && col < 16) src = S64::w_off(3) + row * 16 + col;
             } else if (o < oB1) {
-                if (o - oWo < 8) v = a.mlp[WO + (o - oWo)];
+                if (o - oWo < 8) src = WO + (o - oWo);
             } else if (o < oB2) {
-                v = W1[64 * 128 + (o - oB1)];
+                src = S64::w_off(0) + 64 * 128 + (o - oB1);
             } else if (o < oB3) {
-                v = W2[32 * 64 + (o - oB2)];
+                src = S64::w_off(1) + 32 * 64 + (o - oB2);
             } else if (o < oB4) {
-                v = W3[16 * 32 + (o - oB3)];
+                src = S64::w_off(2) + 16 * 32 + (o - oB3);
             } else if (o < oBo) {
-                if (o - oB4 < 8) v = W4[8 * 16 + (o - oB4)];
+                if (o - oB4 < 8) src = S64::w_off(3) + 8 * 16 + (o - oB4);
             } else if (o == oBo) {
-                v = a.mlp[WO + 8];
+                src = WO + 8;
             }
-            sw[o] = v;
+            const float v = a.mlp[src < 0 ? 0 : src];
+            wvt[k] = src < 0 ? 0.0f : v;
         }
     }
-    __syncthreads();
+    auto store_weights = [&]() {
+#pragma unroll
+        for (int k = 0; k < PT1; ++k) {
+            const int e = tid + k * kThreads;
+            *reinterpret_cast<float4 *>(sw + oW1 + (e / 32) * S1 + (e % 32) * 4) = wv1[k];
+        }
+#pragma unroll
+        for (int k = 0; k < PT2; ++k) {
+            const int e = tid + k * kThreads;
+            *reinterpret_cast<float4 *>(sw + oW2 + (e / 16) * S2 + (e % 16) * 4) = wv2[k];
+        }
+#pragma unroll
+        for (int k = 0; k < PT3; ++k) {
+            const int e = tid + k * kThreads;
+            if (e < 16 * 32 / 4) *reinterpret_cast<float4 *>(sw + oW3 + (e / 8) * S3 + (e % 8) * 4) = wv3[k];
+        }
+#pragma unroll
+        for (int k = 0; k < PTT; ++k)
+            if (tid + k * kThreads < kTail) sw[oW4 + tid + k * kThreads] = wvt[k];
+    };
     const float *W1s = sw + oW1, *W2s = sw + oW2, *W3s = sw + oW3, *W4s = sw + oW4, *Wos = sw + oWo;
     const bool training = a.training != 0;
     const int n = a.n_neg, NP = n + 1, tc = a.tc;
@@ -1077,18 +1105,13 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     const int64_t first = (int64_t)blockIdx.x * kWaves + wave;
     RowRaw nxt{};   // the next tile's record (lanes 0..31), in flight during this tile
     if (lane < kR) nxt = fetch_row(first, lane);
-    for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
-        int tc = a.tc;   // opaque per tile: keeps the loss / row addresses from being hoisted (and spilled)
-        asm volatile("" : "+s"(tc));
-        const int tl_ = (int)((tile - first) / waves_total);
-        (void)tl_;
-        WS(0);
-        // ---- row ids (lanes 0..31: row r = q * tc + cl), as the tile kernel ----
-        int ru = -1, ri = -1, rps = -1;
+    // a tile's start: its record resolved into the wave's row arrays, the gather of X0 issued
+    auto begin_tile = [&](int tcl, int &ru, int &ri, int &rps, int (&ue)[2], int (&ie)[2], int (&re)[2],
+                          uint32_t (&ke)[2], v4f (&x0)[8][2]) {
         int64_t ngj = 0;
-        if (lane < kR) finish_row(nxt, ru, ri, rps, ngj);
         if (lane < kR) {
-            const int r = lane, q = r / tc;
+            finish_row(nxt, ru, ri, rps, ngj);
+            const int r = lane, q = r / tcl;
             sU[r] = ru;
             sI[r] = ri;
             sR[r] = (int)ngj;
@@ -1097,9 +1120,6 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             sPs[r] = rps;
         }
         wave_sync();
-        WS(1);
-        int ue[2], ie[2], re[2];
-        uint32_t ke[2];
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             ue[nb] = sU[nb * 16 + j];
@@ -1110,7 +1130,6 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         // ---- gather X0^T (T layout): features 16 t + 4 g .. + 3 of example nb * 16 + j; a row
         // that is not a valid pair reads row 0 (its dz is 0, so none of its values reach a
         // gradient, and its score is never used) ----
-        v4f x0[8][2];
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             const float *pu = a.user_w + (int64_t)(ue[nb] >= 0 ? ue[nb] : 0) * 64 + 4 * g;
@@ -1118,6 +1137,20 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
             for (int t = 0; t < 8; ++t) x0[t][nb] = *reinterpret_cast<const v4f *>(t < 4 ? pu + 16 * t : pi + 16 * (t - 4));
         }
+    };
+    store_weights();   // (the first record's loads above are in flight meanwhile)
+    __syncthreads();
+    for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
+        int tc = a.tc;   // opaque per tile: keeps the loss / row addresses from being hoisted (and spilled)
+        asm volatile("" : "+s"(tc));
+        const int tl_ = (int)((tile - first) / waves_total);
+        (void)tl_;
+        WS(0);
+        int ru = -1, ri = -1, rps = -1, ue[2], ie[2], re[2];
+        uint32_t ke[2];
+        v4f x0[8][2];
+        begin_tile(tc, ru, ri, rps, ue, ie, re, ke, x0);
+        WS(1);
         // dropout bits of every unit of the tile, computed while the gather is in flight
         // (bit (t * 2 + nb) * 4 + r of a layer's word: feature 16 t + 4 g + r, example nb * 16 + j)
         auto keep_bits = [&](auto tc_, int out, int mask_base) -> uint32_t {
@@ -1462,7 +1495,9 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     // sums are deterministic), and the global write adds the two images ----
     float *red = lds;   // every wave is past its tiles (barrier below): weights and scratch are free
     static_assert(2 * P <= kLdsFloats, "two gradient images");
+    WSK(1);   // tiles done
     __syncthreads();
+    WSK(2);   // the workgroup's last wave is done
     for (int round = 0; round < 2; ++round) {
         if ((wave >> 1) == round) {
             float *img = red + (wave & 1) * P;
@@ -1494,15 +1529,52 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             };
             if (round == 0) {
                 each([&](int idx, float v, bool ok) { if (ok) img[idx] = v; });
-            } else {   // one adder per image and address: an LDS add with no return (fire and forget)
-                each([&](int idx, float v, bool ok) {
-                    if (ok) __hip_atomic_fetch_add(img + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                });
+            } else {   // one adder per image and address: read a group, add, store (a round trip per group)
+                auto group = [&](auto nv, auto &&idx_of, auto &&val_of, auto &&ok_of) {
+                    constexpr int N = decltype(nv)::value;
+                    float cur[N];
+#pragma unroll
+                    for (int q = 0; q < N; ++q) cur[q] = ok_of(q) ? img[idx_of(q)] : 0.0f;
+#pragma unroll
+                    for (int q = 0; q < N; ++q)
+                        if (ok_of(q)) img[idx_of(q)] = cur[q] + val_of(q);
+                };
+                using I32 = std::integral_constant<int, 32>;
+                using I16 = std::integral_constant<int, 16>;
+                using I8 = std::integral_constant<int, 8>;
+                using I4 = std::integral_constant<int, 4>;
+                auto yes = [](int) { return true; };
+#pragma unroll
+                for (int to = 0; to < 4; ++to)   // W1: (to, t, r)
+                    group(I32{}, [&](int q) { return S64::w_off(0) + (16 * to + 4 * g + (q & 3)) * 128 + 16 * (q >> 2) + j; },
+                          [&](int q) { return gW1[to][q >> 2][q & 3]; }, yes);
+#pragma unroll
+                for (int to = 0; to < 2; ++to)   // W2
+                    group(I16{}, [&](int q) { return S64::w_off(1) + (16 * to + 4 * g + (q & 3)) * 64 + 16 * (q >> 2) + j; },
+                          [&](int q) { return gW2[to][q >> 2][q & 3]; }, yes);
+                group(I8{}, [&](int q) { return S64::w_off(2) + (4 * g + (q & 3)) * 32 + 16 * (q >> 2) + j; },
+                      [&](int q) { return gW3[0][q >> 2][q & 3]; }, yes);
+                group(I4{}, [&](int q) { return S64::w_off(3) + min(4 * g + q, 7) * 16 + j; },
+                      [&](int q) { return gW4[0][0][q]; }, [&](int q) { return 4 * g + q < 8; });
+                if (j == 0) {   // bias tiles (column 0) and the output row
+                    group(I16{}, [&](int q) { return S64::w_off(0) + 64 * 128 + 16 * (q >> 2) + 4 * g + (q & 3); },
+                          [&](int q) { return gB1[q >> 2][q & 3]; }, yes);
+                    group(I8{}, [&](int q) { return S64::w_off(1) + 32 * 64 + 16 * (q >> 2) + 4 * g + (q & 3); },
+                          [&](int q) { return gB2[q >> 2][q & 3]; }, yes);
+                    group(I4{}, [&](int q) { return S64::w_off(2) + 16 * 32 + 4 * g + q; },
+                          [&](int q) { return gB3[0][q]; }, yes);
+                    group(I4{}, [&](int q) { return S64::w_off(3) + 8 * 16 + min(4 * g + q, 7); },
+                          [&](int q) { return gB4[0][q]; }, [&](int q) { return 4 * g + q < 8; });
+                    group(I4{}, [&](int q) { return WO + min(4 * g + q, 8); },
+                          [&](int q) { return gO[q]; }, [&](int q) { return 4 * g + q <= 8; });
+                }
             }
         }
         __syncthreads();
+        WSK(3 + round);   // round 0 stored, round 1 added
     }
     for (int e = tid; e < P; e += kThreads) a.wpart[(int64_t)blockIdx.x * P + e] = red[e] + red[P + e];
+    WSK(5);   // kernel exit
 }
 
 static bool ncf_use_wave(int E, int M) {

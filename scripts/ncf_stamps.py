@@ -79,9 +79,9 @@ def main():
 
 def wave_main(lib, e, tu, ti, plans, args, B):
     nw = e.blocks * 4
-    buf = torch.zeros(nw * 2 * 16, dtype=torch.int64, device=tu.device)
+    buf = torch.zeros(nw * 3 * 16, dtype=torch.int64, device=tu.device)
     res = {p: [] for p in WAVE_PHASES}
-    tile_us, first_us, kern_us = [], [], []
+    tile_us, first_us, kern_us, pro, red_us, wr_us, tiles_done, bar_wait, ends = [], [], [], [], [], [], [], [], []
     for s in range(args.steps):
         on = s >= args.steps // 2
         buf.zero_()
@@ -89,7 +89,7 @@ def wave_main(lib, e, tu, ti, plans, args, B):
         e.train_step(tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], plan=plans[s])
         torch.cuda.synchronize()
         if on:
-            st = buf.view(nw, 2, 16).cpu().numpy().astype(np.int64)
+            st = buf.view(nw, 3, 16).cpu().numpy().astype(np.int64)
             t0 = st[:, 0, 0][st[:, 0, 0] > 0].min()
             t = (st - t0) * 0.01
             ok0 = st[:, 0, 13] > 0
@@ -97,13 +97,27 @@ def wave_main(lib, e, tu, ti, plans, args, B):
                 res[p].append(float(np.median(t[ok0, 0, k + 1] - t[ok0, 0, k])))
             tile_us.append(float(np.median(t[ok0, 0, 13] - t[ok0, 0, 0])))
             first_us.append(float(np.percentile(t[ok0, 0, 0], 90)))
-            ok1 = st[:, 1, 13] > 0
-            kern_us.append(float(max(t[ok0, 0, 13].max(), t[ok1, 1, 13].max() if ok1.any() else 0)))
+            # record 2 (kernel level): 0 entry, 1 tiles done, 2 after the workgroup barrier,
+            # 3 / 4 reduction rounds, 5 exit
+            k2 = t[:, 2, :]
+            kern_us.append(float(k2[:, 5].max() - k2[:, 0].min()))
+            pro.append(float(np.median(t[ok0, 0, 0] - k2[ok0, 0])))
+            tiles_done.append(float(np.median(k2[:, 1] - k2[:, 0])))
+            bar_wait.append(float(np.median(k2[:, 2] - k2[:, 1])))
+            red_us.append(float(np.median(k2[:, 4] - k2[:, 2])))
+            wr_us.append(float(np.median(k2[:, 5] - k2[:, 4])))
+            ends.append(float(np.max(k2[:, 1]) - np.min(k2[:, 0])))
     _lib.check(lib.rg_diag_set_ncf_stamps(None), "stamps")
     print(json.dumps({"kernel": "ncf_wave_kernel", "blocks": e.blocks, "waves": nw,
                       "tile_us_median": round(float(np.median(tile_us)), 2),
                       "wave_start_p90_us": round(float(np.median(first_us)), 2),
-                      "last_stamp_us": round(float(np.median(kern_us)), 2),
+                      "kernel_entry_to_exit_us": round(float(np.median(kern_us)), 2),
+                      "prologue_us_median": round(float(np.median(pro)), 2),
+                      "entry_to_tiles_done_us_median": round(float(np.median(tiles_done)), 2),
+                      "last_wave_tiles_done_us": round(float(np.median(ends)), 2),
+                      "barrier_wait_us_median": round(float(np.median(bar_wait)), 2),
+                      "reduction_us_median": round(float(np.median(red_us)), 2),
+                      "partial_write_us_median": round(float(np.median(wr_us)), 2),
                       "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()}}, indent=1))
 
 
