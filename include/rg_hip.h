@@ -514,7 +514,10 @@ typedef struct rg_mf_stepper_config {
     double lr_d, beta1_d, beta2_d;  /* the same as Python floats (Adam bias corrections) */
     int64_t step;                   /* optimizer steps already taken */
     int64_t n_partials;
-    int32_t current_set, pad_;
+    int32_t current_set;
+    int32_t gen_mode;               /* 0: MT words walked inside the step's dense pass when that hides
+                                       them (rg_mf_stepper_train); 1: the consumer has no such pass
+                                       (NCF / NeuMF): 8-step slots on the generator stream */
     /* dp_mode 1: the replicated, reference-exact data-parallel step (rg_mf_grads_sharded ->
      * reduce-scatter -> rg_mf_apply_shard -> all-gather), rank `rank` of `world`; every rank
      * consumes columns [col_offset, col_offset + cols) of one global draw of global_cols
@@ -557,6 +560,9 @@ int rg_mf_stepper_release(void *stepper, void *stream);
  * (ordered after the work `stream` holds), so the next acquire with the same input finds
  * them ready.  A different input there prepares again. */
 int rg_mf_stepper_prefetch(void *stepper, void *stream, const rg_mf_step_in_t *next);
+/* The same prepare enqueued on `stream` itself (no side stream, no events): for callers that
+ * enqueue it after their step's last kernel (the NCF / NeuMF engines). */
+int rg_mf_stepper_prefetch_inline(void *stepper, void *stream, const rg_mf_step_in_t *next);
 /* The replicated data-parallel step (dp_mode 1) in two halves around a caller-run
  * exchange (comm == NULL; tests, gloo): dp_begin = prepare / pairs / release / the next
  * step's prepare / rg_mf_grads_sharded into grad_buf; the caller reduce-scatters grad_buf;

@@ -89,7 +89,7 @@ class MFStepperConfig(ctypes.Structure):
                 ("global_cols", ctypes.c_int64), ("neg_cols", ctypes.c_int64), ("item_grad", ctypes.c_void_p),
                 ("comm", ctypes.c_void_p), ("opt", Opt), ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double),
                 ("beta2_d", ctypes.c_double), ("step", ctypes.c_int64), ("n_partials", ctypes.c_int64),
-                ("current_set", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("current_set", ctypes.c_int32), ("gen_mode", ctypes.c_int32),
                 ("dp_mode", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("pad2_", ctypes.c_int32), ("shard_users", ctypes.c_int64), ("shard_items", ctypes.c_int64),
                 ("grad_buf", ctypes.c_void_p), ("owner_rec", ctypes.c_void_p * 2), ("owner_seg", ctypes.c_void_p * 2),
@@ -223,6 +223,7 @@ SIGNATURES = [
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     ("rg_mf_stepper_prefetch", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn)]),
+    ("rg_mf_stepper_prefetch_inline", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn)]),
     ("rg_topk_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

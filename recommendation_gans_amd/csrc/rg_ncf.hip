@@ -722,6 +722,15 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
     if (e < P) {
         float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         int k = k0;
+        // batches of 16 partials: every load of a batch in flight before the (unchanged)
+        // four-chain sums consume them
+        for (; k + 16 <= k1; k += 16) {
+            float v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = wpart[(int64_t)(k + q) * P + e];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) c[q & 3] += v[q];
+        }
         for (; k + 4 <= k1; k += 4) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) c[j] += wpart[(int64_t)(k + j) * P + e];

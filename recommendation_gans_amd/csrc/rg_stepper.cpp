@@ -318,6 +318,27 @@ int prepare_side(Stepper &st, hipStream_t consumer, int64_t unit, const rg_mf_st
     return RG_OK;
 }
 
+// the same prepare on the consumer stream itself, in stream order (no events: a caller that
+// enqueues it after the step's last kernel trades the prepare's few microseconds for the two
+// cross-queue hops of prepare_side, each a bubble of ~10 us on the consumer queue)
+int prepare_inline(Stepper &st, hipStream_t consumer, int64_t unit, const rg_mf_step_in_t &in) {
+    int rc = keep_ahead(st, unit);
+    if (rc) return rc;
+    const int b = (int)(unit % 2);
+    if ((rc = wait_side(st, consumer, b))) return rc;   // an earlier side write of this buffer
+    if ((rc = wait_words(st, consumer, unit))) return rc;
+    const rg_mf_work_t w = work_for(st, in);
+    const rg_mf_batch_t batch = make_batch(st, in, unit);
+    if ((rc = rg_mf_prepare(consumer, &batch, &w))) return rc;
+    st.side_pending[b] = false;
+    st.prepared = true;
+    st.prep_unit = unit;
+    st.prep_in = in;
+    st.prep_serial = 0;
+    st.prep_claimed = false;
+    return RG_OK;
+}
+
 int ensure_stamps(Stepper &st) {
     if (st.stamp[0]) return RG_OK;
     const rg_mf_tables_t &t = st.cfg.tables[0];
@@ -1036,6 +1057,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         const char *im = getenv("RG_MT_INLINE");
         const int mode = im ? atoi(im) : 1;
         st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
+                         (cfg->gen_mode == 0 || mode == 2) &&
                          cfg->dp_mode == 0 && (mode == 2 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
         st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
@@ -1254,6 +1276,14 @@ extern "C" int rg_mf_stepper_prefetch(void *h, void *stream, const rg_mf_step_in
     if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next) && !st->prep_claimed)
         return RG_OK;
     return prepare_side(*st, (hipStream_t)stream, st->taken, *next);
+}
+
+extern "C" int rg_mf_stepper_prefetch_inline(void *h, void *stream, const rg_mf_step_in_t *next) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !next) return rg::fail_arg("rg_mf_stepper_prefetch_inline: null argument");
+    if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next) && !st->prep_claimed)
+        return RG_OK;
+    return prepare_inline(*st, (hipStream_t)stream, st->taken, *next);
 }
 
 extern "C" int rg_mf_stepper_opt(void *h, int64_t step, rg_opt_t *out) {

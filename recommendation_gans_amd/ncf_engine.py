@@ -24,6 +24,7 @@ data gradients (rg_ncf_grads, rg_ncf_mlp_grad) go into one flat buffer that is a
 update (rg_ncf_apply_dense, rg_ncf_mlp_apply).  R ranks at batch B equal one process at
 batch R*B."""
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -124,6 +125,7 @@ class NCFEngine:
         self.seed = int(seed)
         self.t = 0
         self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
+        self._prefetch_side = os.environ.get("RG_NCF_PREFETCH_SIDE") == "1"
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
                                     self.U, self.I, E, self.M)
@@ -146,6 +148,9 @@ class NCFEngine:
         cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, self.rank * B, B * self.world, B * self.world
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
+        # no fused dense pass walks the MT words here: 8-step slots on the generator stream (one
+        # walk and one cross-stream hop per 8 steps instead of per step)
+        cfg.gen_mode = 0 if os.environ.get("RG_NCF_GEN_INLINE") == "1" else 1
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())
@@ -288,13 +293,14 @@ class NCFEngine:
         if next_step is not None:
             nu, ni, nplan = next_step
             self._next_in = self._step_in_of(nu, ni, None, nplan)
-            check(self.lib.rg_mf_stepper_prefetch(self._stepper, stream, ctypes.byref(self._next_in)),
-                  "rg_mf_stepper_prefetch")
+            if self._prefetch_side:
+                check(self.lib.rg_mf_stepper_prefetch(self._stepper, stream, ctypes.byref(self._next_in)),
+                      "rg_mf_stepper_prefetch")
         o = self._opt(self.t)
         parts = self.adapt_partials if self.loss == "adaptive_hinge" else self.partials
         out = self.loss_out if loss_out is None else loss_out
         if self.world > 1:
-            return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce)
+            return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce, next_step)
         check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
                                      ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
               "rg_ncf_update")
@@ -304,10 +310,18 @@ class NCFEngine:
         else:
             check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
                                         ctypes.byref(o), 0, -1), "rg_ncf_apply")
+        self._prefetch_tail(next_step, stream)
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out
 
-    def _dp_update(self, work, nw, o, parts, global_pos, out, stream, allreduce):
+    def _prefetch_tail(self, next_step, stream):
+        """The next step's negatives prepared at the end of this step, on the same stream (no
+        cross-stream events; RG_NCF_PREFETCH_SIDE=1: on the side stream beside the updates)."""
+        if next_step is not None and not self._prefetch_side:
+            check(self.lib.rg_mf_stepper_prefetch_inline(self._stepper, stream, ctypes.byref(self._next_in)),
+                  "rg_mf_stepper_prefetch_inline")
+
+    def _dp_update(self, work, nw, o, parts, global_pos, out, stream, allreduce, next_step=None):
         """Data-parallel second half: data gradients -> one all-reduce -> the same update on
         every rank."""
         M, ref = self._model, ctypes.byref
@@ -326,6 +340,7 @@ class NCFEngine:
         if self.neumf:
             check(self.lib.rg_ncf_apply_dense(stream, ref(M), ptr(self.dp_gmf), ref(o), 0, -1, 1),
                   "rg_ncf_apply_dense(gmf)")
+        self._prefetch_tail(next_step, stream)
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out
 
