@@ -297,7 +297,9 @@ def bench_ncf(args):
                       "mf_embedding_dim": M,
                       "parallelism": f"dp{world}" + (" replicated (embedding + MLP gradient all-reduce, "
                                                      "reference-exact)" if world > 1 else "")},
-           "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (ncf_pairs_kernel)", "achieved": ach,
+           "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (" + ("ncf_wave_kernel" if E == 64 and not neumf
+                                                                    and os.environ.get("RG_NCF_TILE") != "1"
+                                                                    else "ncf_pairs_kernel") + ")", "achieved": ach,
                         "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
                         "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
            "final_loss": float(eng.loss_out[0])}

@@ -115,3 +115,19 @@ def test_no_gpu_means_loud_failure():
         assert "GPU" in str(e)
     else:
         raise AssertionError("require_gpu must raise without a GPU")
+
+
+def test_ncf_launch_geometry():
+    """Host-side shape functions (no GPU): the E = 64 MLP runs one wave per 32-row tile,
+    4 waves per workgroup, at most 256 workgroups (= weight-gradient partials); the other
+    towers keep the tile kernel's workgroup-per-tile count (capped by LDS residency)."""
+    from recommendation_gans_amd import _lib
+    L = _lib.load()
+    assert L.rg_ncf_rows_per_tile() == 32
+    assert L.rg_ncf_cols_per_tile(5) == 5 and L.rg_ncf_tiles(8192, 5) == 1639
+    wave = os.environ.get("RG_NCF_TILE") != "1"
+    assert L.rg_ncf_blocks(8192, 5, 64, 0) == (256 if wave else 256)
+    assert L.rg_ncf_blocks(1000, 5, 64, 0) == ((200 + 3) // 4 if wave else 200)
+    assert L.rg_ncf_blocks(20, 5, 64, 0) == (1 if wave else 4)
+    assert L.rg_ncf_blocks(1000, 5, 16, 50) == 200   # NeuMF: the tile kernel, one workgroup per tile
+    assert L.rg_ncf_blocks(8192, 5, 48, 0) == -1     # unsupported width
