@@ -702,7 +702,19 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
     }
     if ((loss_out || mode == 1) && loss_partials && blockIdx.x == 0 && wave == 0) {
         double sa = 0.0, sb = 0.0;
-        for (int64_t i = lane; i < n_partials; i += 64) {
+        int64_t i = lane;
+        // batches of 8 strided pairs: the loads of a batch in flight before the same in-order sums
+        for (; i + 7 * 64 < n_partials; i += 8 * 64) {
+            float2 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = reinterpret_cast<const float2 *>(loss_partials)[i + q * 64];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                sa += (double)v[q].x;
+                sb += (double)v[q].y;
+            }
+        }
+        for (; i < n_partials; i += 64) {
             sa += (double)loss_partials[2 * i];
             sb += (double)loss_partials[2 * i + 1];
         }
@@ -1149,6 +1161,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     };
     store_weights();   // (the first record's loads above are in flight meanwhile)
     __syncthreads();
+    float warm = 0.0f;   // the next tile's embedding lines, touched during this tile's backward
     for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
         int tc = a.tc;   // opaque per tile: keeps the loss / row addresses from being hoisted (and spilled)
         asm volatile("" : "+s"(tc));
@@ -1159,6 +1172,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         uint32_t ke[2];
         v4f x0[8][2];
         begin_tile(tc, ru, ri, rps, ue, ie, re, ke, x0);
+        if (warm == 1.0e30f && a.n_pos < 0) a.scores[0] = warm;   // keeps the warm-up loads (never taken)
         WS(1);
         // dropout bits of every unit of the tile, computed while the gather is in flight
         // (bit (t * 2 + nb) * 4 + r of a layer's word: feature 16 t + 4 g + r, example nb * 16 + j)
@@ -1358,6 +1372,12 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             a.loss_partials[2 * tile + 1] = lb;
         }
         if (PHASE == kNcfLossOnly) { wave_sync(); continue; }
+        // the next tile's rows (its record arrived during the loss): one load per 128-B line of
+        // each user / item row, so its gather at the next tile's start hits L2
+        if (lane < kR && nxt.valid) {
+            const float *pu = a.user_w + (int64_t)nxt.pr.x * 64, *pi = a.item_w + (int64_t)nxt.pr.y * 64;
+            warm += (pu[0] + pu[32]) + (pi[0] + pi[32]);
+        }
         WS(5);
         // ---- backward ----
         float dz[2];
