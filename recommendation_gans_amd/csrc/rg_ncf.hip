@@ -1108,10 +1108,15 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         if (valid && w.q == 0) valid = w.s < a.n_pos;
         if (valid && w.q > 0 && pairwise) valid = w.s < a.n_pos;
         w.valid = valid;
-        const int64_t sc = w.s < a.cols ? w.s : a.cols - 1;
-        w.pr = a.pairs[sc * pair_stride(a.n_neg) + min(w.q, n)];
-        w.ps = a.pos_slot != nullptr ? a.pos_slot[sc] : -1;
-        w.perm = a.perm ? a.perm[sc] : 0;
+        w.pr = make_int2(-1, -1);
+        w.ps = -1;
+        w.perm = 0;
+        if (tile < a.tiles) {   // (a tile past the end has no record to read: cols may be 0)
+            const int64_t sc = w.s < a.cols ? w.s : a.cols - 1;
+            w.pr = a.pairs[sc * pair_stride(a.n_neg) + min(w.q, n)];
+            w.ps = a.pos_slot != nullptr ? a.pos_slot[sc] : -1;
+            w.perm = a.perm ? a.perm[sc] : 0;
+        }
         return w;
     };
     auto finish_row = [&](const RowRaw &w, int &u, int &i, int &ps, int64_t &gj) {
