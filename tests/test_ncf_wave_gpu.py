@@ -60,3 +60,43 @@ def test_ncf_e64_kernel_losses_and_shapes(loss, n, planned):
             ok, msg = omf.tensor_parity(p.reshape(r32.shape), r32, r64, before=b0)
             assert ok, f"{loss} n={n} step {s} {nm}: {msg}"
     assert int(e.row_count.abs().sum()) == 0 and float(e.hot_grad.abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("loss", ["pointwise", "bpr", "hinge", "adaptive_hinge"])
+def test_ncf_e64_validation_loss(loss):
+    """run_val_iteration (implicit.py:366-379) through the E = 64 kernel's loss-only phase
+    (eval mode: LeakyReLU without dropout) and, for adaptive hinge, its scores phase: the loss
+    of a batch against a float64 eval-mode forward on the same negatives (1e-5 relative), and
+    the MT stream advanced exactly as the reference's draw."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    dev = torch.device("cuda:0")
+    U, I, E, B, n = 900, 700, 64, 700, 5
+    torch.manual_seed(4)
+    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    params = [p.detach().clone() for p in net.parameters()]
+    rs = np.random.RandomState(21)
+    pool_u, pool_i = rs.randint(0, U, 20000), rs.randint(0, I, 20000)
+    mt = orng.py_seed_state(9)
+    e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, mt.copy(), loss=loss, optimizer="adam",
+                  lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev)
+    P = [t.double() for t in params]
+
+    def eval_p(u, i):
+        a = torch.cat([P[0][u], P[1][i]], 1)
+        for k in range(2, len(P) - 2, 2):
+            z = a @ P[k].T + P[k + 1]
+            a = torch.where(z > 0, z, z * 0.1)
+        return torch.sigmoid(a @ P[-2].T + P[-1]).reshape(-1)
+    state = mt.copy()
+    for s in range(2):
+        pu = torch.from_numpy(rs.randint(0, U, B))
+        pi = torch.from_numpy(rs.randint(0, I, B))
+        got = float(e.val_loss(pu.to(dev), pi.to(dev))[0])
+        idx = torch.from_numpy(orng.py_choices_indices(state, len(pool_u), n * B)).long()
+        nu, ni = torch.as_tensor(pool_u).long()[idx], torch.as_tensor(pool_i).long()[idx]
+        ref, _, _ = omf.loss_and_dp(loss, eval_p(pu, pi), eval_p(nu, ni), n, B)
+        torch.cuda.synchronize()
+        assert abs(got - float(ref)) <= 1e-5 * abs(float(ref)), (loss, s, got, float(ref))
+        assert (e.mt_state() == state).all(), f"MT state after validation batch {s}"
