@@ -19,7 +19,7 @@ for s, e, n, q in ks:
         gaps[n].append((s - last_end[q]) / 1e3)
     last_end[q] = e
 span = (ks[-1][1] - ks[0][0]) / 1e3
-npairs = len(dur.get("mf_pairs_kernel") or dur.get("ncf_wave_kernel") or dur.get("ncf_pairs_kernel") or [1])
+npairs = len(dur.get("mf_pairs_kernel") or dur.get("owner_scores_kernel") or dur.get("ncf_wave_kernel") or dur.get("ncf_pairs_kernel") or [1])
 print(sys.argv[1], f"span/step {span / npairs:.1f} us")
 for n in dur:
     d, g = dur[n], gaps.get(n, [0])
