@@ -48,10 +48,12 @@ def up_to_date():
 DIAG_LIB = os.path.join(PKG, "librg_hip_diag.so")
 
 
-def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=()):
+def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=(), only=None):
     """diag=True: librg_hip_diag.so with the RG_DIAG_STAMPS phase stamps (scripts only;
     the product never loads it).  variant=NAME: _variants/librg_hip_NAME.so built with the
-    extra -D defines, for same-box A/B runs (scripts load it through RG_LIB)."""
+    extra -D defines, for same-box A/B runs (scripts load it through RG_LIB).  only=[src, ...]
+    (variants): compile just those sources with the defines and link the product's objects
+    for the rest."""
     if variant:
         os.makedirs(os.path.join(PKG, "_variants"), exist_ok=True)
         lib = os.path.join(PKG, "_variants", f"librg_hip_{variant}.so")
@@ -68,6 +70,9 @@ def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=
     procs, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
+        if variant and only and s not in only:
+            objs.append(os.path.join(PKG, "_obj", s + ".o"))
+            continue
         obj = os.path.join(objdir, s + ".o")
         objs.append(obj)
         lang = ["-x", "hip"] if s.endswith(".hip") else []
@@ -97,5 +102,6 @@ def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=
 if __name__ == "__main__":
     var = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else None
     defs = [a[2:] for a in sys.argv if a.startswith("-D")]
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, diag="--diag" in sys.argv, variant=var,
-                defines=defs))
+                defines=defs, only=only))

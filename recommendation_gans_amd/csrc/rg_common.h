@@ -240,6 +240,28 @@ struct RowLayout {
         }
     }
 
+    // write-through store (sc1): the bytes go to memory and the line leaves the XCD's L2, so
+    // the pass leaves no dirty lines for the end-of-kernel write-back (MI355X guide: "stores of
+    // each flavour")
+    __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int D, int sub,
+                                                    const float (&v)[EPL]) {
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f t = {v[0], v[1], v[2], v[3]};
+            float *p = base + row * (int64_t)(4 * LPU) + sub * 4;
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + LPU * e;
+                if (c < D) store1_wt(base + row * (int64_t)D + c, v[e]);
+            }
+        }
+    }
+    __device__ static __forceinline__ void store1_wt(float *p, float v) {
+        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    }
+
     __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base,
                                                    int64_t row, int D, int sub) {
         if constexpr (VEC) {

@@ -589,6 +589,9 @@ struct ApplyArgs {
     int32_t lazy_cap;             // > 0: a row that has missed this many steps is processed anyway
 };
 
+#ifndef RG_DENSE_WT
+#define RG_DENSE_WT 0
+#endif
 #ifndef RG_MF_SORTED_PULL
 #define RG_MF_SORTED_PULL 1
 #endif
@@ -760,10 +763,177 @@ __device__ __forceinline__ void catch_up(const ApplyArgs &a, float2 cl, int wmax
     }
 }
 
+#ifndef RG_LEAN_PULL
+#define RG_LEAN_PULL 0
+#endif
+#ifndef RG_LEAN_PG
+#define RG_LEAN_PG 2
+#endif
+// Ascending sort of the 8 list entries held one per lane (lanes sub 0..7 of each LPU-lane row
+// group; sub >= 8 hold +inf keys and sort among themselves): a bitonic network over lane
+// XOR partners, 6 compare-exchange stages of 64-bit keys.  The result (entry e on lane e) is
+// the order sort_entries gives, so the row sums its contributions in the same order.
+template <int LPU>
+__device__ __forceinline__ uint64_t lane_sort8(uint64_t key, int sub) {
+#pragma unroll
+    for (int k = 2; k <= 8; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = __shfl_xor(key, j, LPU);
+            const bool up = (sub & k) == 0;
+            const bool lower = (sub & j) == 0;
+            const uint64_t lo = key < o ? key : o, hi = key < o ? o : key;
+            key = (lower == up) ? lo : hi;
+        }
+    }
+    return key;
+}
+
+// Pull-and-update of unified row r (the single-GPU dense pass, MODE kApplyPull) with a small
+// register footprint: each row's 8 list entries are held one per lane and sorted across the
+// lanes (apply_row holds all 8 in every lane and sorts them in registers: 85 VGPRs, 5 waves per
+// SIMD, against 8 here for the streaming loads).  Same loads in the same round trip (count,
+// list, the item's partial-slot range beside p, m, v), partner rows PG at a time, the same
+// summation order (sorted entries, fma chain; overflowed rows in fixed point; planned
+// partials after), so the result is bit-identical to apply_row.
+template <class L>
+__device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t r, const int sub) {
+    constexpr int EPL = L::EPL, LPU = L::LPU, PG = RG_LEAN_PG;
+    static_assert(LPU >= kCap, "one list entry per lane");
+    const int D = a.dim;
+    const int t = r < a.num_users ? 0 : 1;
+    const int64_t lr_ = t ? r - a.num_users : r;
+    const bool adam = a.opt.kind == RG_OPT_ADAM;
+    const bool has_v = a.opt.kind != RG_OPT_SGD;
+    float p[EPL], m[EPL], v[EPL], g[EPL];
+    float pb = 0.0f, mb = 0.0f, vb = 0.0f, gb = 0.0f;
+    L::load(p, a.w_in[t], lr_, D, sub);
+    if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
+    if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
+    if (sub == 0 && a.has_bias) {
+        pb = a.b_in[t][lr_];
+        if (adam) mb = a.b_m[t][lr_];
+        if (has_v) vb = a.b_v[t][lr_];
+    }
+#ifdef RG_X_STREAMONLY   // timing experiments only (wrong results): p, m, v and biases alone
+    const int c = 0;
+    const int2 my = make_int2(0, 0);
+    const bool parts = false;
+#else
+    const int c = a.row_count[r];
+    const int2 my = sub < kCap ? a.row_list[r * kCap + sub] : make_int2(0, 0);
+    const bool parts = t == 1 && a.item_slot_off != nullptr;
+#endif
+    int s0 = 0, s1 = 0;
+    if (parts) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
+    L::zero(g);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int rowbase = lane & ~(LPU - 1);
+    if (__any(c > 0)) {
+        const int ne = c < kCap ? c : kCap;
+        uint64_t key = ent_key(my, sub < ne);
+#if RG_MF_SORTED_PULL
+        key = lane_sort8<LPU>(key, sub);
+#endif
+        const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
+        const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
+#ifdef RG_X_NOFIX   // timing experiments only (wrong results for overflowed rows)
+        const bool fixp = false;
+#else
+        const bool fixp = c > kCap;   // an overflowed row sums list and surplus in fixed point
+#endif
+        long long gf[EPL];
+        long long gbf = 0;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) gf[q] = 0;
+#pragma unroll
+        for (int h = 0; h < kCap; h += PG) {
+            if (h > 0 && !__any(ne > h)) break;
+            uint64_t k[PG];
+            float o[PG][EPL];
+#pragma unroll
+            for (int e = 0; e < PG; ++e) {
+                k[e] = __shfl(key, rowbase + h + e);
+                if (h + e < ne) L::load_strided(o[e], other, (int)(uint32_t)(k[e] >> 32), ostride, D, sub);
+                else L::zero(o[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < PG; ++e) {
+                if (h + e < ne) {
+                    const float dz = __uint_as_float((uint32_t)k[e]);
+                    if (fixp) {
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q) gf[q] += to_fix(dz * o[e][q]);
+                        gbf += to_fix(dz);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q) g[q] = fmaf(dz, o[e][q], g[q]);
+                        gb += dz;
+                    }
+                }
+            }
+        }
+        if (fixp) {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int cc = L::elem(sub, e);
+                if (L::VEC || cc < D) {
+                    long long *hp = a.hot_grad + r * (int64_t)D + cc;
+                    gf[e] += *hp;
+                    *hp = 0;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < EPL; ++q) g[q] = from_fix(gf[q]);
+            if (sub == 0 && a.has_bias) {
+                gbf += a.hot_bias_grad[r];
+                a.hot_bias_grad[r] = 0;
+            }
+            gb = from_fix(gbf);
+        }
+        if (sub == 0 && c > 0 && !a.keep_count) a.row_count[r] = 0;
+    }
+    if (parts) {   // planned positive partials of this item, in slot order
+        for (int sl = s0; sl < s1; sl += PG) {
+            float h[PG][EPL];
+            float hb[PG];
+#pragma unroll
+            for (int u = 0; u < PG; ++u) {
+                const int ss = sl + u < s1 ? sl + u : s0;
+                L::load(h[u], a.part_row, ss, D, sub);
+                hb[u] = a.has_bias ? a.part_bias[ss] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < PG; ++u) {
+                if (sl + u < s1) {
+#pragma unroll
+                    for (int q = 0; q < EPL; ++q) g[q] += h[u][q];
+                    gb += hb[u];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
+    L::store(a.w_out[t], lr_, D, sub, p);
+    if (adam) L::store(a.w_m[t], lr_, D, sub, m);
+    if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
+    if (sub == 0 && a.has_bias) {
+        pb = opt_update(a.opt, pb, gb, mb, vb);
+        a.b_out[t][lr_] = pb;
+        if (adam) a.b_m[t][lr_] = mb;
+        if (has_v) a.b_v[t][lr_] = vb;
+    }
+}
+
 template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false>
 __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub,
                                           const LazyRow lzr = LazyRow{}) {
     constexpr int EPL = L::EPL;
+    if constexpr (RG_LEAN_PULL && MODE == kApplyPull && !LAZY && !COLD && NT == 0 && L::LPU >= kCap) {
+        apply_row_lean<L>(a, r, sub);
+        return;
+    }
     const int64_t rb = a.row_begin, nr = a.row_end - rb;
     const int D = a.dim;
     const int t = r < a.num_users ? 0 : 1;          // 0: user table, 1: item table
@@ -1032,6 +1202,10 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         L::store_nt(a.w_out[t], lr_, D, sub, p);
         if (adam) L::store_nt(a.w_m[t], lr_, D, sub, m);
         if (has_v) L::store_nt(a.w_v[t], lr_, D, sub, v);
+    } else if (RG_DENSE_WT) {
+        L::store_wt(a.w_out[t], lr_, D, sub, p);
+        if (adam) L::store_wt(a.w_m[t], lr_, D, sub, m);
+        if (has_v) L::store_wt(a.w_v[t], lr_, D, sub, v);
     } else {
         L::store(a.w_out[t], lr_, D, sub, p);
         if (adam) L::store(a.w_m[t], lr_, D, sub, m);
@@ -1039,9 +1213,15 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     }
     if (sub == 0 && a.has_bias) {
         pb = opt_update(a.opt, pb, gb, mb, vb);
-        a.b_out[t][lr_] = pb;
-        if (adam) a.b_m[t][lr_] = mb;
-        if (has_v) a.b_v[t][lr_] = vb;
+        if (RG_DENSE_WT) {
+            L::store1_wt(a.b_out[t] + lr_, pb);
+            if (adam) L::store1_wt(a.b_m[t] + lr_, mb);
+            if (has_v) L::store1_wt(a.b_v[t] + lr_, vb);
+        } else {
+            a.b_out[t][lr_] = pb;
+            if (adam) a.b_m[t][lr_] = mb;
+            if (has_v) a.b_v[t][lr_] = vb;
+        }
     }
     if (lz && sub == 0) {
         a.last_rel[r] = (int32_t)((int64_t)a.lazy_t - a.lazy_base);
@@ -1167,7 +1347,12 @@ struct BackGrid {
 };
 
 template <class L, int NT, bool SPEC = false, bool OWN = false, bool LAZY = false, bool LSPEC = false>
-__global__ __launch_bounds__(kBlock) void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
+#ifdef RG_BACK_WAVES
+#define RG_BACK_ATTR __attribute__((amdgpu_waves_per_eu(RG_BACK_WAVES, 8)))
+#else
+#define RG_BACK_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
                                                         int64_t apply_blocks, MtGenArgs gen, BackGrid bg,
                                                         OwnerArgs own) {
     static_assert(kBlock == kOwnSeg, "an owner prepare segment is one workgroup");

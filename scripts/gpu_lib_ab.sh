@@ -20,7 +20,7 @@ for name in "$@"; do
   for st in "20 5" "200 20"; do
     set -- $st
     RG_LIB=$lib timeout -k 10 200 python3 bench.py --steps $1 --warmup $2 --no-cpu-baseline > gpurun_out/lab_${TAG}_${name}_$1.json 2>gpurun_out/lab_${TAG}_${name}_$1.err || exit $?
-    python3 -c "import json;d=json.load(open('gpurun_out/lab_${TAG}_${name}_$1.json'));print('$name', $1, round(d['value']/1e6,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2))"
+    python3 -c "import json;d=json.load(open('gpurun_out/lab_${TAG}_${name}_$1.json'));print('$name', $1, round(d['value']/1e6,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2), repr(d.get('final_loss')))"
   done
   (cd /tmp && RG_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/lab_prof_${TAG}_$name -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline > $R/gpurun_out/lab_prof_${TAG}_$name.json 2>$R/gpurun_out/lab_prof_${TAG}_$name.err) || exit $?
   python3 - "$R/gpurun_out/lab_prof_${TAG}_$name" "$name" <<'EOF'
