@@ -116,6 +116,49 @@ def dense_grads(U, I, ub, ib, u, i, dz):
     return dU, dI, dub, dib
 
 
+# Rounding noise of the gradient sums: an element's data gradient is a sum of n terms
+# dz * partner (biases: dz), each carrying a few units of rounding from the forward and from
+# the partner rows' own earlier rounding; summed in another fp32 order the result moves by a
+# random walk of n roundings.  The band is (C1 sqrt(n) + C0) u sum|terms| -- a statistical
+# scale, not a worst case ((n - 1) u sum|terms| would flag most of a Zipf-hot table), checked
+# against fp32 restatements that sum in permuted orders (tests/test_parity_cpu.py: the
+# largest observed deviation stays several times inside it).
+NOISE_U = 2.0 ** -24
+NOISE_C1, NOISE_C0 = 2.0, 4.0
+
+
+def pair_noise(U, I, nz, u, i):
+    """First-order bound on how far an fp32 implementation's score logit z of each pair can be
+    from this one's, given the parameters' noise bands nz = [nU, nI, nub, nib] so far."""
+    Ud, Id = U.double(), I.double()
+    return ((Ud[u].abs() * nz[1][i]).sum(1) + (Id[i].abs() * nz[0][u]).sum(1) + nz[2][u, 0] + nz[3][i, 0]
+            + (NOISE_C0 * NOISE_U) * (Ud[u] * Id[i]).abs().sum(1))
+
+
+def gradient_noise(U, I, u, i, dz, nz=None, dzn=None):
+    """Noise band of the four data gradients.  ``nz``: the parameters' noise bands carried from
+    earlier steps (the terms' partner rows differ by them); ``dzn``: per-pair bound on dz's own
+    deviation (its logits' noise times the loss curvature)."""
+    az = dz.double().abs()
+    cu = torch.bincount(u, minlength=U.shape[0]).double()
+    ci = torch.bincount(i, minlength=I.shape[0]).double()
+    ku = (NOISE_C1 * cu.sqrt() + NOISE_C0) * NOISE_U
+    ki = (NOISE_C1 * ci.sqrt() + NOISE_C0) * NOISE_U
+    aU = torch.zeros(U.shape, dtype=torch.float64).index_add_(0, u, az[:, None] * I.double()[i].abs())
+    aI = torch.zeros(I.shape, dtype=torch.float64).index_add_(0, i, az[:, None] * U.double()[u].abs())
+    aub = torch.zeros(U.shape[0], dtype=torch.float64).index_add_(0, u, az)
+    aib = torch.zeros(I.shape[0], dtype=torch.float64).index_add_(0, i, az)
+    out = [ku[:, None] * aU, ki[:, None] * aI, (ku * aub)[:, None], (ki * aib)[:, None]]
+    if nz is not None:
+        e = dzn.double() if dzn is not None else torch.zeros_like(az)
+        Ud, Id = U.double(), I.double()
+        out[0].index_add_(0, u, az[:, None] * nz[1][i] + e[:, None] * Id[i].abs())
+        out[1].index_add_(0, i, az[:, None] * nz[0][u] + e[:, None] * Ud[u].abs())
+        out[2].index_add_(0, u, e[:, None])
+        out[3].index_add_(0, i, e[:, None])
+    return out
+
+
 # ------------------------------------------------------------------ optimizers
 class Optim:
     """torch.optim single-tensor CPU update (spotlight/optimizers.py:4-22)."""
@@ -127,6 +170,48 @@ class Optim:
         self.eps, self.alpha = eps, alpha
         self.t = 0
         self.state = [(torch.zeros_like(p), torch.zeros_like(p)) for p in params]
+
+    def sensitivity(self, params, grads, dgrads, dstate):
+        """Bound (per element, float64) on how far ANY fp32 implementation's update of this
+        step can land from this one's when its data gradient is off by up to ``dgrads`` (the
+        rounding noise of the gradient sums) and its optimizer state by up to ``dstate``
+        (the [dm, dv] carried from earlier steps, updated in place).  Evaluated at the corners
+        of the box; call before ``step`` (it reads the pre-step state)."""
+        t = self.t + 1
+        out = []
+        for k, (p, g, dg) in enumerate(zip(params, grads, dgrads)):
+            m, v = self.state[k]
+            dm, dv = dstate[k]
+            p, g, dg, m, v = (x.double() for x in (p, g, dg, m, v))
+            if self.wd != 0:
+                g = g + self.wd * p
+            if self.kind == "sgd":
+                out.append(self.lr * dg)
+                continue
+            if self.kind == "adam":
+                b1, b2 = self.b1, self.b2
+                m1 = b1 * m + (1 - b1) * g
+                dm1 = b1 * dm + (1 - b1) * dg
+                bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+
+                def upd(mm, vv):
+                    return (self.lr / bc1) * mm / (vv.clamp(min=0).sqrt() / math.sqrt(bc2) + self.eps)
+            else:
+                b2 = self.alpha
+                m1, dm1 = g, dg
+
+                def upd(mm, vv):
+                    return self.lr * mm / (vv.clamp(min=0).sqrt() + self.eps)
+            v1 = b2 * v + (1 - b2) * g * g
+            dv1 = b2 * dv + (1 - b2) * (2 * g.abs() * dg + dg * dg)
+            base = upd(m1, v1)
+            dev = torch.zeros_like(base)
+            for sm in (-1.0, 1.0):
+                for sv in (-1.0, 1.0):
+                    dev = torch.maximum(dev, (upd(m1 + sm * dm1, v1 + sv * dv1) - base).abs())
+            dstate[k] = (dm1, dv1)
+            out.append(dev)
+        return out
 
     def step(self, params, grads):
         self.t += 1
@@ -162,9 +247,15 @@ class MFOracle:
 
     def __init__(self, U, I, ub, ib, pool_u, pool_i, mt_state, loss="pointwise",
                  optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=5, batch_size=256,
-                 betas=(0.5, 0.999), python_sampler=False):
+                 betas=(0.5, 0.999), python_sampler=False, noise=False):
         assert loss in LOSSES
         self.params = [U, I, ub, ib]
+        # noise=True (run it in float64): per element, a bound on how far an fp32 implementation
+        # summing the same gradient terms in another order can land (self.noise, accumulated over
+        # the steps; see gradient_noise / Optim.sensitivity) -- the band of elementwise_parity
+        self.noise = [torch.zeros_like(p, dtype=torch.float64) for p in self.params] if noise else None
+        self.grads_fn = dense_grads
+        self._dstate = [(torch.zeros_like(p, dtype=torch.float64),) * 2 for p in self.params] if noise else None
         self.loss_kind = loss
         self.n = n_neg
         self.batch_size = batch_size
@@ -202,9 +293,28 @@ class MFOracle:
         dzn = dpn * (1.0 - p_neg) * p_neg
         u = torch.cat([pos_u, nu])
         i = torch.cat([pos_i, ni])
-        grads = dense_grads(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
+        grads = self.grads_fn(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
         if exchange is not None:
             grads = exchange(grads)
+        if self.noise is not None:
+            # dz's deviation: its logits' noise (and, paired, its column's) times |d dz / d z|,
+            # bounded by 2 |dz| + |dL/dp| p (1 - p) / 4 per unit of z
+            zp = pair_noise(U, I, self.noise, pos_u, pos_i)
+            zn = pair_noise(U, I, self.noise, nu, ni)
+            Bp, Bn = len(pos_u), len(nu)
+            if self.loss_kind in ("bpr", "hinge", "adaptive_hinge"):
+                zc = zn.view(self.n, -1)[:, :Bp]
+                zp_eff = zp + (zc.sum(0) if self.loss_kind != "adaptive_hinge" else zn.max())
+                zn_eff = zn.clone()
+                zn_eff.view(self.n, -1)[:, :Bp] += zp
+            else:
+                zp_eff, zn_eff = zp, zn
+            cp = 2 * dzp.double().abs() + dpp.double().abs() * 0.25
+            cn = 2 * dzn.double().abs() + dpn.double().abs() * 0.25
+            dg = gradient_noise(U, I, u, i, torch.cat([dzp, dzn]), self.noise,
+                                torch.cat([cp * zp_eff, cn * zn_eff]))
+            for k, dev in enumerate(self.opt.sensitivity(self.params, grads, dg, self._dstate)):
+                self.noise[k] += dev.reshape(self.noise[k].shape)
         self.opt.step(self.params, grads)
         if return_all:
             return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx,
@@ -347,3 +457,46 @@ def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None):
     er = float((r - r64).norm())
     ok = eg <= band * er + 0.1 * rtol * float(r64.norm())
     return ok, (f"rel-to-fp32 {e32 / max(n32, 1e-30):.2e}; |gpu-fp64| {eg:.3e} vs |fp32-fp64| {er:.3e}")
+
+
+def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, noise=None):
+    """Elementwise companion of tensor_parity (a norm can hide a few bad elements).
+
+    Element e passes if |got - ref32| <= rtol * |ref32| + floor (floor = rtol * 1e-3 *
+    max|ref32|: elements a thousand times below the tensor's largest are held to that
+    absolute level), or, given ``before``, <= rtol * |before| (a step that cancelled the
+    element), or -- an element on which two fp32 restatements of the same step differ
+    (Adam's g / (|g| + eps) of a cancelled gradient sum) -- |got - ref64| <= band *
+    |ref32 - ref64| + rtol / 10 * |ref64| + floor; given ``noise`` (MFOracle(noise=True)'s
+    per-element bound on an fp32 step's rounding noise, accumulated over the steps) instead:
+    |got - ref64| <= rtol * |ref64| + 2 noise + floor.  Returns (ok, stats) with ok = no element
+    failing both, and stats: n, n_out (elements outside rtol of ref32), frac_out, n_fail,
+    max_rel (max |got - ref32| / max |ref32|), max_elem_rel (max |got - ref32| / (|ref32| +
+    floor))."""
+    g = torch.as_tensor(got).double().reshape(-1).cpu()
+    r = torch.as_tensor(ref32).double().reshape(-1)
+    d = (g - r).abs()
+    mx = float(r.abs().max()) if r.numel() else 0.0
+    floor = rtol * 1e-3 * mx
+    in_tol = d <= rtol * r.abs() + floor
+    if before is not None:
+        b = torch.as_tensor(before).double().reshape(-1).cpu()
+        in_tol |= d <= rtol * b.abs()
+    ok_e = in_tol.clone()
+    n_ill = 0
+    if ref64 is not None:
+        r64 = torch.as_tensor(ref64).double().reshape(-1)
+        if noise is not None:
+            # the float64 step's own noise band (MFOracle(noise=True)): an element whose update
+            # any fp32 order of its gradient sum could move by more than rtol is ill-conditioned
+            nz = torch.as_tensor(noise).double().reshape(-1)
+            ok_e |= (g - r64).abs() <= rtol * r64.abs() + 2.0 * nz + floor
+            n_ill = int((nz > rtol * r64.abs() + floor).sum())
+        else:
+            ok_e |= (g - r64).abs() <= band * (r - r64).abs() + 0.1 * rtol * r64.abs() + floor
+    n = int(r.numel())
+    n_out = int((~in_tol).sum())
+    stats = {"n": n, "n_out": n_out, "frac_out": n_out / max(n, 1), "n_fail": int((~ok_e).sum()), "n_ill": n_ill,
+             "max_rel": float(d.max()) / max(mx, 1e-30) if n else 0.0,
+             "max_elem_rel": float((d / (r.abs() + max(floor, 1e-38))).max()) if n else 0.0}
+    return stats["n_fail"] == 0, stats

@@ -15,9 +15,15 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 
 #include "rg_common.h"
 
@@ -41,26 +47,96 @@ struct Comm {
     struct HostCall {
         Comm *c;
         int64_t n;
-    } calls[64];
-    int next_call = 0;
-    int host_error = 0;
+    };
+    std::atomic<int> host_error{0};
+    // RCCL deadline (bounded failure of a multi-process run): a watchdog thread checks the
+    // communicator's asynchronous error and the completion of the last tracked collective; past
+    // the deadline it aborts the communicator (which releases the GPU's waiting kernels) and
+    // exits the process non-zero with a message naming the rank
+    std::thread watchdog;
+    std::atomic<bool> stop{false};
+    std::mutex mu;
+    hipEvent_t ev_track = nullptr;          // recorded after every kTrackEvery-th collective
+    std::chrono::steady_clock::time_point track_t0;
+    bool tracking = false;
+    int64_t ncoll = 0;
+    double timeout_s = 600.0;
 };
+constexpr int kTrackEvery = 16;
 
+// each in-flight host exchange owns its call record (freed by the callback): any number of
+// exchanges may be enqueued before the callbacks drain
 static void host_trampoline(void *p) {
     Comm::HostCall *hc = static_cast<Comm::HostCall *>(p);
     if (hc->c->host_fn(hc->c->host_ctx, hc->c->pinned, hc->n) != 0) hc->c->host_error = 1;
+    delete hc;
+}
+
+static double env_seconds(const char *name, double dflt) {
+    const char *e = getenv(name);
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : dflt;
+}
+
+[[noreturn]] static void comm_die(Comm *c, const std::string &why) {
+    fprintf(stderr, "[librg_hip] rank %d of %d: %s; aborting the RCCL communicator and exiting\n", c->rank, c->world,
+            why.c_str());
+    fflush(stderr);
+    if (c->comm) ncclCommAbort(c->comm);
+    std::_Exit(3);
+}
+
+static void watchdog_loop(Comm *c) {
+    while (!c->stop.load()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(500));
+        if (c->stop.load()) break;
+        ncclResult_t ae = ncclSuccess;
+        if (c->comm && ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+            comm_die(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->tracking) continue;
+        if (hipEventQuery(c->ev_track) == hipSuccess) { c->tracking = false; continue; }
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->track_t0).count();
+        if (waited > c->timeout_s)
+            comm_die(c, "collective #" + std::to_string(c->ncoll) + " not complete after " + std::to_string((int)waited) +
+                            " s (RG_COMM_TIMEOUT_S; a peer rank failed or diverged)");
+    }
+}
+
+// after an RCCL call on `stream`: wait out ncclInProgress (non-blocking communicator) within
+// the deadline, and every kTrackEvery-th collective arm the watchdog on its completion
+static int nccl_after(Comm *c, hipStream_t stream, ncclResult_t r, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        if (ncclCommGetAsyncError(c->comm, &r) != ncclSuccess) break;
+        if (r != ncclInProgress) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+            comm_die(c, std::string(what) + " still in progress after the deadline");
+        std::this_thread::yield();
+    }
+    if (r != ncclSuccess) {
+        set_error(std::string(what) + ": " + ncclGetErrorString(r));
+        return RG_E_LAUNCH;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    if (++c->ncoll % kTrackEvery == 0 && !c->tracking && c->ev_track) {
+        if (hipEventRecord(c->ev_track, stream) == hipSuccess) {
+            c->tracking = true;
+            c->track_t0 = std::chrono::steady_clock::now();
+        }
+    }
+    return RG_OK;
 }
 
 // host-staged all-reduce: D2H -> host callback -> H2D, all on the communicator stream
 static int host_allreduce(Comm *c, float *buf, int64_t n) {
     if (n > c->pinned_floats) return fail_arg("rg_comm (host): buffer larger than the staging area");
     if (c->host_error) return fail_arg("rg_comm (host): an earlier host all-reduce failed");
-    Comm::HostCall *hc = &c->calls[c->next_call];
-    c->next_call = (c->next_call + 1) % 64;
-    hc->c = c;
-    hc->n = n;
+    Comm::HostCall *hc = new (std::nothrow) Comm::HostCall{c, n};
+    if (!hc) return fail_arg("rg_comm (host): out of memory");
     hipError_t e = hipMemcpyAsync(c->pinned, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipLaunchHostFunc(c->stream, host_trampoline, hc);
+    else delete hc;
     if (e == hipSuccess) e = hipMemcpyAsync(buf, c->pinned, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) {
         set_error(std::string("rg_comm (host): ") + hipGetErrorString(e));
@@ -111,9 +187,8 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
     if (e != hipSuccess) return hip_fail("rg_comm_allreduce_begin", e);
     if (c->local) return local_roundtrip(c, c->stream, buf, n);
     if (c->host_fn) return host_allreduce(c, buf, n);
-    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream);
-    if (r != ncclSuccess) return nccl_fail("ncclAllReduce", r);
-    return RG_OK;
+    return nccl_after(c, c->stream, ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream),
+                      "ncclAllReduce");
 }
 
 hipStream_t comm_stream(void *h) { return h ? static_cast<Comm *>(h)->stream : nullptr; }
@@ -127,8 +202,8 @@ int comm_allreduce_on(void *h, hipStream_t stream, float *buf, int64_t n) {
     }
     if (c->local) return local_roundtrip(c, stream, buf, n);
     if (c->world == 1) return RG_OK;       // a one-rank sum is the buffer itself: no RCCL launch
-    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, stream);
-    return r == ncclSuccess ? RG_OK : nccl_fail("ncclAllReduce", r);
+    return nccl_after(c, stream, ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, stream),
+                      "ncclAllReduce");
 }
 
 int comm_end(void *h, hipStream_t stream) {
@@ -145,9 +220,8 @@ int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) 
     if (!c || !buf || chunk < 0) return fail_arg("rg_comm_reduce_scatter_f32: bad argument");
     if (c->local) return local_roundtrip(c, stream, buf + (int64_t)c->rank * chunk, chunk * c->world);
     if (c->host_fn) return fail_arg("rg_comm (host): reduce-scatter not supported (all-reduce only)");
-    const ncclResult_t r = ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
-                                             ncclSum, c->comm, stream);
-    return r == ncclSuccess ? RG_OK : nccl_fail("ncclReduceScatter", r);
+    return nccl_after(c, stream, ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
+                                                   ncclSum, c->comm, stream), "ncclReduceScatter");
 }
 
 int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const int64_t *counts) {
@@ -166,8 +240,8 @@ int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const
         r = ncclAllGather(bufs[k] + (int64_t)c->rank * counts[k], bufs[k], (size_t)counts[k], ncclFloat32, c->comm,
                           stream);
     const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail("ncclAllGather", r);
-    return r2 == ncclSuccess ? RG_OK : nccl_fail("ncclGroupEnd", r2);
+    if (r != ncclSuccess && r != ncclInProgress) return nccl_fail("ncclAllGather", r);
+    return nccl_after(c, stream, r2, "ncclAllGather (group)");
 }
 
 }  // namespace rg
@@ -212,15 +286,38 @@ extern "C" void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, 
         delete c;
         return nullptr;
     }
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, sizeof(uid));
-    const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
-    if (r != ncclSuccess) {
-        rg::nccl_fail("ncclCommInitRank", r);
-        hipStreamDestroy(c->stream);
-        delete c;
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_track, evf);
+    if (e != hipSuccess) {
+        rg::hip_fail("rg_comm_create", e);
+        rg_comm_destroy(c);
         return nullptr;
     }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    // non-blocking initialisation polled against a deadline: a rank that never joins (or a
+    // peer that died) ends the run with a message instead of a hang until the job's time limit
+    c->timeout_s = rg::env_seconds("RG_COMM_TIMEOUT_S", 600.0);
+    const double init_s = rg::env_seconds("RG_COMM_INIT_TIMEOUT_S", 300.0);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c->comm, world, uid, rank, &cfg);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (ncclCommGetAsyncError(c->comm, &r) != ncclSuccess) break;
+        if (r == ncclInProgress &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > init_s)
+            rg::comm_die(c, "ncclCommInitRankConfig not complete after " + std::to_string((int)init_s) +
+                                " s (RG_COMM_INIT_TIMEOUT_S; a rank did not join)");
+    }
+    if (r != ncclSuccess) {
+        rg::nccl_fail("ncclCommInitRankConfig", r);
+        if (c->comm) ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        rg_comm_destroy(c);
+        return nullptr;
+    }
+    c->watchdog = std::thread(rg::watchdog_loop, c);
     return c;
 }
 
@@ -276,7 +373,10 @@ extern "C" void *rg_comm_create_host(int32_t world, int32_t rank, int32_t device
 extern "C" int rg_comm_destroy(void *h) {
     rg::Comm *c = static_cast<rg::Comm *>(h);
     if (!c) return RG_OK;
+    c->stop = true;
+    if (c->watchdog.joinable()) c->watchdog.join();
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ev_track) hipEventDestroy(c->ev_track);
     if (c->scratch) hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm) ncclCommDestroy(c->comm);

@@ -1729,6 +1729,8 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     if (!m || !b || !w || !nw) return fail_arg("rg_ncf_pairs: null argument");
     if (ncf_mlp_len(m->dim) < 0) return fail_arg("rg_ncf_pairs: embedding_dim must be 8, 16, 32 or 64");
     if (b->n_neg < 1 || b->n_neg > RG_MF_MAX_NEG) return fail_arg("rg_ncf_pairs: n_neg out of range");
+    if (b->loss < RG_LOSS_POINTWISE || b->loss > RG_LOSS_ADAPTIVE_HINGE)   // no positives-only NCF step
+        return fail_arg("rg_ncf_pairs: loss must be pointwise, bpr, hinge or adaptive hinge");
     if (!b->pairs || !m->user_w || !m->item_w || !m->mlp) return fail_arg("rg_ncf_pairs: null tables / pairs");
     if (b->n_pos > b->cols) return fail_arg("rg_ncf_pairs: n_pos > cols");
     if (phase != kNcfScores && phase != kNcfLossOnly && (!w->row_count || !w->row_list || !w->hot_grad ||

@@ -146,6 +146,9 @@ class ImplicitFactorizationModel:
                 from .comm import RcclComm
                 comm = RcclComm(dev)
             ncf_dp = dict(rank=self._rank, world_size=self._world, comm=comm)
+        is_mf = hasattr(net, "user_embeddings") and hasattr(net, "item_biases")
+        if self._no_negatives and not is_mf:   # before any engine (and its device state) is built
+            raise NotImplementedError("training without a negative pool is implemented for BilinearNet")
         if hasattr(net, "embedding_user_mlp") and hasattr(net, "affine_output"):   # NeuMF (neuMF.py:7-55)
             self._kind = "ncf"
             self._params = [net.embedding_user_mlp.weight, net.embedding_item_mlp.weight,
@@ -180,8 +183,6 @@ class ImplicitFactorizationModel:
                                     self._pool.item_ids, _mtstate.current(), **common, **dp)
         else:
             raise NotImplementedError("the fused steps train BilinearNet, the NCF MLP and NeuMF representations")
-        if self._no_negatives and self._kind != "mf":
-            raise NotImplementedError("training without a negative pool is implemented for BilinearNet")
         self.configuration = {"num_users": self._num_users, "num_items": self._num_items,
                               "weight_decay": self._l2, "lr": self._learning_rate,
                               "embedding_dim": self._embedding_dim, "batch_size": self._batch_size,

@@ -40,7 +40,7 @@ class NCFEngine:
                  device="cuda", seed=0, mf_user_w=None, mf_item_w=None, rank=0, world_size=1, comm=None):
         _lib.require_gpu()
         self.rank, self.world, self.comm = int(rank), int(world_size), comm
-        if loss not in LOSS_KINDS:
+        if loss not in LOSS_KINDS or loss == "pointwise_pos":   # the NCF kernels have no positives-only loss
             raise ValueError(f"unknown loss {loss!r}")
         if optimizer not in OPT_KINDS:
             raise ValueError(f"unknown optimizer {optimizer!r}")

@@ -78,7 +78,20 @@ __global__ __launch_bounds__(256) void gather(const float *__restrict__ w, const
     if (sub == 0) out[q] = 1.0f / (1.0f + expf(-d));
 }
 
-int main() {
+// touches `lines` random 128-B lines of a large buffer (the pair pass's pool gathers and the
+// rest of a step's traffic that competes with the tables for the Infinity Cache)
+__global__ __launch_bounds__(256) void pollute(const float *__restrict__ buf, long nlines, long lines, unsigned seed,
+                                               float *__restrict__ sink) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= lines) return;
+    unsigned x = (unsigned)t * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    const float v = buf[((long)x % nlines) * 32];
+    if (v == 12345.0f) sink[0] = v;
+}
+
+int main(int argc, char **argv) {
+    const int random_data = argc > 1 ? atoi(argv[1]) : 0;
     const long U = 136677, I = 20108, rows = U + I, npairs = 49152;
     const size_t tb = rows * 64 * 4;
     float *P[2], *m, *v, *B[2], *bm, *bv, *out;
@@ -88,6 +101,20 @@ int main() {
     hipMalloc(&bm, rows * 4); hipMalloc(&bv, rows * 4); hipMalloc(&out, npairs * 4); hipMalloc(&ids, npairs * 8);
     hipMemset(P[0], 0, tb); hipMemset(P[1], 0, tb); hipMemset(m, 0, tb); hipMemset(v, 0, tb);
     hipMemset(B[0], 0, rows * 4); hipMemset(B[1], 0, rows * 4); hipMemset(bm, 0, rows * 4); hipMemset(bv, 0, rows * 4);
+    if (random_data) {     // tables of N(0, 1/64)-like values, m ~ 1e-6, v ~ 1e-12, not zeros
+        std::vector<float> hv(rows * 64);
+        srand(3);
+        for (auto &x : hv) x = ((rand() & 0xffff) - 32768) * (1.0f / 32768 / 64);
+        hipMemcpy(P[0], hv.data(), tb, hipMemcpyHostToDevice);
+        hipMemcpy(P[1], hv.data(), tb, hipMemcpyHostToDevice);
+        for (auto &x : hv) x *= 1e-4f;
+        hipMemcpy(m, hv.data(), tb, hipMemcpyHostToDevice);
+        for (auto &x : hv) x = x * x + 1e-12f;
+        hipMemcpy(v, hv.data(), tb, hipMemcpyHostToDevice);
+    }
+    const long big = 1l << 30;   // 1 GiB pollution buffer (pool + positives + plans + ring are ~0.5 GB)
+    float *junk, *sink;
+    hipMalloc(&junk, big); hipMemset(junk, 0, big); hipMalloc(&sink, 64);
     std::vector<int2> h(npairs);
     srand(7);
     for (long k = 0; k < npairs; ++k) h[k] = make_int2(rand() % (int)U, rand() % (int)I);
@@ -101,16 +128,23 @@ int main() {
         if (st == 1) hipLaunchKernelGGL(stream<1>, dim3(sg), dim3(256), 0, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
         if (st == 2) hipLaunchKernelGGL(stream<2>, dim3(sg), dim3(256), 0, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
     };
+    long pl = 0;                                              // lines polluted per iteration
+    unsigned seed = 1;
+    auto polluter = [&]() {
+        if (pl > 0) hipLaunchKernelGGL(pollute, dim3((unsigned)((pl + 255) / 256)), dim3(256), 0, 0, junk, big / 128, pl,
+                                       seed++, sink);
+    };
     auto timeit = [&](const char *what, int st, int mode) {   // mode 0 stream, 1 gather, 2 both
         const int it = 200;
         for (int k = 0; k < 20; ++k) {
-            if (mode != 1) launch(st, k & 1);
-            if (mode != 0) hipLaunchKernelGGL(gather, dim3(gg), dim3(256), 0, 0, P[(k + 1) & 1], B[(k + 1) & 1], ids, out, npairs, U);
+            if (mode == 0 || mode == 2) launch(st, k & 1);
+            if (mode == 1 || mode == 2) hipLaunchKernelGGL(gather, dim3(gg), dim3(256), 0, 0, P[(k + 1) & 1], B[(k + 1) & 1], ids, out, npairs, U);
         }
         hipEventRecord(e0, 0);
         for (int k = 0; k < it; ++k) {
-            if (mode != 1) launch(st, k & 1);
-            if (mode != 0) hipLaunchKernelGGL(gather, dim3(gg), dim3(256), 0, 0, P[(k + 1) & 1], B[(k + 1) & 1], ids, out, npairs, U);
+            polluter();
+            if (mode == 0 || mode == 2) launch(st, k & 1);
+            if (mode == 1 || mode == 2) hipLaunchKernelGGL(gather, dim3(gg), dim3(256), 0, 0, P[(k + 1) & 1], B[(k + 1) & 1], ids, out, npairs, U);
         }
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);
@@ -121,13 +155,21 @@ int main() {
         if (mode == 0) printf("  %.2f TB/s algorithmic", 6.0 * rows * 65 * 4 / us / 1e6);
         printf("\n");
     };
-    for (int rep = 0; rep < 2; ++rep) {
-        timeit("gather alone", 0, 1);
-        for (int st = 0; st < 3; ++st) {
-            timeit("stream alone", st, 0);
-            timeit("stream -> gather", st, 2);
-        }
+    printf("random_data %d\n", random_data);
+    timeit("gather alone", 0, 1);
+    for (int st = 0; st < 3; st += 2) {
+        timeit("stream alone", st, 0);
+        timeit("stream -> gather", st, 2);
     }
+    for (long mb : {2, 8, 32, 64}) {      // MB of random lines pulled in per iteration
+        pl = mb * (1l << 20) / 128;
+        char what[64];
+        snprintf(what, sizeof what, "pollute %ld MB + stream", mb);
+        timeit(what, 0, 0);
+        snprintf(what, sizeof what, "pollute %ld MB alone", mb);
+        timeit(what, 0, 3);
+    }
+    pl = 0;
     hipError_t err = hipDeviceSynchronize();
     printf("status %s\n", hipGetErrorString(err));
     return err == hipSuccess ? 0 : 1;

@@ -130,3 +130,29 @@ def test_prefetched_negatives_leave_the_trajectory_unchanged():
         np.testing.assert_allclose(out[m][0], out[0][0], rtol=1e-5)
         for a, b in zip(out[0][1], out[m][1]):
             assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-12
+
+
+def test_ncf_rejects_the_positives_only_loss(tmp_path, monkeypatch):
+    """RG_LOSS_POINTWISE_POS (neg_examples=None, implemented for BilinearNet only) is refused by
+    the NCF engine, and the drop-in refuses it before building any engine (round-3 advisor)."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.implicit import ImplicitFactorizationModel
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.spotlight.interactions import Interactions
+    from oracle import rng as orng
+    monkeypatch.chdir(tmp_path)                 # the drop-in writes experiments_results/ under the cwd
+    dev = torch.device("cuda:0")
+    U, I, E = 40, 30, 8
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E), torch.randn(I, E)]
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+        params += [torch.zeros(b_, a_), torch.zeros(b_)]
+    with pytest.raises(ValueError):
+        NCFEngine(params[0], params[1], params[2:], np.zeros(4, np.int64), np.zeros(4, np.int64),
+                  orng.py_seed_state(0), loss="pointwise_pos", n_neg=5, batch_size=16, device=dev)
+    rs = np.random.RandomState(0)
+    train = Interactions(rs.randint(0, U, 200), rs.randint(0, I, 200), num_users=U, num_items=I)
+    net = MLP(layers=[2 * E, E], num_users=U, num_items=I, embedding_dim=E)
+    m = ImplicitFactorizationModel(representation=net, n_iter=1, batch_size=16, use_cuda=True, neg_examples=None)
+    with pytest.raises(NotImplementedError):
+        m.fit(train, train)

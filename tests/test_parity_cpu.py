@@ -1,0 +1,69 @@
+"""oracle.mf.elementwise_parity: the elementwise rule behind the full-size GPU tests."""
+import torch
+
+from oracle import mf as omf
+
+
+def test_elementwise_catches_what_the_norm_hides():
+    torch.manual_seed(0)
+    r32 = torch.randn(1_000_000) / 64
+    r64 = r32.double() + torch.randn(1_000_000).double() * 1e-9
+    got = r32.clone()
+    got[123] *= 1.003                         # one element 0.3 % off: the norm rule still passes
+    ok_n, _ = omf.tensor_parity(got, r32, r64)
+    ok_e, st = omf.elementwise_parity(got, r32, r64)
+    assert ok_n and not ok_e
+    assert st["n_out"] == 1 and st["n_fail"] == 1 and abs(st["frac_out"] - 1e-6) < 1e-12
+
+
+def test_elementwise_band_and_operand_rules():
+    r64 = torch.tensor([1.0, 2.0, 1e-3, 0.0], dtype=torch.float64)
+    r32 = torch.tensor([1.0, 2.0, 1.2e-3, 0.0])          # the fp32 reference itself 20 % off on [2]
+    got = torch.tensor([1.0 + 5e-6, 2.0, 0.85e-3, 1e-12])   # [2]: outside 1e-5 of r32, inside the band
+    ok, st = omf.elementwise_parity(got, r32, r64)
+    assert ok and st["n_out"] == 1 and st["n_fail"] == 0
+    got[2] = 2e-3                                          # 5x the fp32 reference's distance from fp64
+    assert not omf.elementwise_parity(got, r32, r64)[0]
+    before = torch.tensor([1.0, 2.0, 1.0, 0.0])            # a cancelled step: judged on the operand
+    got[2] = 1.2e-3 + 5e-6
+    assert omf.elementwise_parity(got, r32, None, before=before)[0]
+
+
+def test_mf_noise_band_covers_other_fp32_orders():
+    """The float64 oracle's noise band (MFOracle(noise=True)) holds every element of two fp32
+    restatements that sum the gradients in different orders (the reference's index order and
+    the reverse), over three steps with Zipf-hot items overflowing any per-row list: the
+    elementwise rule the full-size GPU tests apply cannot fail an fp32 result for its order."""
+    import numpy as np
+    from oracle import rng as orng
+    torch.manual_seed(0)
+    U, I, d, B, n = 3000, 400, 64, 1024, 5
+    tabs = omf.init_tables(U, I, d)
+    rs = np.random.RandomState(1)
+    pool_u, pool_i = rs.randint(0, U, 20000), rs.randint(0, I, 20000)
+    items = np.minimum((rs.zipf(1.3, 3 * B) - 1), I - 1)
+    users = rs.randint(0, U, 3 * B)
+    for loss in ("bpr", "pointwise"):
+        kw = dict(loss=loss, optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+        st = orng.py_seed_state(0)
+        fp32 = [omf.MFOracle(*[t.clone() for t in tabs], pool_u, pool_i, st.copy(), **kw) for _ in range(4)]
+        r = omf.MFOracle(*[t.clone().double() for t in tabs], pool_u, pool_i, st.copy(), noise=True, **kw)
+        for j, o in enumerate(fp32[1:]):          # the reverse and two random orders of the gradient sums
+            g = torch.Generator().manual_seed(j)
+
+            def perm_grads(U_, I_, ub, ib, u, i, dz, j=j, g=g):
+                pr = torch.arange(len(u) - 1, -1, -1) if j == 0 else torch.randperm(len(u), generator=g)
+                return omf.dense_grads(U_, I_, ub, ib, u[pr], i[pr], dz[pr])
+            o.grads_fn = perm_grads
+        for s in range(3):
+            for o in fp32 + [r]:
+                o.step(users[s * B:(s + 1) * B], items[s * B:(s + 1) * B])
+            for k in range(4):
+                r64, nz = r.params[k].reshape(-1), r.noise[k].reshape(-1)
+                fl = 1e-8 * float(r64.abs().max())
+                for o in fp32:
+                    ok, st_ = omf.elementwise_parity(o.params[k], fp32[0].params[k], r.params[k], noise=r.noise[k])
+                    assert ok, (loss, s, k, st_)
+                    # and with room to spare: the deviation stays a quarter of the band
+                    dev = (o.params[k].double().reshape(-1) - r64).abs()
+                    assert float((dev / (1e-5 * r64.abs() + 2 * nz + fl)).max()) < 0.25, (loss, s, k)
