@@ -123,8 +123,9 @@ int main(int argc, char **argv) {
     const int sg = (int)((rows * 16 + 255) / 256), gg = (int)((npairs * 16 + 255) / 256);
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
+    size_t lds = 0;                                           // dynamic LDS per block (occupancy sweep)
     auto launch = [&](int st, int s) {
-        if (st == 0) hipLaunchKernelGGL(stream<0>, dim3(sg), dim3(256), 0, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
+        if (st == 0) hipLaunchKernelGGL(stream<0>, dim3(sg), dim3(256), lds, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
         if (st == 1) hipLaunchKernelGGL(stream<1>, dim3(sg), dim3(256), 0, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
         if (st == 2) hipLaunchKernelGGL(stream<2>, dim3(sg), dim3(256), 0, 0, P[s], P[1 - s], m, v, B[s], B[1 - s], bm, bv, rows, o);
     };
@@ -161,6 +162,13 @@ int main(int argc, char **argv) {
         timeit("stream alone", st, 0);
         timeit("stream -> gather", st, 2);
     }
+    for (int per_cu : {6, 4, 3, 2}) {      // resident blocks per CU (waves per SIMD) by LDS
+        lds = 160 * 1024 / per_cu - 1024;
+        char what[64];
+        snprintf(what, sizeof what, "stream, %d blocks/CU", per_cu);
+        timeit(what, 0, 0);
+    }
+    lds = 0;
     for (long mb : {2, 8, 32, 64}) {      // MB of random lines pulled in per iteration
         pl = mb * (1l << 20) / 128;
         char what[64];
