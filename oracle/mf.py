@@ -459,7 +459,7 @@ def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None):
     return ok, (f"rel-to-fp32 {e32 / max(n32, 1e-30):.2e}; |gpu-fp64| {eg:.3e} vs |fp32-fp64| {er:.3e}")
 
 
-def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, noise=None):
+def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, noise=None, alt32=None):
     """Elementwise companion of tensor_parity (a norm can hide a few bad elements).
 
     Element e passes if |got - ref32| <= rtol * |ref32| + floor (floor = rtol * 1e-3 *
@@ -467,7 +467,8 @@ def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None,
     absolute level), or, given ``before``, <= rtol * |before| (a step that cancelled the
     element), or -- an element on which two fp32 restatements of the same step differ
     (Adam's g / (|g| + eps) of a cancelled gradient sum) -- |got - ref64| <= band *
-    |ref32 - ref64| + rtol / 10 * |ref64| + floor; given ``noise`` (MFOracle(noise=True)'s
+    |ref32 - ref64| + rtol / 10 * |ref64| + floor (the larger of that distance and
+    ``alt32``'s, a second fp32 restatement summing in another order); given ``noise`` (MFOracle(noise=True)'s
     per-element bound on an fp32 step's rounding noise, accumulated over the steps) instead:
     |got - ref64| <= rtol * |ref64| + 2 noise + floor.  Returns (ok, stats) with ok = no element
     failing both, and stats: n, n_out (elements outside rtol of ref32), frac_out, n_fail,
@@ -493,7 +494,12 @@ def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None,
             ok_e |= (g - r64).abs() <= rtol * r64.abs() + 2.0 * nz + floor
             n_ill = int((nz > rtol * r64.abs() + floor).sum())
         else:
-            ok_e |= (g - r64).abs() <= band * (r - r64).abs() + 0.1 * rtol * r64.abs() + floor
+            # the fp32 restatement's distance from float64 (and a second fp32 order's, ``alt32``)
+            # samples the rounding noise of the element
+            dist = (r - r64).abs()
+            if alt32 is not None:
+                dist = torch.maximum(dist, (torch.as_tensor(alt32).double().reshape(-1) - r64).abs())
+            ok_e |= (g - r64).abs() <= band * dist + 0.1 * rtol * r64.abs() + floor
     n = int(r.numel())
     n_out = int((~in_tol).sum())
     stats = {"n": n, "n_out": n_out, "frac_out": n_out / max(n, 1), "n_fail": int((~ok_e).sum()), "n_ill": n_ill,

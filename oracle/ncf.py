@@ -104,8 +104,13 @@ class NCFOracle:
     """One run_train_iteration (implicit.py:347-364) of the NCF MLP per ``step``."""
 
     def __init__(self, tensors, names, pool_u, pool_i, mt_state, loss="pointwise", lr=1e-2, weight_decay=1e-5,
-                 n_neg=5, batch_size=256, betas=(0.5, 0.999)):
+                 n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None):
         self.P = MLPParams(tensors, names)
+        # order_seed (pointwise, test infrastructure): run the step over the examples in a
+        # seeded permuted order -- the same arithmetic summed in another fp32 order, a second
+        # sample of the rounding noise for tests/parity_report.py's elementwise band
+        assert order_seed is None or loss == "pointwise"
+        self.order = None if order_seed is None else torch.Generator().manual_seed(order_seed)
         self.loss_kind = loss
         self.n, self.batch_size = n_neg, batch_size
         self.opt_lr, self.opt_wd, self.opt_betas = lr, weight_decay, betas
@@ -119,11 +124,19 @@ class NCFOracle:
         t = torch.from_numpy(idx)
         return idx, self.pool_u[t], self.pool_i[t]
 
+    def _permuted(self, u, i, masks):
+        if self.order is None:
+            return u, i, masks
+        pr = torch.randperm(len(u), generator=self.order)
+        return u[pr], i[pr], [m[pr] for m in masks]
+
     def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
         u = torch.as_tensor(pos_u).long()
         i = torch.as_tensor(pos_i).long()
+        u, i, masks_pos = self._permuted(u, i, masks_pos)
         p_pos, c_pos = forward(self.P, u, i, masks_pos)
         idx, nu, ni = self.draw(self.n * self.batch_size)
+        nu, ni, masks_neg = self._permuted(nu, ni, masks_neg)
         p_neg, c_neg = forward(self.P, nu, ni, masks_neg)
         kind = self.loss_kind
         loss, dpp, dpn = omf.loss_and_dp(kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n, self.batch_size)
@@ -215,8 +228,10 @@ class NeuMFOracle(NCFOracle):
     def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
         u = torch.as_tensor(pos_u).long()
         i = torch.as_tensor(pos_i).long()
+        u, i, masks_pos = self._permuted(u, i, masks_pos)
         p_pos, c_pos = neumf_forward(self.P, u, i, masks_pos)
         idx, nu, ni = self.draw(self.n * self.batch_size)
+        nu, ni, masks_neg = self._permuted(nu, ni, masks_neg)
         p_neg, c_neg = neumf_forward(self.P, nu, ni, masks_neg)
         loss, dpp, dpn = omf.loss_and_dp(self.loss_kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n,
                                          self.batch_size)

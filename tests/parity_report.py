@@ -18,9 +18,10 @@ class ParityReport(UserWarning):
     pass
 
 
-def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None):
+def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None, alt32=None):
     ok_n, msg = omf.tensor_parity(got, ref32, ref64, rtol=rtol, band=band, before=before)
-    ok_e, st = omf.elementwise_parity(got, ref32, ref64, rtol=rtol, band=band, before=before, noise=noise)
+    ok_e, st = omf.elementwise_parity(got, ref32, ref64, rtol=rtol, band=band, before=before, noise=noise,
+                                      alt32=alt32)
     line = (f"{tag}: max|d|/max|ref| {st['max_rel']:.2e}, outside 1e-5 {st['n_out']}/{st['n']} "
             f"({st['frac_out']:.2e}), ill-conditioned {st['n_ill']}, failing the fp64 band too {st['n_fail']}")
     warnings.warn(line, ParityReport)

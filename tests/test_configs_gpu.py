@@ -356,6 +356,9 @@ def test_ncf_full_size_steps(ml20m):
                   device=dev, **kw)
     o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
     o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    # a second fp32 restatement summing over the examples in another order: with the first, the
+    # elementwise band's sample of the fp32 rounding noise (tests/parity_report.py)
+    o32b = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=1, **kw)
     widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
     rs = np.random.RandomState(5)
     for s in range(2):
@@ -368,11 +371,12 @@ def test_ncf_full_size_steps(ml20m):
         got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
         l32 = o32.step(pu, pi, mp, mn)
         o64.step(pu, pi, mp, mn)
+        o32b.step(pu, pi, mp, mn)
         torch.cuda.synchronize()
         assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
         assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
-        for nm, p, r32, r64 in zip(names, e.params(), o32.P.t, o64.P.t):
-            ok, msg = parity_report.check(f"C3 ncf step {s} {nm}", p.reshape(r32.shape), r32, r64)
+        for nm, p, r32, r64, rb in zip(names, e.params(), o32.P.t, o64.P.t, o32b.P.t):
+            ok, msg = parity_report.check(f"C3 ncf step {s} {nm}", p.reshape(r32.shape), r32, r64, alt32=rb)
             assert ok, f"step {s} {nm}: {msg}"
 
 
@@ -399,6 +403,8 @@ def test_neumf_full_size_steps(ml20m):
                   device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
     o32 = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
     o64 = oncf.NeuMFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o32b = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=1,
+                            **kw)
     widths = oncf.layer_sizes(E)[1:]
     rs = np.random.RandomState(6)
     for s in range(2):
@@ -412,10 +418,11 @@ def test_neumf_full_size_steps(ml20m):
         got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
         l32 = o32.step(pu, pi, mp, mn)
         o64.step(pu, pi, mp, mn)
+        o32b.step(pu, pi, mp, mn)
         torch.cuda.synchronize()
         assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
         assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
-        for nm, p, r32, r64, b in zip(names, e.params(), o32.P.t, o64.P.t, prev):
+        for nm, p, r32, r64, b, rb in zip(names, e.params(), o32.P.t, o64.P.t, prev, o32b.P.t):
             ok, msg = parity_report.check(f"NeuMF step {s} {nm}", p.reshape(r32.shape), r32, r64,
-                                          before=b.reshape(r32.shape))
+                                          before=b.reshape(r32.shape), alt32=rb)
             assert ok, f"step {s} {nm}: {msg}"

@@ -67,3 +67,38 @@ def test_mf_noise_band_covers_other_fp32_orders():
                     # and with room to spare: the deviation stays a quarter of the band
                     dev = (o.params[k].double().reshape(-1) - r64).abs()
                     assert float((dev / (1e-5 * r64.abs() + 2 * nz + fl)).max()) < 0.25, (loss, s, k)
+
+
+def test_ncf_two_order_band_covers_a_third_order():
+    """NCF / NeuMF (no noise model): the band is the larger distance from float64 of two fp32
+    restatements that sum over the examples in different orders; a third order stays inside it."""
+    import numpy as np
+    from oracle import ncf as oncf
+    from oracle import rng as orng
+    torch.manual_seed(0)
+    U, I, E, B, n = 2000, 300, 16, 512, 5
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E), torch.randn(I, E)]
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+        w = torch.empty(b_, a_)
+        torch.nn.init.xavier_uniform_(w)
+        params += [w, torch.full((b_,), 0.01)]
+    names = [f"p{k}" for k in range(len(params))]
+    rs = np.random.RandomState(0)
+    pool_u, pool_i = rs.randint(0, U, 20000), rs.randint(0, I, 20000)
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    st = orng.py_seed_state(0)
+    a = oncf.NCFOracle([t.clone() for t in params], names, pool_u, pool_i, st.copy(), **kw)
+    b = oncf.NCFOracle([t.clone() for t in params], names, pool_u, pool_i, st.copy(), order_seed=1, **kw)
+    c = oncf.NCFOracle([t.clone() for t in params], names, pool_u, pool_i, st.copy(), order_seed=2, **kw)
+    r = oncf.NCFOracle([t.double() for t in params], names, pool_u, pool_i, st.copy(), **kw)
+    widths = sizes[1:]
+    for s in range(3):
+        pu, pi = rs.randint(0, U, B), np.minimum(rs.zipf(1.3, B) - 1, I - 1)
+        mp = [torch.from_numpy((rs.rand(B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        for o in (a, b, c, r):
+            o.step(pu, pi, mp, mn)
+        for k in range(len(params)):
+            ok, st_ = omf.elementwise_parity(c.P.t[k], a.P.t[k], r.P.t[k], alt32=b.P.t[k])
+            assert ok, (s, k, st_)
