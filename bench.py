@@ -720,10 +720,12 @@ def main():
     # step inputs (ids + plan pointers) built before timing; each call also hands the
     # NEXT step's input to the native stepper, which generates its words ahead
     n_extra = 6          # untimed steps after the timed region (lazy-pass row counts)
-    inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + n_extra + 1)]
+    inputs = [eng.step_input(*batch(s)[:2], gb, batch(s)[2]) for s in range(args.warmup + args.steps + n_extra + 2)]
 
     def step(s, ev=None):
-        return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev)
+        # two steps of lookahead: the pipelined single-GPU step runs step s+1's pair pass and
+        # step s+2's prepare inside step s's launch (rg_mf_stepper_train_ahead)
+        return eng.train_step_in(inputs[s], inputs[s + 1], apply_events=ev, next2=inputs[s + 2])
 
     for s in range(args.warmup):
         step(s)
@@ -755,6 +757,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss_last = float(eng.loss_out[0])
+    if getattr(eng, "pipelined", False) and eng.pipe_error():
+        raise RuntimeError("pipelined MF step: a pair workgroup's bounded wait ran out (results invalid)")
     lazy_rows = None
     if eng.lazy_rows(enable=True) is not None:
         # untimed: user rows the lazy pass processes per step (the counter is contended, so it
@@ -826,6 +830,12 @@ def main():
                 alg = 6 * (I + lazy_rows) * (4 * d + 4)
                 kname = ("rg_mf_apply_lazy (mf_back_kernel<LAZY>: every item row + the user rows with a "
                          "gradient or a next-step mark; deferred cold updates applied on the way)")
+            elif eng.pipelined:
+                # rg_mf_pipe_step: step s's dense pass, step s+1's pair pass (row gathers) and
+                # step s+2's prepare (ids) in one launch
+                alg = user_adam + ids + gather
+                kname = ("rg_mf_pipe_step (mf_pipe_kernel: dense update of step s + pair pass of s+1 + prepare "
+                         "of s+2)")
             else:
                 # rg_mf_apply_prepare: the dense optimizer pass and the next step's prepare
                 # (ids in, prepared pairs out) in one launch

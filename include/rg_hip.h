@@ -311,6 +311,34 @@ int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *tables, rg_mf_wo
                             int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
                             const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mt_gen_t *gen);
 
+/* Pipelined single-GPU step (the stepper's default): ONE launch that runs
+ *   the dense update of step t (tables t -> tables' out set, as rg_mf_apply),
+ *   the pair pass of step t+1 (pair_b / pair_w, prepared with claimed slots; it reads the
+ *     rows this launch writes and waits, in the launch, until every row it reads is written),
+ *   the prepare of step t+2 (optional: next null; claims in next_w->row_count and appends
+ *     every user it claims a first slot of to pipe->hot_out / *pipe->nhot_out).
+ * Replaces run_train_iteration's forward/backward (implicit.py:348-361) of step t+1 and the
+ * optimizer step (implicit.py:363) of step t, overlapped.  pair_w's scratch (lists, overflow
+ * accumulators, partials, planned partials) must not alias w's.  Loss: pointwise, bpr, hinge. */
+typedef struct rg_mf_pipe {
+    const int32_t *hot_users;   /* users step t+1's pair pass reads (rg_mf_prepare_hot of step t+1) */
+    const int32_t *nhot;        /* [1] their number */
+    const int32_t *counts_next; /* step t+1's claim counts (a user with a claim is one of them) */
+    int32_t *gate;              /* [1] 0 on entry (this launch's hot-row counter) */
+    int32_t *gate_next;         /* [1] set to 0 (the next launch's gate) */
+    int32_t *nhot_free;         /* [1] set to 0 (the hot-list length the launch after next appends to) */
+    int32_t *hot_out, *nhot_out;/* step t+2's hot list (next != null); *nhot_out 0 on entry */
+    int32_t *err;               /* [1] set to 1 if a pair workgroup's bounded wait ran out */
+} rg_mf_pipe_t;
+int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
+                    const rg_mf_loss_t *loss, const rg_mf_batch_t *pair_batch, rg_mf_work_t *pair_work,
+                    const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mf_pipe_t *pipe,
+                    const rg_mt_gen_t *gen);
+/* rg_mf_prepare with claimed slots that also lists the users it claims a first slot of
+ * (hot_out, *nhot_out; 0 on entry): the first step of a pipelined sequence. */
+int rg_mf_prepare_hot(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work, int32_t *hot_out,
+                      int32_t *nhot_out);
+
 /* Pull the DATA gradient (no weight decay) of the rows in range into the flat
  * buffer grad_dev = [n*dim row grads | n bias grads | loss], n = row_end - row_begin
  * (the loss slot is written when loss->out is non-null).  Resets the lists like
@@ -550,6 +578,17 @@ int rg_mf_stepper_destroy(void *stepper);
  * events (hipEvent_t) are recorded around rg_mf_apply. */
 int rg_mf_stepper_train(void *stepper, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
                         float *loss_out_dev, void *ev_apply_begin, void *ev_apply_end);
+/* rg_mf_stepper_train with two steps of lookahead: the pipelined single-GPU step
+ * (rg_mf_pipe_step) runs step t's dense update, step t+1's pair pass (`next`) and step t+2's
+ * prepare (`next2`, optional) in one launch; a later call whose input is not the `next` given
+ * here, or any acquire, drops what ran ahead.  Other configurations: rg_mf_stepper_train. */
+int rg_mf_stepper_train_ahead(void *stepper, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
+                              const rg_mf_step_in_t *next2, float *loss_out, void *ev_apply_begin,
+                              void *ev_apply_end);
+/* 1 if the stepper runs the pipelined step (rg_mf_stepper_train_ahead), 0 if not. */
+int rg_mf_stepper_pipelined(void *stepper);
+/* *err_out = 1 if a pipelined launch's pair workgroups ran out of their bounded wait (synchronises). */
+int rg_mf_stepper_pipe_error(void *stepper, int32_t *err_out);
 /* Words + pairs of `cur` for an external consumer on `stream` (validation, split
  * data-parallel steps); *batch_out / *work_out are ready for rg_mf_pairs.
  * Follow the consumer's launch with rg_mf_stepper_release. */

@@ -62,6 +62,12 @@ class MFMark(ctypes.Structure):
                 ("pad_", ctypes.c_int32)]
 
 
+class MFPipe(ctypes.Structure):
+    _fields_ = [("hot_users", ctypes.c_void_p), ("nhot", ctypes.c_void_p), ("counts_next", ctypes.c_void_p),
+                ("gate", ctypes.c_void_p), ("gate_next", ctypes.c_void_p), ("nhot_free", ctypes.c_void_p),
+                ("hot_out", ctypes.c_void_p), ("nhot_out", ctypes.c_void_p), ("err", ctypes.c_void_p)]
+
+
 class MFLoss(ctypes.Structure):
     _fields_ = [("n_partials", ctypes.c_int64), ("inv_a", ctypes.c_double), ("inv_b", ctypes.c_double),
                 ("out", ctypes.c_void_p)]
@@ -266,6 +272,12 @@ SIGNATURES = [
                                                ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64,
                                                ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch),
                                                ctypes.POINTER(MFWork), ctypes.POINTER(MTGen)]),
+    ("rg_mf_prepare_hot", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_pipe_step", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                       ctypes.POINTER(Opt), ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch),
+                                       ctypes.POINTER(MFWork), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                       ctypes.POINTER(MFPipe), ctypes.POINTER(MTGen)]),
     ("rg_mf_step_front", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFBatch),
                                         ctypes.POINTER(MFWork), ctypes.POINTER(MFMark), ctypes.POINTER(Opt),
                                         ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MFBatch),
@@ -322,6 +334,11 @@ SIGNATURES = [
     ("rg_mf_stepper_train", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                            ctypes.POINTER(MFStepIn), ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    ("rg_mf_stepper_train_ahead", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
+                                                 ctypes.POINTER(MFStepIn), ctypes.POINTER(MFStepIn), ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_pipe_error", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_stepper_pipelined", ctypes.c_int, [ctypes.c_void_p]),
     ("rg_mf_stepper_acquire", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                              ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
     ("rg_mf_stepper_release", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -262,6 +262,28 @@ struct RowLayout {
         asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
     }
 
+    // load past the CU's L1 (sc1: served by L2 / memory): reads rows another workgroup of the
+    // same launch wrote with write-through stores (the pipelined MF step's pair pass)
+    __device__ static __forceinline__ void load_sc1(float (&v)[EPL], const float *__restrict__ base,
+                                                    int64_t row, int D, int sub) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0xffffffff,
+                                                                           0x00020000);
+        if constexpr (VEC) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, 16);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+                const int c = sub + LPU * e;
+                v[e] = c < D ? __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((row * D + c) * 4), 0, 16) : 0.0f;
+            }
+        }
+    }
+    __device__ static __forceinline__ float load1_sc1(const float *p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
     __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base,
                                                    int64_t row, int D, int sub) {
         if constexpr (VEC) {

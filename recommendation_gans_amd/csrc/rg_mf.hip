@@ -78,6 +78,9 @@ struct PairsArgs {
     // claimed list slots (rg_mf_work_t claim_num_users): the prepare claims them in row_count and
     // stores them in the ids' bits 27-30; the pair pass reads them instead of claiming
     int32_t claimed;
+    // pipelined step (mf_pipe_kernel): the prepare appends every user it claims a first slot of
+    // (the users this step's pair pass reads) to hot_out, its length in *nhot_out
+    int32_t *hot_out, *nhot_out;
 };
 
 // Prepared ids carry ownership flags in bit 31 when the prepare pass stamped rows:
@@ -151,6 +154,7 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         const bool v = q == 0 ? s < a.n_pos : (a.loss != RG_LOSS_POINTWISE_POS && (s < a.n_pos || !pairwise));
         if (v) {
             const int su = atomicAdd(a.row_count + r.x, 1);
+            if (su == 0 && a.hot_out != nullptr) a.hot_out[atomicAdd(a.nhot_out, 1)] = r.x;
             const bool item_side = !(q == 0 && a.pos_slot != nullptr);
             const int si = item_side ? atomicAdd(a.row_count + a.num_users + r.y, 1) : 0;
             r.x |= (su < kCap ? su : kCap) << kSlotShift;
@@ -207,7 +211,7 @@ constexpr int kLdsFloats = 5 * kPairBlock;   // >= units per block * (dim + 1) f
 // processed in item-sorted order and the positive's item side (t = 1, the Zipf-hot
 // rows) is instead reduced per block in LDS into one partial row per
 // (item, block): plain stores, no atomics, fixed order.
-template <class L, int PHASE, int NMAX>
+template <class L, int PHASE, int NMAX, bool SC1 = false>
 __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk) {
     constexpr int LPU = L::LPU, EPL = L::EPL, NP = NMAX + 1;
     constexpr int UPB = kPairBlock / LPU;                  // units per block
@@ -297,10 +301,17 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         float ur[NP][EPL], ir[NP][EPL], ub[NP], ib[NP];
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-            L::load(ur[q], a.user_w, uid[q], D, sub);
-            L::load(ir[q], a.item_w, iid[q], D, sub);
-            ub[q] = a.user_b[uid[q]];
-            ib[q] = a.item_b[iid[q]];
+            if (SC1) {   // rows written by this launch's hot workgroups (mf_pipe_kernel)
+                L::load_sc1(ur[q], a.user_w, uid[q], D, sub);
+                L::load_sc1(ir[q], a.item_w, iid[q], D, sub);
+                ub[q] = L::load1_sc1(a.user_b + uid[q]);
+                ib[q] = L::load1_sc1(a.item_b + iid[q]);
+            } else {
+                L::load(ur[q], a.user_w, uid[q], D, sub);
+                L::load(ir[q], a.item_w, iid[q], D, sub);
+                ub[q] = a.user_b[uid[q]];
+                ib[q] = a.item_b[iid[q]];
+            }
         }
 #pragma unroll
         for (int e = 0; e < EPL; ++e) upos[e] = ur[0][e];
@@ -422,11 +433,13 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                     float o[EPL];
                     if (t & 1) {
                         const int64_t row = a.num_users + iid[q];
-                        L::load(o, a.user_w, uid[q], D, sub);
+                        if (SC1) L::load_sc1(o, a.user_w, uid[q], D, sub);
+                        else L::load(o, a.user_w, uid[q], D, sub);
                         overflow_add<L>(a.hot_grad, row, D, sub, dz[q], o);
                         if (sub == 0) fix_add(a.hot_bias_grad + row, dz[q]);
                     } else {
-                        L::load(o, a.item_w, iid[q], D, sub);
+                        if (SC1) L::load_sc1(o, a.item_w, iid[q], D, sub);
+                        else L::load(o, a.item_w, iid[q], D, sub);
                         overflow_add<L>(a.hot_grad, uid[q], D, sub, dz[q], o);
                         if (sub == 0) fix_add(a.hot_bias_grad + uid[q], dz[q]);
                     }
@@ -769,6 +782,9 @@ __device__ __forceinline__ void catch_up(const ApplyArgs &a, float2 cl, int wmax
 #ifndef RG_LEAN_PG
 #define RG_LEAN_PG 2
 #endif
+#ifndef RG_DENSE_PIPE_DEFAULT
+#define RG_DENSE_PIPE_DEFAULT 0
+#endif
 // Ascending sort of the 8 list entries held one per lane (lanes sub 0..7 of each LPU-lane row
 // group; sub >= 8 hold +inf keys and sort among themselves): a bitonic network over lane
 // XOR partners, 6 compare-exchange stages of 64-bit keys.  The result (entry e on lane e) is
@@ -791,13 +807,54 @@ __device__ __forceinline__ uint64_t lane_sort8(uint64_t key, int sub) {
 
 // Pull-and-update of unified row r (the single-GPU dense pass, MODE kApplyPull) with a small
 // register footprint: each row's 8 list entries are held one per lane and sorted across the
-// lanes (apply_row holds all 8 in every lane and sorts them in registers: 85 VGPRs, 5 waves per
-// SIMD, against 8 here for the streaming loads).  Same loads in the same round trip (count,
-// list, the item's partial-slot range beside p, m, v), partner rows PG at a time, the same
-// summation order (sorted entries, fma chain; overflowed rows in fixed point; planned
-// partials after), so the result is bit-identical to apply_row.
+// lanes (apply_row holds all 8 in every lane and sorts them in registers).  Split in two so a
+// wave can hold the NEXT row group's loads in flight while it finishes this one
+// (mf_dense_kernel): lean_load issues every load a row needs that does not depend on another
+// load (p, m, v, biases, count, its list entries, the item's partial-slot range); lean_finish
+// pulls the partner rows (and planned partials) those name, updates and stores.  The
+// summation order is apply_row's (sorted entries, fma chain; overflowed rows in fixed point;
+// planned partials after), so the result is bit-identical to it.
 template <class L>
-__device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t r, const int sub) {
+struct LeanRow {
+    float p[L::EPL], m[L::EPL], v[L::EPL];
+    float pb, mb, vb;
+    int c;
+    int2 ent;
+    int s0, s1;
+};
+
+template <class L>
+__device__ __forceinline__ void lean_load(const ApplyArgs &a, const int64_t r, const int sub, const bool valid,
+                                          LeanRow<L> &x) {
+    const int t = r < a.num_users ? 0 : 1;
+    const int64_t lr_ = t ? r - a.num_users : r;
+    const bool adam = a.opt.kind == RG_OPT_ADAM;
+    const bool has_v = a.opt.kind != RG_OPT_SGD;
+    const int D = a.dim;
+    L::zero(x.p); L::zero(x.m); L::zero(x.v);
+    x.pb = x.mb = x.vb = 0.0f;
+    x.c = 0;
+    x.ent = make_int2(0, 0);
+    x.s0 = x.s1 = 0;
+    if (!valid) return;
+    L::load(x.p, a.w_in[t], lr_, D, sub);
+    if (adam) L::load(x.m, a.w_m[t], lr_, D, sub);
+    if (has_v) L::load(x.v, a.w_v[t], lr_, D, sub);
+    if (sub == 0 && a.has_bias) {
+        x.pb = a.b_in[t][lr_];
+        if (adam) x.mb = a.b_m[t][lr_];
+        if (has_v) x.vb = a.b_v[t][lr_];
+    }
+#ifndef RG_X_STREAMONLY   // timing experiments only (wrong results): p, m, v and biases alone
+    x.c = a.row_count[r];
+    if (sub < kCap) x.ent = a.row_list[r * kCap + sub];
+    if (t == 1 && a.item_slot_off != nullptr) { x.s0 = a.item_slot_off[lr_]; x.s1 = a.item_slot_off[lr_ + 1]; }
+#endif
+}
+
+template <class L, bool WT = false>
+__device__ __forceinline__ void lean_finish(const ApplyArgs &a, const int64_t r, const int sub, const bool valid,
+                                            LeanRow<L> &x) {
     constexpr int EPL = L::EPL, LPU = L::LPU, PG = RG_LEAN_PG;
     static_assert(LPU >= kCap, "one list entry per lane");
     const int D = a.dim;
@@ -805,33 +862,15 @@ __device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t
     const int64_t lr_ = t ? r - a.num_users : r;
     const bool adam = a.opt.kind == RG_OPT_ADAM;
     const bool has_v = a.opt.kind != RG_OPT_SGD;
-    float p[EPL], m[EPL], v[EPL], g[EPL];
-    float pb = 0.0f, mb = 0.0f, vb = 0.0f, gb = 0.0f;
-    L::load(p, a.w_in[t], lr_, D, sub);
-    if (adam) L::load(m, a.w_m[t], lr_, D, sub); else L::zero(m);
-    if (has_v) L::load(v, a.w_v[t], lr_, D, sub); else L::zero(v);
-    if (sub == 0 && a.has_bias) {
-        pb = a.b_in[t][lr_];
-        if (adam) mb = a.b_m[t][lr_];
-        if (has_v) vb = a.b_v[t][lr_];
-    }
-#ifdef RG_X_STREAMONLY   // timing experiments only (wrong results): p, m, v and biases alone
-    const int c = 0;
-    const int2 my = make_int2(0, 0);
-    const bool parts = false;
-#else
-    const int c = a.row_count[r];
-    const int2 my = sub < kCap ? a.row_list[r * kCap + sub] : make_int2(0, 0);
-    const bool parts = t == 1 && a.item_slot_off != nullptr;
-#endif
-    int s0 = 0, s1 = 0;
-    if (parts) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
+    const int c = x.c;
+    float g[EPL];
+    float gb = 0.0f;
     L::zero(g);
     const int lane = threadIdx.x & (kWave - 1);
     const int rowbase = lane & ~(LPU - 1);
     if (__any(c > 0)) {
         const int ne = c < kCap ? c : kCap;
-        uint64_t key = ent_key(my, sub < ne);
+        uint64_t key = ent_key(x.ent, sub < ne);
 #if RG_MF_SORTED_PULL
         key = lane_sort8<LPU>(key, sub);
 #endif
@@ -891,17 +930,23 @@ __device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t
             }
             gb = from_fix(gbf);
         }
-        if (sub == 0 && c > 0 && !a.keep_count) a.row_count[r] = 0;
+        if (valid && sub == 0 && c > 0 && !a.keep_count) a.row_count[r] = 0;
     }
-    if (parts) {   // planned positive partials of this item, in slot order
-        for (int sl = s0; sl < s1; sl += PG) {
+    const int s0 = x.s0, s1 = x.s1;
+    if (__any(s1 > s0)) {   // planned positive partials of this item, in slot order
+        for (int sl = s0; __any(sl < s1); sl += PG) {
             float h[PG][EPL];
             float hb[PG];
 #pragma unroll
             for (int u = 0; u < PG; ++u) {
-                const int ss = sl + u < s1 ? sl + u : s0;
-                L::load(h[u], a.part_row, ss, D, sub);
-                hb[u] = a.has_bias ? a.part_bias[ss] : 0.0f;
+                const bool in = sl + u < s1;
+                if (in) {
+                    L::load(h[u], a.part_row, sl + u, D, sub);
+                    hb[u] = a.has_bias ? a.part_bias[sl + u] : 0.0f;
+                } else {
+                    L::zero(h[u]);
+                    hb[u] = 0.0f;
+                }
             }
 #pragma unroll
             for (int u = 0; u < PG; ++u) {
@@ -913,17 +958,37 @@ __device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t
             }
         }
     }
+    if (!valid) return;
 #pragma unroll
-    for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
-    L::store(a.w_out[t], lr_, D, sub, p);
-    if (adam) L::store(a.w_m[t], lr_, D, sub, m);
-    if (has_v) L::store(a.w_v[t], lr_, D, sub, v);
-    if (sub == 0 && a.has_bias) {
-        pb = opt_update(a.opt, pb, gb, mb, vb);
-        a.b_out[t][lr_] = pb;
-        if (adam) a.b_m[t][lr_] = mb;
-        if (has_v) a.b_v[t][lr_] = vb;
+    for (int q = 0; q < EPL; ++q) x.p[q] = opt_update(a.opt, x.p[q], g[q], x.m[q], x.v[q]);
+    if (WT) {   // write-through: another workgroup of the launch reads the row (mf_pipe_kernel)
+        L::store_wt(a.w_out[t], lr_, D, sub, x.p);
+        if (adam) L::store_wt(a.w_m[t], lr_, D, sub, x.m);
+        if (has_v) L::store_wt(a.w_v[t], lr_, D, sub, x.v);
+    } else {
+        L::store(a.w_out[t], lr_, D, sub, x.p);
+        if (adam) L::store(a.w_m[t], lr_, D, sub, x.m);
+        if (has_v) L::store(a.w_v[t], lr_, D, sub, x.v);
     }
+    if (sub == 0 && a.has_bias) {
+        x.pb = opt_update(a.opt, x.pb, gb, x.mb, x.vb);
+        if (WT) {
+            L::store1_wt(a.b_out[t] + lr_, x.pb);
+            if (adam) L::store1_wt(a.b_m[t] + lr_, x.mb);
+            if (has_v) L::store1_wt(a.b_v[t] + lr_, x.vb);
+        } else {
+            a.b_out[t][lr_] = x.pb;
+            if (adam) a.b_m[t][lr_] = x.mb;
+            if (has_v) a.b_v[t][lr_] = x.vb;
+        }
+    }
+}
+
+template <class L>
+__device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t r, const int sub) {
+    LeanRow<L> x;
+    lean_load<L>(a, r, sub, true, x);
+    lean_finish<L>(a, r, sub, true, x);
 }
 
 template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false>
@@ -1419,6 +1484,190 @@ __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs 
     apply_row<L, kApplyPull, NT, false, SPEC>(a, r, sub);
 }
 
+// The single-GPU dense pass as a software pipeline (the default split step): a grid of a few
+// workgroups per CU whose waves each walk a contiguous chunk of row groups (UPW rows per group),
+// the NEXT group's independent loads (p, m, v, biases, count, list entries, slot range) issued
+// before this group's dependent ones (partner rows, planned partials).  One memory round trip
+// per group instead of two: in mf_back_kernel a touched row's wave waited for its list, then for
+// its partner rows, with nothing else in flight (rows with a contribution are ~40 % of all,
+// ~87 % of the 4-row groups).  Grid as mf_back_kernel's: [MT walk] [next prepare] [pad] [dense].
+template <class L>
+__global__ __launch_bounds__(kBlock) void mf_dense_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
+                                                          int64_t dense_blocks, MtGenArgs gen, BackGrid bg) {
+    const int64_t B = blockIdx.x;
+    int64_t blk = B;
+    if (gen.nwords > 0) {
+        if (B == 0) {
+            __shared__ uint32_t X[kRing + 2];
+            mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
+            return;
+        }
+        --blk;
+    }
+    if (blk < bg.prep_blocks) {
+        prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+        return;
+    }
+    if (B < bg.apply_start) return;                         // alignment padding
+    blk = B - bg.apply_start;
+    if (blk >= dense_blocks) return;
+    constexpr int LPU = L::LPU, UPW = L::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t rb = a.row_begin, re = a.row_end, nr = re - rb;
+    if (a.loss_out != nullptr && blk == 0 && threadIdx.x < kWave) {
+        const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);
+        if (lane == 0) *a.loss_out = lv;
+    }
+    const int64_t ia0 = rb > a.num_users ? rb : a.num_users;      // item rows first, as mf_apply_kernel
+    const int64_t ni = re > ia0 ? re - ia0 : 0;
+    // this wave's row groups [g0, g1): contiguous, so a wave's stores fill whole lines
+    const int64_t waves = dense_blocks * (kBlock / kWave);
+    const int64_t wave = (blk * kBlock + threadIdx.x) >> 6;
+    const int64_t groups = (nr + UPW - 1) / UPW;
+    const int64_t per = (groups + waves - 1) / waves;
+    const int64_t g0 = wave * per, g1 = g0 + per < groups ? g0 + per : groups;
+    if (g0 >= g1) return;                                   // wave-uniform
+    auto row_of = [&](int64_t g, bool &valid) {
+        const int64_t k = g * UPW + lane / LPU;
+        valid = k < nr;
+        const int64_t kk = valid ? k : 0;
+        return kk < ni ? ia0 + kk : rb + (kk - ni);
+    };
+    LeanRow<L> cur, nxt;
+    bool vc, vn;
+    int64_t rc = row_of(g0, vc), rn = 0;
+    lean_load<L>(a, rc, sub, vc, cur);
+    for (int64_t g = g0; g < g1; ++g) {
+        const bool more = g + 1 < g1;                       // wave-uniform
+        if (more) {
+            rn = row_of(g + 1, vn);
+            lean_load<L>(a, rn, sub, vn, nxt);
+        }
+        lean_finish<L>(a, rc, sub, vc, cur);
+        if (!more) break;
+        cur = nxt;
+        rc = rn;
+        vc = vn;
+    }
+}
+
+// ---------------------------------------------------------------------------- pipelined step
+// One launch per training step t that also runs the pair pass of step t + 1 and the prepare of
+// step t + 2 (rg_mf_pipe_step, the stepper's default single-GPU step):
+//
+//   [prepare t+2]  the next-but-one step's draws -> pool pairs, list-slot claims, and the list
+//                  of users it claims a first slot of (the users pair pass t+2 will read)
+//   [hot items]    the dense update of every item row              } the rows pair pass t+1
+//   [hot users]    the dense update of the users of step t+1's list } reads; write-through
+//                  stores, then each workgroup adds 1 to the gate
+//   [cold users 1] the dense update of the other users
+//   [pair t+1]     waits until the gate counts every hot workgroup, then runs step t+1's pair
+//                  pass on the updated rows (loads past L1) beside the cold stream
+//   [cold users 2]
+//
+// The latency-bound pair pass (~11 us on its own) thus overlaps the HBM-bound update of the rows
+// it does not read.  Deadlock-free by construction: only pair workgroups wait, on workgroups that
+// never wait, and they are too few (cols / units-per-workgroup) to hold every slot of the chip.
+// Results are bit-identical to the split step (same per-row and per-column arithmetic).
+struct PipeArgs {
+    const int32_t *hot_users, *nhot;   // step t+1's hot user list
+    const int32_t *counts_next;        // step t+1's claims (a user with one is hot)
+    int32_t *gate, *gate_next, *nhot_free, *err;
+    int64_t prep_blocks, item_blocks, huser_blocks, cold1_blocks, pair_blocks, cold2_blocks;
+    int64_t users_begin;               // unified row of user 0 in the dense rows (0)
+    uint32_t spin_limit;
+};
+
+template <class L>
+__device__ __forceinline__ void pipe_rows(const ApplyArgs &a, const int64_t r, const bool valid, const int sub) {
+    LeanRow<L> x;
+    lean_load<L>(a, r, sub, valid, x);
+    lean_finish<L, true>(a, r, sub, valid, x);
+}
+
+template <class L, int NMAX>
+__global__ __launch_bounds__(kBlock) void mf_pipe_kernel(ApplyArgs a, PairsArgs pa, PairsArgs prep, int2 *prep_out,
+                                                         PipeArgs pp, MtGenArgs gen) {
+    static_assert(kPairBlock == kBlock, "the pair workgroups share the launch's block size");
+    constexpr int LPU = L::LPU, UPW = L::UPW;
+    int64_t blk = blockIdx.x;
+    if (gen.nwords > 0) {
+        if (blk == 0) {
+            __shared__ uint32_t X[kRing + 2];
+            mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
+            return;
+        }
+        --blk;
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t rows_per_block = (kBlock / kWave) * UPW;
+    const int64_t U = a.num_users;
+    if (blk < pp.prep_blocks) {                              // prepare of step t + 2
+        if (blk == 0 && threadIdx.x == 0) {                  // counters of later launches
+            *pp.gate_next = 0;
+            *pp.nhot_free = 0;
+        }
+        if (blk == 0 && a.loss_out != nullptr && threadIdx.x >= kWave && threadIdx.x < 2 * kWave) {
+            const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);   // step t's loss
+            if (lane == 0) *a.loss_out = lv;
+        }
+        prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+        return;
+    }
+    blk -= pp.prep_blocks;
+    const int64_t in_block = (threadIdx.x >> 6) * UPW + lane / LPU;   // row slot of this lane group
+    const bool hot = blk < pp.item_blocks + pp.huser_blocks;
+    int64_t row = 0;
+    bool valid = false;
+    if (hot) {                                               // the rows pair pass t + 1 reads
+        if (blk < pp.item_blocks) {
+            const int64_t k = blk * rows_per_block + in_block;
+            valid = k < a.num_items;
+            row = U + (valid ? k : 0);
+        } else {
+            const int64_t k = (blk - pp.item_blocks) * rows_per_block + in_block;
+            valid = k < *pp.nhot;
+            row = valid ? (int64_t)pp.hot_users[k] : 0;
+        }
+    } else {
+        blk -= pp.item_blocks + pp.huser_blocks;
+        int64_t cold;
+        if (blk < pp.cold1_blocks) {
+            cold = blk;
+        } else if (blk < pp.cold1_blocks + pp.pair_blocks) {     // pair pass of step t + 1
+        const int64_t pb = blk - pp.cold1_blocks;
+        if (threadIdx.x == 0) {
+            const int target = (int)(pp.item_blocks + pp.huser_blocks);
+            uint32_t spins = 0;
+            while (__hip_atomic_load(pp.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(8);
+                if (++spins > pp.spin_limit) {               // bounded: flag and go on (wrong results)
+                    atomicOr(pp.err, 1);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        pairs_body<L, kFused, NMAX, true>(pa, pb);
+        return;
+        } else {
+            cold = blk - pp.pair_blocks;
+        }
+        // cold users: chunk `cold` of the user rows, minus the hot ones
+        const int64_t u = cold * rows_per_block + in_block;
+        valid = u < U && pp.counts_next[u] <= 0;
+        row = valid ? u : 0;
+    }
+    if (__any(valid)) pipe_rows<L>(a, row, valid, sub);
+    if (hot) {   // publish: every wave's write-through stores done, then one add for the workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(pp.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---------------------------------------------------------------------------- overlapped step
 // One training step as two launches instead of prepare / pairs / apply:
 //
@@ -1818,6 +2067,20 @@ extern "C" int rg_mf_prepare(void *stream, const rg_mf_batch_t *b, const rg_mf_w
     return rg_mf_prepare_marked(stream, b, w, nullptr);
 }
 
+extern "C" int rg_mf_prepare_hot(void *stream, const rg_mf_batch_t *b, const rg_mf_work_t *w, int32_t *hot_out,
+                                 int32_t *nhot_out) {
+    PairsArgs a;
+    int rc = prepare_args(b, w, nullptr, a);
+    if (rc) return rc;
+    if (!a.claimed || !hot_out || !nhot_out) return fail_arg("rg_mf_prepare_hot: needs claimed slots and a hot list");
+    a.hot_out = hot_out;
+    a.nhot_out = nhot_out;
+    const int64_t total = prepare_threads(b->cols, b->n_neg);
+    hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream, a,
+                       reinterpret_cast<int2 *>(b->pairs), 0);
+    return check_launch("rg_mf_prepare_hot");
+}
+
 static int apply_args(const rg_mf_tables_t *t, const rg_mf_work_t *w, const float *grad_in, float *grad_out,
                       const rg_opt_t *opt, int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
                       float *dense_loss_out, int mode, ApplyArgs &a) {
@@ -1976,6 +2239,27 @@ struct BackLaunchF {
             else
                 hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         };
+        static const int dense_v2 = [] { const char *e = getenv("RG_DENSE_PIPE"); return e ? atoi(e) : RG_DENSE_PIPE_DEFAULT; }();
+        if constexpr (L::LPU >= kCap) {
+            if (!own && !lazy && dense_v2 && a->contrib == nullptr) {
+                // a few workgroups per CU, each wave walking a chunk of row groups (mf_dense_kernel)
+                static const int per_cu = [] { const char *e = getenv("RG_DENSE_PER_CU"); return e ? atoi(e) : 4; }();
+                int64_t db = (int64_t)num_cus() * per_cu;
+                const int64_t groups = (rows + L::UPW - 1) / L::UPW;
+                const int64_t need = (groups + kBlock / kWave - 1) / (kBlock / kWave);
+                if (db > need) db = need;
+                if (db < 1) db = 1;
+                BackGrid dg{prep_blocks, 0, 0, 1, 0};
+                dg.apply_start = (head + 7) / 8 * 8;
+                const dim3 dgrid((unsigned)(dg.apply_start + db));
+                if (e0 || e1)
+                    hipExtLaunchKernelGGL(mf_dense_kernel<L>, dgrid, dim3(kBlock), 0, s, e0, e1, 0, *a, *prep, prep_out, db,
+                                          gen, dg);
+                else
+                    hipLaunchKernelGGL(mf_dense_kernel<L>, dgrid, dim3(kBlock), 0, s, *a, *prep, prep_out, db, gen, dg);
+                return check_launch("rg_mf_apply_prepare");
+            }
+        }
         if (own) go(mf_back_kernel<L, 0, true, true>);
         else if (lazy && lazy_spec) go(mf_back_kernel<L, 0, true, false, true, true>);
         else if (lazy) go(mf_back_kernel<L, 0, true, false, true>);
@@ -1989,6 +2273,105 @@ struct BackLaunchF {
     }
 };
 }  // namespace
+
+namespace {
+struct PipeLaunchF {
+    ApplyArgs *a;
+    PairsArgs *pa, *prep;
+    int2 *prep_out;
+    PipeArgs pp;
+    MtGenArgs gen;
+    int64_t pair_cols, pair_users;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        if constexpr (L::LPU < kCap) {
+            return fail_arg("rg_mf_pipe_step: dim must be a multiple of 4 and >= 32");
+        } else {
+            const int64_t rpb = (kBlock / kWave) * L::UPW;
+            pp.item_blocks = (a->num_items + rpb - 1) / rpb;
+            const int64_t hu = pair_users < a->num_users ? pair_users : a->num_users;
+            pp.huser_blocks = (hu + rpb - 1) / rpb;
+            const int64_t cold = (a->num_users + rpb - 1) / rpb;
+            // cold rows ahead of the pair workgroups: about one chip's worth, so the hot rows are
+            // mostly done when the pair workgroups start waiting
+            static const int64_t c1 = [] { const char *e = getenv("RG_PIPE_COLD1"); return e ? atoll(e) : 2048LL; }();
+            pp.cold1_blocks = cold < c1 ? cold : c1;
+            pp.cold2_blocks = cold - pp.cold1_blocks;
+            pp.pair_blocks = pairs_blocks<L>(pair_cols);
+            const int64_t total = (gen.nwords > 0 ? 1 : 0) + pp.prep_blocks + pp.item_blocks + pp.huser_blocks +
+                                  pp.cold1_blocks + pp.pair_blocks + pp.cold2_blocks;
+            LaunchEvents &le = launch_events();
+            const hipEvent_t e0 = le.start, e1 = le.stop;
+            le = LaunchEvents{};
+            auto go = [&](auto kernel) {
+                if (e0 || e1)
+                    hipExtLaunchKernelGGL(kernel, dim3((unsigned)total), dim3(kBlock), 0, s, e0, e1, 0, *a, *pa, *prep,
+                                          prep_out, pp, gen);
+                else
+                    hipLaunchKernelGGL(kernel, dim3((unsigned)total), dim3(kBlock), 0, s, *a, *pa, *prep, prep_out, pp,
+                                       gen);
+            };
+            if (pa->n_neg <= 5) go(mf_pipe_kernel<L, 5>);
+            else go(mf_pipe_kernel<L, kNMax>);
+            return check_launch("rg_mf_pipe_step");
+        }
+    }
+};
+}  // namespace
+
+extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                               const rg_mf_loss_t *loss, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w,
+                               const rg_mf_batch_t *next, const rg_mf_work_t *next_w, const rg_mf_pipe_t *pipe,
+                               const rg_mt_gen_t *gen) {
+    if (kPairBlock != kBlock) return fail_arg("rg_mf_pipe_step: built with a pair-pass workgroup != 256 threads");
+    if (!pipe || !pipe->hot_users || !pipe->nhot || !pipe->counts_next || !pipe->gate || !pipe->gate_next ||
+        !pipe->nhot_free || !pipe->err)
+        return fail_arg("rg_mf_pipe_step: incomplete rg_mf_pipe_t");
+    if (!pair_b || !pair_w) return fail_arg("rg_mf_pipe_step: null pair batch / work");
+    if (pair_b->loss != RG_LOSS_POINTWISE && pair_b->loss != RG_LOSS_BPR && pair_b->loss != RG_LOSS_HINGE)
+        return fail_arg("rg_mf_pipe_step: pointwise, bpr or hinge only (the adaptive hinge needs the max first)");
+    if (pair_w->claim_num_users <= 0) return fail_arg("rg_mf_pipe_step: the paired step must carry claimed slots");
+    if (pair_w->row_list == w->row_list || pair_w->hot_grad == w->hot_grad || pair_w->loss_partials == w->loss_partials ||
+        (w->part_row && pair_w->part_row == w->part_row))
+        return fail_arg("rg_mf_pipe_step: the paired step's scratch must not alias this step's");
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, 0, -1, loss, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    // the pair pass reads the tables this launch writes
+    rg_mf_tables_t pt = *t;
+    pt.user_w = t->user_w_out; pt.item_w = t->item_w_out; pt.user_b = t->user_b_out; pt.item_b = t->item_b_out;
+    PairsArgs pa;
+    if ((rc = pairs_args(&pt, pair_b, pair_w, 1, pa))) return rc;
+    PairsArgs prep{};
+    int2 *prep_out = nullptr;
+    PipeArgs pp{};
+    if (next) {
+        if ((rc = prepare_args(next, next_w, nullptr, prep))) return rc;
+        if (!prep.claimed || !pipe->hot_out || !pipe->nhot_out)
+            return fail_arg("rg_mf_pipe_step: the prepared step needs claimed slots and a hot list");
+        if (next->pairs == pair_b->pairs) return fail_arg("rg_mf_pipe_step: prepared pairs alias the paired step's");
+        prep.hot_out = pipe->hot_out;
+        prep.nhot_out = pipe->nhot_out;
+        prep_out = reinterpret_cast<int2 *>(next->pairs);
+        pp.prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
+    } else {
+        pp.prep_blocks = 1;   // block 0 still resets the counters and finalizes the loss
+        prep.cols = 0;
+    }
+    MtGenArgs g{};
+    if (gen && gen->nwords > 0) {
+        if (!gen->state || !gen->out) return fail_arg("rg_mf_pipe_step: null MT state / output");
+        g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
+    }
+    pp.hot_users = pipe->hot_users; pp.nhot = pipe->nhot; pp.counts_next = pipe->counts_next;
+    pp.gate = pipe->gate; pp.gate_next = pipe->gate_next; pp.nhot_free = pipe->nhot_free; pp.err = pipe->err;
+    static const uint32_t spin = [] { const char *e = getenv("RG_PIPE_SPIN"); return e ? (uint32_t)atoll(e) : 4000000u; }();
+    pp.spin_limit = spin;
+    PipeLaunchF f{&a, &pa, &prep, prep_out, pp, g, pair_b->cols, (int64_t)(1 + pair_b->n_neg) * pair_b->cols,
+                  (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
+}
 
 extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
                                    int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,

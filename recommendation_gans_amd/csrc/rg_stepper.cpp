@@ -41,6 +41,7 @@
 // overlapped step and (jump path) the jump tables.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -48,6 +49,10 @@
 
 #include "rg_common.h"
 #include "rg_owner.h"
+
+#ifndef RG_PIPE_DEFAULT
+#define RG_PIPE_DEFAULT 0
+#endif
 
 namespace {
 
@@ -126,6 +131,26 @@ struct Stepper {
     bool count_dirty[2] = {false, false};  // counts[b] hold claims no dense pass consumed yet
     bool prep_claimed = false;             // the prepared pairs carry claimed slots
     bool prep_in_pairs = false;            // split step: the next prepare rides in the pair pass
+    // pipelined step (rg_mf_pipe_step; single rank, claimed slots, pointwise / bpr / hinge):
+    // launch t updates step t's rows, runs step t+1's pair pass and step t+2's prepare.  A unit's
+    // scratch by its parity -- claims in pcounts[u % 3], lists / overflow accumulators / partials
+    // / planned partials in set u % 2 ([0] the caller's cfg.work, [1] owned here) -- and the
+    // users its pair pass reads in hot[u % 3] (length pint[u % 3]).
+    bool pipe = false;
+    int32_t *pcounts[3] = {nullptr, nullptr, nullptr};
+    int32_t *p_counts2 = nullptr;          // owned: pcounts[2]
+    bool pdirty[3] = {false, false, false};   // pcounts[k] hold claims no dense pass consumed
+    int32_t *p_list1 = nullptr;
+    int64_t *p_hg1 = nullptr, *p_hbg1 = nullptr;
+    float *p_part1 = nullptr, *p_prow1 = nullptr, *p_pbias1 = nullptr;
+    int32_t *hot[3] = {nullptr, nullptr, nullptr};
+    int32_t *pint = nullptr;               // [0..3) hot-list lengths, [3..5) gates, [5] error flag
+    bool pair_dirty[2] = {false, false};   // overflow accumulators of set k hold a pair pass's adds
+    int64_t paired = -1;                   // unit whose pair pass has run (its lists ready)
+    rg_mf_step_in_t paired_in{};
+    int64_t hot_prepped = -1;              // unit prepared with claims and a hot list, pair pending
+    rg_mf_step_in_t hot_in{};
+    int64_t last_pipe = -1;                // unit of the last pipelined launch (its counter resets)
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -382,9 +407,13 @@ int release(Stepper &st, hipStream_t stream) {
 int lazy_flush(Stepper &st, hipStream_t s);
 
 // words + pairs of unit `taken` for `in`, visible to `stream` (split-step consumers)
+int pipe_abandon(Stepper &st, hipStream_t s);
+
 int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t *unit_out) {
     const int64_t unit = st.taken;
-    int rc = lazy_flush(st, stream);      // external consumers read every row
+    int rc = pipe_abandon(st, stream);    // a pipelined unit ahead is this consumer's now
+    if (rc) return rc;
+    rc = lazy_flush(st, stream);          // external consumers read every row
     if (rc) return rc;
     rc = keep_ahead(st, unit);
     if (rc) return rc;
@@ -583,6 +612,177 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         st.prep_serial = 0;
         st.prep_claimed = st.claim;
     }
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
+// ---------------------------------------------------------------- pipelined step
+rg_mf_work_t pipe_work(const Stepper &st, const rg_mf_step_in_t &in, int64_t unit) {
+    rg_mf_work_t w = work_for(st, in);
+    w.row_count = st.pcounts[unit % 3];
+    w.claim_num_users = st.cfg.tables[0].num_users;
+    if (unit % 2) {
+        w.row_list = st.p_list1;
+        w.hot_grad = st.p_hg1;
+        w.hot_bias_grad = st.p_hbg1;
+        w.loss_partials = st.p_part1;
+        w.part_row = st.p_prow1;
+        w.part_bias = st.p_pbias1;
+    }
+    return w;
+}
+
+int pipe_memset(void *p, size_t bytes, hipStream_t s, const char *what) {
+    hipError_t e = hipMemsetAsync(p, 0, bytes, s);
+    return e == hipSuccess ? RG_OK : hip_fail(what, e);
+}
+
+int pipe_clean_counts(Stepper &st, hipStream_t s, int k) {
+    if (!st.pdirty[k]) return RG_OK;
+    const rg_mf_tables_t &t = st.cfg.tables[0];
+    int rc = pipe_memset(st.pcounts[k], (size_t)(t.num_users + t.num_items) * sizeof(int32_t), s,
+                         "stepper: reset claims");
+    if (rc == RG_OK) st.pdirty[k] = false;
+    return rc;
+}
+
+// the overflow accumulators of set k after a pair pass whose dense pass never ran
+int pipe_clean_accum(Stepper &st, hipStream_t s, int k) {
+    if (!st.pair_dirty[k]) return RG_OK;
+    const rg_mf_tables_t &t = st.cfg.tables[0];
+    const int64_t rows = t.num_users + t.num_items;
+    int64_t *hg = k ? st.p_hg1 : reinterpret_cast<int64_t *>(st.cfg.work.hot_grad);
+    int64_t *hb = k ? st.p_hbg1 : reinterpret_cast<int64_t *>(st.cfg.work.hot_bias_grad);
+    int rc = pipe_memset(hg, (size_t)rows * t.dim * sizeof(int64_t), s, "stepper: reset overflow");
+    if (rc == RG_OK) rc = pipe_memset(hb, (size_t)rows * sizeof(int64_t), s, "stepper: reset overflow");
+    if (rc == RG_OK) st.pair_dirty[k] = false;
+    return rc;
+}
+
+// drop every pipelined unit not trained yet (a pair pass and / or a prepare ahead): their
+// claims and overflow adds are cleared; their words stay (input independent)
+int pipe_abandon(Stepper &st, hipStream_t s) {
+    if (!st.pipe) return RG_OK;
+    int rc = RG_OK;
+    for (int k = 0; k < 3 && rc == RG_OK; ++k) rc = pipe_clean_counts(st, s, k);
+    for (int k = 0; k < 2 && rc == RG_OK; ++k) rc = pipe_clean_accum(st, s, k);
+    st.paired = -1;
+    st.hot_prepped = -1;
+    st.last_pipe = -1;
+    st.prepared = false;
+    st.count_dirty[0] = st.count_dirty[1] = false;
+    return rc;
+}
+
+// Pipelined step of unit t = taken (see rg_mf_pipe_step).  Cold start (no pair pass of t
+// pending): prepare t (claims), pair pass t, prepare t+1 with its hot list, each its own launch;
+// then, while `next` is known, one launch per step.  Without `next` the step is the plain dense
+// pass and the pipeline drains.
+int train_pipe(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+               const rg_mf_step_in_t *next2, float *loss_out, void *ev0, void *ev1) {
+    const int64_t unit = st.taken;
+    int rc = generate_upto(st, unit + (next2 ? 2 : next ? 1 : 0), 0);
+    if (rc) return rc;
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    const rg_mf_tables_t &t0 = st.cfg.tables[0];
+    rg_mf_work_t w = pipe_work(st, cur, unit);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if (!(st.paired == unit && same_input(st.paired_in, cur))) {
+        // cold start: whatever ran ahead belongs to another input
+        if ((rc = pipe_abandon(st, s))) return rc;
+        if ((rc = wait_side(st, s, (int)(unit % 2))) || (rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+        st.pdirty[unit % 3] = true;
+        if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) return rc;
+        st.pair_dirty[unit % 2] = true;
+        st.paired = unit;
+        st.paired_in = cur;
+    }
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+    if (!next) {                       // the last step of a sequence: dense pass only
+        if ((rc = release(st, s))) return rc;
+        rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};
+        rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, t0.num_users + t0.num_items, &l, nullptr, nullptr, nullptr);
+        rg::launch_events() = rg::LaunchEvents{};
+        if (rc) return rc;
+        st.pdirty[unit % 3] = false;
+        st.pair_dirty[unit % 2] = false;
+        st.paired = -1;
+        st.last_pipe = -1;
+        st.set = 1 - st.set;
+        return RG_OK;
+    }
+    // step t+1: prepared with claims and its hot list (done by the previous launch, or now)
+    const int64_t u1 = unit + 1, u2 = unit + 2;
+    rg_mf_work_t w1 = pipe_work(st, *next, u1);
+    const rg_mf_batch_t b1 = make_batch(st, *next, u1);
+    int32_t *nhot = st.pint, *gate = st.pint + 3, *err = st.pint + 5;
+    if (!(st.hot_prepped == u1 && same_input(st.hot_in, *next))) {
+        if ((rc = pipe_clean_counts(st, s, (int)(u1 % 3)))) return rc;
+        if ((rc = pipe_clean_accum(st, s, (int)(u1 % 2)))) return rc;
+        if ((rc = wait_side(st, s, (int)(u1 % 2))) || (rc = wait_words(st, s, u1))) return rc;
+        if ((rc = pipe_memset(nhot + u1 % 3, sizeof(int32_t), s, "stepper: hot list"))) return rc;
+        if ((rc = rg_mf_prepare_hot(s, &b1, &w1, st.hot[u1 % 3], nhot + u1 % 3))) return rc;
+        st.pdirty[u1 % 3] = true;
+        st.hot_prepped = u1;
+        st.hot_in = *next;
+    }
+    if (st.last_pipe != unit - 1) {    // counters a previous launch of the sequence would have reset
+        if ((rc = pipe_memset(gate + unit % 2, sizeof(int32_t), s, "stepper: gate")) ||
+            (rc = pipe_memset(nhot + u2 % 3, sizeof(int32_t), s, "stepper: hot list")))
+            return rc;
+    }
+    rg_mf_batch_t b2{};
+    rg_mf_work_t w2{};
+    if (next2) {
+        if ((rc = pipe_clean_counts(st, s, (int)(u2 % 3)))) return rc;
+        if ((rc = wait_side(st, s, (int)(u2 % 2))) || (rc = wait_words(st, s, u2))) return rc;
+        b2 = make_batch(st, *next2, u2);
+        w2 = pipe_work(st, *next2, u2);
+    }
+    if ((rc = pipe_clean_accum(st, s, (int)(u1 % 2)))) return rc;   // set u1 % 2 is the pair pass's
+    if ((rc = release(st, s))) return rc;
+    rg_mt_gen_t gen{};
+    int gen_slot = -1;
+    if (st.inline_gen && st.gen_slots == rel_slot(st, unit + 3)) {
+        gen_slot = (int)(st.gen_slots % kSlots);
+        if ((rc = begin_production(st, s, gen_slot))) return rc;
+        gen.state = st.cfg.mt_state;
+        gen.out = st.words[gen_slot];
+        gen.state_before = st.start_state[gen_slot];
+        gen.nwords = st.G * st.W;
+    }
+    rg_mf_pipe_t pp{};
+    pp.hot_users = st.hot[u1 % 3];
+    pp.nhot = nhot + u1 % 3;
+    pp.counts_next = st.pcounts[u1 % 3];
+    pp.gate = gate + unit % 2;
+    pp.gate_next = gate + u1 % 2;
+    pp.nhot_free = nhot + unit % 3;
+    pp.hot_out = next2 ? st.hot[u2 % 3] : nullptr;
+    pp.nhot_out = next2 ? nhot + u2 % 3 : nullptr;
+    pp.err = err;
+    rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};
+    rc = rg_mf_pipe_step(s, tb, &w, &o, &l, &b1, &w1, next2 ? &b2 : nullptr, next2 ? &w2 : nullptr, &pp,
+                         gen_slot >= 0 ? &gen : nullptr);
+    rg::launch_events() = rg::LaunchEvents{};
+    if (rc) return rc;
+    if (gen_slot >= 0) end_production(st, s, gen_slot);
+    st.pdirty[unit % 3] = false;                 // the dense pass consumed and reset its claims
+    st.pair_dirty[unit % 2] = false;             // and its overflow accumulators
+    st.pair_dirty[u1 % 2] = true;
+    st.paired = u1;
+    st.paired_in = *next;
+    if (next2) {
+        st.pdirty[u2 % 3] = true;
+        st.hot_prepped = u2;
+        st.hot_in = *next2;
+    } else {
+        st.hot_prepped = -1;
+    }
+    st.last_pipe = unit;
     st.set = 1 - st.set;
     return RG_OK;
 }
@@ -1003,6 +1203,10 @@ void destroy(Stepper *st) {
     if (st->consts) hipFree(st->consts);
     if (st->rows_done) hipFree(st->rows_done);
     if (st->own_counts) hipFree(st->own_counts);
+    for (void *p : {(void *)st->p_counts2, (void *)st->p_list1, (void *)st->p_hg1, (void *)st->p_hbg1,
+                    (void *)st->p_part1, (void *)st->p_prow1, (void *)st->p_pbias1, (void *)st->hot[0],
+                    (void *)st->hot[1], (void *)st->hot[2], (void *)st->pint})
+        if (p) hipFree(p);
     if (st->own_back) hipEventDestroy(st->own_back);
     if (st->own_grads) hipEventDestroy(st->own_grads);
     if (st->own_users) hipEventDestroy(st->own_users);
@@ -1137,6 +1341,45 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         st->counts[1] = st->own_counts;
     }
     st->prep_in_pairs = env_flag("RG_PREP_IN_PAIRS", false);
+    // pipelined step (rg_mf_pipe_step): single rank, claimed slots, pointwise / bpr / hinge, a
+    // float4 row layout of >= 8 lanes (dim a multiple of 4, 32..256)
+    st->pipe = env_flag("RG_PIPE", RG_PIPE_DEFAULT) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
+               (cfg->loss == RG_LOSS_POINTWISE || cfg->loss == RG_LOSS_BPR || cfg->loss == RG_LOSS_HINGE) &&
+               t0.dim % 4 == 0 && t0.dim >= 32 && t0.dim <= 256 && cfg->work.part_row && cfg->work.part_bias &&
+               cfg->work.loss_partials && cfg->n_partials > 0;
+    if (st->pipe) {
+        // the pair workgroups wait inside the launch: keep them at most half of what the chip
+        // holds (>= 4 workgroups per CU at the launch's register count), so the rows they wait
+        // for always have room to run whatever the dispatch order
+        const int64_t upb = rg_mf_plan_units_per_block(t0.dim);
+        st->pipe = upb > 0 && (cfg->cols + upb - 1) / upb <= 2 * (int64_t)rg::num_cus();
+    }
+    if (st->pipe) {
+        const int64_t rows = t0.num_users + t0.num_items;
+        const int64_t hot_len = std::min<int64_t>(t0.num_users, (int64_t)(1 + cfg->n_neg) * cfg->cols);
+        e = hipMalloc(&st->p_counts2, (size_t)rows * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMemset(st->p_counts2, 0, (size_t)rows * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&st->p_list1, (size_t)rows * RG_MF_LIST_CAP * 2 * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&st->p_hg1, (size_t)rows * t0.dim * sizeof(int64_t));
+        if (e == hipSuccess) e = hipMemset(st->p_hg1, 0, (size_t)rows * t0.dim * sizeof(int64_t));
+        if (e == hipSuccess) e = hipMalloc(&st->p_hbg1, (size_t)rows * sizeof(int64_t));
+        if (e == hipSuccess) e = hipMemset(st->p_hbg1, 0, (size_t)rows * sizeof(int64_t));
+        if (e == hipSuccess) e = hipMalloc(&st->p_part1, (size_t)cfg->n_partials * 2 * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&st->p_prow1, (size_t)cfg->cols * t0.dim * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&st->p_pbias1, (size_t)cfg->cols * sizeof(float));
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipMalloc(&st->hot[k], (size_t)hot_len * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&st->pint, 8 * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMemset(st->pint, 0, 8 * sizeof(int32_t));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            hip_fail("rg_mf_stepper_create: pipelined step buffers", e);
+            destroy(st);
+            return nullptr;
+        }
+        st->pcounts[0] = st->counts[0];
+        st->pcounts[1] = st->counts[1];
+        st->pcounts[2] = st->p_counts2;
+    }
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
     if (env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
@@ -1164,10 +1407,37 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
                                                "(or rg_mf_stepper_owner_begin / _mid / _end around the exchanges)");
         return train_owner(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     }
+    if (st->pipe) return train_pipe(*st, s, *cur, next, nullptr, loss_out, ev_apply_begin, ev_apply_end);
     if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
         return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     if (st->lazy) return train_lazy(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     return train_split(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
+}
+
+extern "C" int rg_mf_stepper_train_ahead(void *h, void *stream, const rg_mf_step_in_t *cur,
+                                         const rg_mf_step_in_t *next, const rg_mf_step_in_t *next2, float *loss_out,
+                                         void *ev_apply_begin, void *ev_apply_end) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !cur) return rg::fail_arg("rg_mf_stepper_train_ahead: null handle/input");
+    if (!next && next2) return rg::fail_arg("rg_mf_stepper_train_ahead: next2 without next");
+    if (st->pipe) return train_pipe(*st, (hipStream_t)stream, *cur, next, next2, loss_out, ev_apply_begin, ev_apply_end);
+    return rg_mf_stepper_train(h, stream, cur, next, loss_out, ev_apply_begin, ev_apply_end);
+}
+
+extern "C" int rg_mf_stepper_pipelined(void *h) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st) return rg::fail_arg("rg_mf_stepper_pipelined: null handle");
+    return st->pipe ? 1 : 0;
+}
+
+extern "C" int rg_mf_stepper_pipe_error(void *h, int32_t *err_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !err_out) return rg::fail_arg("rg_mf_stepper_pipe_error: null argument");
+    *err_out = 0;
+    if (!st->pipe) return RG_OK;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(err_out, st->pint + 5, sizeof(int32_t), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? RG_OK : hip_fail("rg_mf_stepper_pipe_error", e);
 }
 
 extern "C" int rg_mf_stepper_dp_begin(void *h, void *stream, const rg_mf_step_in_t *cur, const rg_mf_step_in_t *next,
@@ -1304,6 +1574,8 @@ extern "C" int rg_mf_stepper_state(void *h, int32_t *current_set, int64_t *step)
 extern "C" int rg_mf_stepper_advance(void *h, int32_t flip_sets, int64_t steps) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st) return rg::fail_arg("rg_mf_stepper_advance: null handle");
+    if (st->pipe && (st->paired >= 0 || st->hot_prepped >= 0))
+        return rg::fail_arg("rg_mf_stepper_advance: a pipelined step is pending (acquire first)");
     if (st->lazy_pending) return rg::fail_arg("rg_mf_stepper_advance: lazy rows pending (rg_mf_stepper_flush first)");
     if (flip_sets) st->set = 1 - st->set;
     st->cfg.step += steps;
@@ -1333,6 +1605,12 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
         return rc;
     }
     // host -> device: words generated ahead are dropped; unit numbering restarts here
+    {
+        const int rc = pipe_abandon(*st, nullptr);
+        if (rc) return rc;
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return hip_fail("stepper: sync", e);
+    }
     st->unit_base = st->taken;
     st->gen_slots = 0;
     for (int i = 0; i < kSlots; ++i) {

@@ -468,9 +468,11 @@ class MFEngine:
         cur = self.step_input(pos_u, pos_i, global_pos, plan)
         return self.train_step_in(cur, next_input if self.prefetch else None, apply_events)
 
-    def train_step_in(self, cur, next_input=None, apply_events=None, loss_out=None):
+    def train_step_in(self, cur, next_input=None, apply_events=None, loss_out=None, next2=None):
         """One native step for a prebuilt ``step_input``; the loss goes to ``loss_out``
-        (a float32 device tensor of >= 1 element) or to the engine's own slot."""
+        (a float32 device tensor of >= 1 element) or to the engine's own slot.  ``next_input`` /
+        ``next2``: the following steps' inputs (the pipelined single-GPU step runs the next
+        step's pair pass and the one after's prepare inside this step's launch)."""
         if self.dp == "user_shard" and self.world > 1 and self.comm is None:
             raise RuntimeError("user-sharded step over several ranks needs an RcclComm (or train_step_sharded)")
         if self.dp == "global_stream" and self.comm is None:
@@ -489,10 +491,27 @@ class MFEngine:
         out = self.loss_out if loss_out is None else loss_out
         if out.dtype != torch.float32 or out.device != self.device:
             raise ValueError("loss_out must be a float32 tensor on the engine's device")
+        if next2 is not None and next_input is not None:
+            check(self.lib.rg_mf_stepper_train_ahead(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
+                                                     ctypes.byref(next_input), ctypes.byref(next2), ptr(out), ev0,
+                                                     ev1), "rg_mf_stepper_train_ahead")
+            return out
         check(self.lib.rg_mf_stepper_train(self._stepper, _lib.stream_handle(), ctypes.byref(cur),
                                            ctypes.byref(next_input) if next_input is not None else None,
                                            ptr(out), ev0, ev1), "rg_mf_stepper_train")
         return out
+
+    @property
+    def pipelined(self):
+        """True if the native step is the pipelined one (rg_mf_pipe_step)."""
+        return self.lib.rg_mf_stepper_pipelined(self._stepper) == 1
+
+    def pipe_error(self):
+        """True if a pipelined launch's pair workgroups ran out of their bounded wait (then its
+        results are wrong; synchronises)."""
+        e = ctypes.c_int32(0)
+        check(self.lib.rg_mf_stepper_pipe_error(self._stepper, ctypes.byref(e)), "rg_mf_stepper_pipe_error")
+        return bool(e.value)
 
     def _acquire(self, cur):
         batch, work = _lib.MFBatch(), _lib.MFWork()

@@ -46,7 +46,7 @@ CTYPES_MIRRORS = {
     "rg_mf_owner_batch_t": "MFOwnerBatch", "rg_mf_stepper_config_t": "MFStepperConfig",
     "rg_mf_step_in_t": "MFStepIn", "rg_ncf_model_t": "NCFModel", "rg_ncf_work_t": "NCFWork",
     "rg_gan_dims_t": "GANDims", "rg_gan_model_t": "GANModel", "rg_gan_batch_t": "GANBatch",
-    "rg_gan_noise_t": "GANNoise", "rg_mf_lazy_t": "MFLazy"}
+    "rg_gan_noise_t": "GANNoise", "rg_mf_lazy_t": "MFLazy", "rg_mf_pipe_t": "MFPipe"}
 
 
 def header_structs():

@@ -1,0 +1,100 @@
+"""The pipelined single-GPU MF step (rg_mf_pipe_step: step t's dense update, step t+1's pair pass
+and step t+2's prepare in one launch) against the split step (RG_PIPE=0): the same per-row and
+per-column arithmetic in the same order, so losses, tables, optimizer state and the MT stream are
+bit-identical -- over several steps, with item plans and Zipf-hot rows overflowing their lists,
+for every loss the pipeline takes, at d = 32 / 64 / 128; and when the lookahead it was given turns
+out wrong (another next batch, a validation pass in between), what it ran ahead is dropped."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(pipe, loss, d, U, I, B, n, seed=0):
+    from oracle import rng as orng
+    from recommendation_gans_amd.mf_engine import MFEngine
+    old = os.environ.get("RG_PIPE")
+    os.environ["RG_PIPE"] = "1" if pipe else "0"
+    try:
+        torch.manual_seed(seed)
+        Uw, Iw = torch.empty(U, d).normal_(0, 1.0 / d), torch.empty(I, d).normal_(0, 1.0 / d)
+        rs = np.random.RandomState(seed)
+        pool_u, pool_i = rs.randint(0, U, 40000), rs.randint(0, I, 40000)
+        e = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), pool_u, pool_i, orng.py_seed_state(seed), loss=loss,
+                     optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B,
+                     device=torch.device("cuda:0"))
+    finally:
+        if old is None:
+            os.environ.pop("RG_PIPE", None)
+        else:
+            os.environ["RG_PIPE"] = old
+    assert e.pipelined == pipe
+    return e
+
+
+def _inputs(e, U, I, B, steps, seed=1):
+    rs = np.random.RandomState(seed)
+    dev = torch.device("cuda:0")
+    out = []
+    for s in range(steps):
+        pu = torch.from_numpy(rs.randint(0, U, B).astype(np.int64)).to(dev)
+        pi = torch.from_numpy(np.minimum(rs.zipf(1.2, B) - 1, I - 1).astype(np.int64)).to(dev)
+        out.append(e.step_input(pu, pi, B, e.make_plan(pi)))
+    return out
+
+
+def _state(e):
+    torch.cuda.synchronize()
+    t = [p.detach().cpu().clone() for p in e.params()]
+    st = [x.detach().cpu().clone() for x in (e.m + e.v) if x is not None]
+    return t, st, e.mt_state().copy()
+
+
+def _same(a, b):
+    for x, y in zip(a[0] + a[1], b[0] + b[1]):
+        assert torch.equal(x, y), float((x - y).abs().max())
+    assert (a[2] == b[2]).all()
+
+
+@pytest.mark.parametrize("loss,d", [("bpr", 64), ("pointwise", 64), ("hinge", 64), ("bpr", 32), ("bpr", 128)])
+def test_pipelined_step_is_bit_identical(loss, d):
+    U, I, B, n, steps = 3000, 400, 1024, 5, 7
+    ref, pipe = _engine(False, loss, d, U, I, B, n), _engine(True, loss, d, U, I, B, n)
+    ins_r, ins_p = _inputs(ref, U, I, B, steps), _inputs(pipe, U, I, B, steps)
+    lr, lp = [], []
+    for s in range(steps):
+        nx = ins_r[s + 1] if s + 1 < steps else None
+        lr.append(float(ref.train_step_in(ins_r[s], nx)[0]))
+        nxp = ins_p[s + 1] if s + 1 < steps else None
+        nx2 = ins_p[s + 2] if s + 2 < steps else None
+        lp.append(float(pipe.train_step_in(ins_p[s], nxp, next2=nx2)[0]))
+    assert lr == lp, (lr, lp)
+    assert not pipe.pipe_error()
+    _same(_state(ref), _state(pipe))
+
+
+def test_pipelined_lookahead_dropped():
+    """The lookahead given to step s names batch X for step s+1, but step s+1 trains batch Y; and
+    a validation pass (rg_mf_stepper_acquire) comes between two pipelined steps: both engines end
+    bit-identical to the split step over the same sequence."""
+    U, I, B, n, d = 3000, 400, 1024, 5, 64
+    ref, pipe = _engine(False, "bpr", d, U, I, B, n), _engine(True, "bpr", d, U, I, B, n)
+    ins_r, ins_p = _inputs(ref, U, I, B, 6), _inputs(pipe, U, I, B, 6)
+    vr, vp = _inputs(ref, U, I, B, 1, seed=9)[0], _inputs(pipe, U, I, B, 1, seed=9)[0]
+    # s0 announces (1, 2), but s1 trains batch 3 (announcing 4, 5); then validation; then 4, 5
+    seq = [(0, 1, 2), (3, 4, 5), "val", (4, 5, None), (5, None, None)]
+    lr, lp = [], []
+    for item in seq:
+        if item == "val":
+            lr.append(float(ref.val_loss(*vr._keep[:2], plan=vr._keep[2])[0]))
+            lp.append(float(pipe.val_loss(*vp._keep[:2], plan=vp._keep[2])[0]))
+            continue
+        a, b, c = item
+        lr.append(float(ref.train_step_in(ins_r[a], ins_r[b] if b is not None else None)[0]))
+        lp.append(float(pipe.train_step_in(ins_p[a], ins_p[b] if b is not None else None,
+                                           next2=ins_p[c] if c is not None else None)[0]))
+    assert lr == lp, (lr, lp)
+    _same(_state(ref), _state(pipe))
