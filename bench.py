@@ -10,8 +10,8 @@ MT19937 stream, the BPR loss on the neg.view(n, B) pairing, backward, and a dens
 coupled-L2 Adam update of every row of the four BilinearNet tables (the
 reference's semantics: implicit.py:347-364, spotlight/optimizers.py:10-16).
 The native stepper runs it as rg_mf_pairs -> rg_mf_apply_prepare (the dense
-update and the next step's prepare in one launch); RG_FUSED=1 selects the
-overlapped two-launch step (rg_mf_step_front + rg_mf_step_hot, measured slower).
+update and the next step's prepare in one launch); under an A/B build
+RG_FUSED=1 selects the overlapped two-launch step (measured slower).
 Inputs (positive ids, pool, tables) are resident in HBM before timing starts.
 
 With N > 1 ranks (one process per GPU) the default is the reference-exact
@@ -204,6 +204,7 @@ def bench_ncf(args):
     """Config 3: ncf_spotlight.py MovieLens-20M, mlp_embedding_dim=64, 1 GPU (pointwise, the CLI's
     loss; dropout from the device hash RNG).  --model neumf: neuMF_spotlight.py with the
     CLI's defaults (mlp_embedding_dim 16, mf_embedding_dim 50), same data and loop."""
+    from recommendation_gans_amd import _lib
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,7 +299,8 @@ def bench_ncf(args):
                       "parallelism": f"dp{world}" + (" replicated (embedding + MLP gradient all-reduce, "
                                                      "reference-exact)" if world > 1 else "")},
            "roofline": {"bound": "mfma", "kernel": "rg_ncf_pairs (" + ("ncf_wave_kernel" if E == 64 and not neumf
-                                                                    and os.environ.get("RG_NCF_TILE") != "1"
+                                                                    and not (_lib.ab_build() and
+                                                                             os.environ.get("RG_NCF_TILE") == "1")
                                                                     else "ncf_pairs_kernel") + ")", "achieved": ach,
                         "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
                         "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
@@ -625,7 +627,8 @@ def main():
         rg_build.build()
     d, B, n = args.dim, args.batch, args.neg
     # the stepper's overlapped step (rg_stepper.cpp train_fused) unless disabled
-    fused = os.environ.get("RG_FUSED", "0") == "1" and args.loss != "adaptive_hinge"
+    from recommendation_gans_amd import _lib as _rglib
+    fused = _rglib.ab_build() and os.environ.get("RG_FUSED", "0") == "1" and args.loss != "adaptive_hinge"
     data = movielens_like(ML20M, seed=0, zipf_s=args.zipf)
     U, I = data.num_users, data.num_items
     torch.manual_seed(0)                               # mf_spotlight.py:37

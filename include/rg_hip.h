@@ -876,6 +876,11 @@ const char *rg_last_error(void);
 
 /* Library build identification (gfx target, ABI version). */
 const char *rg_version(void);
+/* Build flags: RG_BUILD_AB = an A/B build (build.py --variant NAME -DRG_AB=1) carrying the
+ * measured-slower alternatives behind RG_* environment switches; the product
+ * library returns 0 and reads none of those switches. */
+#define RG_BUILD_AB 1
+int32_t rg_build_flags(void);
 
 #ifdef __cplusplus
 }

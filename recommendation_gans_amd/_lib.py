@@ -359,6 +359,7 @@ SIGNATURES = [
     ("rg_event_elapsed_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_last_error", ctypes.c_char_p, []),
     ("rg_version", ctypes.c_char_p, []),
+    ("rg_build_flags", ctypes.c_int32, []),
 ]
 
 _lib = None
@@ -386,6 +387,15 @@ def load(path=None):
         fn.argtypes = args
     _lib = L
     return L
+
+
+RG_BUILD_AB = 1
+
+
+def ab_build():
+    """True when the loaded library is an A/B build (RG_AB): only then do the measured-slower
+    alternatives' RG_* switches select anything."""
+    return bool(load().rg_build_flags() & RG_BUILD_AB)
 
 
 def check(rc, what):

@@ -6,6 +6,13 @@
 
 #include "../../include/rg_hip.h"
 
+// RG_AB=1 (build.py --variant NAME -DRG_AB=1): the measured-slower alternatives kept for
+// same-box A/B runs, selected by RG_* environment switches.  The product library
+// is built without them: one tested path per configuration, no environment switches on it.
+#ifndef RG_AB
+#define RG_AB 0
+#endif
+
 namespace rg {
 
 constexpr int kWave = 64;

@@ -782,9 +782,6 @@ __device__ __forceinline__ void catch_up(const ApplyArgs &a, float2 cl, int wmax
 #ifndef RG_LEAN_PG
 #define RG_LEAN_PG 2
 #endif
-#ifndef RG_DENSE_PIPE_DEFAULT
-#define RG_DENSE_PIPE_DEFAULT 0
-#endif
 // Ascending sort of the 8 list entries held one per lane (lanes sub 0..7 of each LPU-lane row
 // group; sub >= 8 hold +inf keys and sort among themselves): a bitonic network over lane
 // XOR partners, 6 compare-exchange stages of 64-bit keys.  The result (entry e on lane e) is
@@ -1872,9 +1869,11 @@ struct ApplyLaunchF {
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
+#if RG_AB
+        // A/B build only (measured no faster): non-temporal stores, the list loaded
+        // beside the count
         static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
         static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 0; }();
-        static const int grad_spec = [] { const char *e = getenv("RG_GRAD_SPEC"); return e ? atoi(e) : 1; }();
         if (mode == kApplyPull && spec && nt == 1)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1, true>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kApplyPull && spec)
@@ -1883,12 +1882,12 @@ struct ApplyLaunchF {
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 1>), dim3(nb), dim3(kBlock), 0, s, *a);
         else if (mode == kApplyPull && nt >= 2)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull, 2>), dim3(nb), dim3(kBlock), 0, s, *a);
-        else if (mode == kApplyPull)
+        else
+#endif
+        if (mode == kApplyPull)
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyPull>), dim3(nb), dim3(kBlock), 0, s, *a);
-        else if (mode == kGradOnly && grad_spec)   // list and slot range loaded beside the count
+        else if (mode == kGradOnly)   // list and slot range loaded beside the count
             hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly, 0, true>), dim3(nb), dim3(kBlock), 0, s, *a);
-        else if (mode == kGradOnly)
-            hipLaunchKernelGGL((mf_apply_kernel<L, kGradOnly>), dim3(nb), dim3(kBlock), 0, s, *a);
         else
             hipLaunchKernelGGL((mf_apply_kernel<L, kApplyDense>), dim3(nb), dim3(kBlock), 0, s, *a);
         return check_launch("rg_mf_apply");
@@ -2212,8 +2211,19 @@ struct BackLaunchF {
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         if (nb < 1) nb = 1;
+#if RG_AB
+        // A/B build only (each measured slower or no faster): prepare blocks after the
+        // dense blocks, the XCD-aware dense mapping, non-temporal stores, the list read after the
+        // count, the persistent pipelined dense kernel
         static const int prep_first = [] { const char *e = getenv("RG_PREP_FIRST"); return e ? atoi(e) : 1; }();
-        static const int xcd_map = [] { const char *e = getenv("RG_XCD_MAP"); return e ? atoi(e) : 0; }();   // measured 3 us slower
+        static const int xcd_map = [] { const char *e = getenv("RG_XCD_MAP"); return e ? atoi(e) : 0; }();
+        static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
+        static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
+        static const int lazy_spec = [] { const char *e = getenv("RG_LAZY_SPEC"); return e ? atoi(e) : 0; }();
+        static const int dense_v2 = [] { const char *e = getenv("RG_DENSE_PIPE"); return e ? atoi(e) : 0; }();
+#else
+        constexpr int prep_first = 1, xcd_map = 0;
+#endif
         BackGrid bg{prep_blocks, 0, 0, prep_first, prep_first ? xcd_map : 0};
         const int64_t head = prep_blocks + (gen.nwords > 0 ? 1 : 0);
         int64_t total = nb + head;
@@ -2223,12 +2233,6 @@ struct BackLaunchF {
             total = bg.apply_start + bg.apply_padded;
         }
         const dim3 grid((unsigned)total);
-        static const int nt = [] { const char *e = getenv("RG_APPLY_NT"); return e ? atoi(e) : 0; }();
-        // the list is loaded beside the count (one dependent round trip fewer; +1 % same-box,
-        // RG_APPLY_SPEC=0 turns it off)
-        static const int spec = [] { const char *e = getenv("RG_APPLY_SPEC"); return e ? atoi(e) : 1; }();
-        // lazy pass: the optimizer state loaded before the row decision (RG_LAZY_SPEC=1)
-        static const int lazy_spec = [] { const char *e = getenv("RG_LAZY_SPEC"); return e ? atoi(e) : 0; }();
         const OwnerArgs oa = own ? *own : OwnerArgs{};
         LaunchEvents &le = launch_events();
         const hipEvent_t e0 = le.start, e1 = le.stop;
@@ -2239,9 +2243,13 @@ struct BackLaunchF {
             else
                 hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
         };
-        static const int dense_v2 = [] { const char *e = getenv("RG_DENSE_PIPE"); return e ? atoi(e) : RG_DENSE_PIPE_DEFAULT; }();
+        if (own) {
+            go(mf_back_kernel<L, 0, true, true>);
+            return check_launch("rg_mf_apply_prepare");
+        }
+#if RG_AB
         if constexpr (L::LPU >= kCap) {
-            if (!own && !lazy && dense_v2 && a->contrib == nullptr) {
+            if (!lazy && dense_v2 && a->contrib == nullptr) {
                 // a few workgroups per CU, each wave walking a chunk of row groups (mf_dense_kernel)
                 static const int per_cu = [] { const char *e = getenv("RG_DENSE_PER_CU"); return e ? atoi(e) : 4; }();
                 int64_t db = (int64_t)num_cus() * per_cu;
@@ -2260,8 +2268,7 @@ struct BackLaunchF {
                 return check_launch("rg_mf_apply_prepare");
             }
         }
-        if (own) go(mf_back_kernel<L, 0, true, true>);
-        else if (lazy && lazy_spec) go(mf_back_kernel<L, 0, true, false, true, true>);
+        if (lazy && lazy_spec) go(mf_back_kernel<L, 0, true, false, true, true>);
         else if (lazy) go(mf_back_kernel<L, 0, true, false, true>);
         else if (spec && nt == 1) go(mf_back_kernel<L, 1, true>);
         else if (spec && nt == 3) go(mf_back_kernel<L, 3, true>);
@@ -2269,6 +2276,10 @@ struct BackLaunchF {
         else if (nt == 1) go(mf_back_kernel<L, 1>);
         else if (nt >= 2) go(mf_back_kernel<L, 2>);
         else go(mf_back_kernel<L, 0>);
+#else
+        if (lazy) return fail_arg("the lazy dense pass is an A/B build (build.py --variant lazy -DRG_AB=1)");
+        go(mf_back_kernel<L, 0, true>);   // the list loaded beside the count
+#endif
         return check_launch("rg_mf_apply_prepare");
     }
 };
@@ -2446,10 +2457,15 @@ int lazy_args(const rg_mf_lazy_t *lz, const rg_opt_t *opt, ApplyArgs &a) {
     a.lazy_t = (int32_t)lz->step;
     a.lazy_full = lz->full;
     a.lazy_rows = reinterpret_cast<unsigned long long *>(lz->rows_done);
+#if RG_AB
     static const int dbg = [] { const char *e = getenv("RG_LAZY_DBG"); return e ? atoi(e) : 0; }();
     static const int cap = [] { const char *e = getenv("RG_LAZY_CAP"); return e ? atoi(e) : 0; }();
     a.lazy_dbg = dbg;
     a.lazy_cap = cap;
+#else
+    a.lazy_dbg = 0;
+    a.lazy_cap = 0;
+#endif
     return RG_OK;
 }
 }  // namespace

@@ -172,7 +172,11 @@ MtJumpPlan *mt_jump_plan_create(int64_t words) {
     const int64_t head = kDeg + kN - 1;          // windows S_i, i < 19937, need x[0 .. 20560)
     if (words < 2 * head || mtj::charpoly().empty()) return nullptr;
     // tail segments of ~20k words: each walks about as long as the head does
+#if RG_AB
     const char *env = getenv("RG_MT_TAIL");
+#else
+    const char *env = nullptr;
+#endif
     int n = env ? atoi(env) : (int)((words - head + 19999) / 20000);
     n = n < 1 ? 1 : (n > kMtMaxTail ? kMtMaxTail : n);
     MtJumpPlan *p = new MtJumpPlan();

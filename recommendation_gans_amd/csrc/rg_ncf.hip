@@ -1612,10 +1612,15 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 }
 
 static bool ncf_use_wave(int E, int M) {
+#if RG_AB
+    // the tile kernel for E = 64 (measured slower), A/B build only
     static const bool off = [] {
         const char *s = getenv("RG_NCF_TILE");
         return s && s[0] == '1';
     }();
+#else
+    constexpr bool off = false;
+#endif
     return E == 64 && M == 0 && !off;
 }
 

@@ -147,7 +147,11 @@ extern "C" int rg_mt_generate(void *stream, uint32_t *state_dev, uint32_t *out_w
     if (state_dev == nullptr) return rg::fail_arg("rg_mt_generate: null state");
     if (nwords < 0) return rg::fail_arg("rg_mt_generate: nwords < 0");
     if (nwords > 0 && out_words_dev == nullptr) return rg::fail_arg("rg_mt_generate: null output");
+#if RG_AB
     static const int prio = [] { const char *e = getenv("RG_MT_PRIO"); return e ? atoi(e) : 0; }();
+#else
+    constexpr int prio = 0;
+#endif
     hipLaunchKernelGGL(rg::mt_generate_kernel, dim3(1), dim3(rg::kGenThreads), 0, (hipStream_t)stream,
                        state_dev, out_words_dev, nwords, state_before_dev, prio);
     return rg::check_launch("rg_mt_generate");

@@ -512,6 +512,26 @@ bool env_flag(const char *name, bool dflt) {
     return e ? atoi(e) != 0 : dflt;
 }
 
+// a switch of the A/B build only (RG_AB, rg_common.h): the product keeps its default
+bool ab_flag(const char *name, bool dflt) {
+#if RG_AB
+    return env_flag(name, dflt);
+#else
+    (void)name;
+    return dflt;
+#endif
+}
+
+int ab_int(const char *name, int dflt) {
+#if RG_AB
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
+
 int record(void *ev, hipStream_t s) {
     if (!ev) return RG_OK;
     hipError_t e = hipEventRecord((hipEvent_t)ev, s);
@@ -1249,7 +1269,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->set = cfg->current_set;
     st->W = 2 * (int64_t)cfg->n_neg * cfg->global_cols;
     if (st->cfg.neg_cols <= 0) st->cfg.neg_cols = cfg->global_cols;
-    st->fused = env_flag("RG_FUSED", false);
+    st->fused = ab_flag("RG_FUSED", false);
     {
         // inline walk (default): one unit per slot, walked inside the dense pass two steps
         // ahead, when the walk (~0.47 ns/word on one workgroup) hides under that pass
@@ -1268,19 +1288,19 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         if (st->G < 1) st->G = 1;
         if (st->G > 64) st->G = 64;
     }
-    st->hot_scan = env_flag("RG_HOT_SCAN", true);
+    st->hot_scan = ab_flag("RG_HOT_SCAN", true);
     // separate priorities keep the streams on separate hardware queues: the walk is
     // background work (lowest), the short side prepare is on the step's path (highest)
     int least = 0, greatest = 0;
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const int prio_mode = getenv("RG_STREAM_PRIO") ? atoi(getenv("RG_STREAM_PRIO")) : 1;
+    const int prio_mode = ab_int("RG_STREAM_PRIO", 1);
     if (e == hipSuccess)
         e = hipStreamCreateWithPriority(&st->gen, hipStreamNonBlocking, prio_mode ? least : 0);
     if (e == hipSuccess)
         e = hipStreamCreateWithPriority(&st->prep, hipStreamNonBlocking, prio_mode ? greatest : 0);
     // the events only order streams of this device: no system-scope fence (which
     // writes back and invalidates caches at every marker, ~7 us of idle per packet)
-    const int ev_mode = getenv("RG_EVENT_MODE") ? atoi(getenv("RG_EVENT_MODE")) : 1;
+    const int ev_mode = ab_int("RG_EVENT_MODE", 1);
     const unsigned evf = hipEventDisableTiming | (ev_mode == 1 ? hipEventDisableSystemFence
                                                  : ev_mode == 2 ? hipEventReleaseToDevice : 0u);
     const size_t slot_words = (size_t)(st->G * st->W + RG_MT_PAD);
@@ -1302,7 +1322,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->cp_pos = (int32_t)pos;
     // lazy dense pass (opt-in, RG_LAZY=1): the single-rank split step.  Bit-exact with the
     // eager pass but measured slower on gfx950 (the catch-up is ALU-bound).
-    st->lazy = env_flag("RG_LAZY", false) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
+    st->lazy = ab_flag("RG_LAZY", false) && cfg->dp_mode == 0 && !cfg->item_grad && !st->fused;
     if (st->lazy) {
         const size_t ub = (size_t)cfg->tables[0].num_users * sizeof(int32_t);
         e = hipMalloc(&st->last_rel, ub);
@@ -1323,7 +1343,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     // claims its slots with returning atomics, as before)
     const rg_mf_tables_t &t0 = cfg->tables[0];
     // (the owner-sharded step claims in its owner prepare, records keep the slots beside the ids)
-    st->claim = env_flag("RG_MF_CLAIM", true) && !cfg->item_grad && !st->fused && !st->lazy &&
+    st->claim = ab_flag("RG_MF_CLAIM", true) && !cfg->item_grad && !st->fused && !st->lazy &&
                 cfg->loss != RG_LOSS_ADAPTIVE_HINGE && cfg->work.row_count != nullptr &&
                 (cfg->dp_mode == 2 ||
                  (cfg->dp_mode == 0 && t0.num_users < ((int64_t)1 << 27) && t0.num_items < ((int64_t)1 << 27)));
@@ -1340,7 +1360,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         st->counts[0] = cfg->work.row_count;
         st->counts[1] = st->own_counts;
     }
-    st->prep_in_pairs = env_flag("RG_PREP_IN_PAIRS", false);
+    st->prep_in_pairs = ab_flag("RG_PREP_IN_PAIRS", false);
     // pipelined step (rg_mf_pipe_step): single rank, claimed slots, pointwise / bpr / hinge, a
     // float4 row layout of >= 8 lanes (dim a multiple of 4, 32..256)
     st->pipe = env_flag("RG_PIPE", RG_PIPE_DEFAULT) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&

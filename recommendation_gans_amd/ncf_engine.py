@@ -125,7 +125,7 @@ class NCFEngine:
         self.seed = int(seed)
         self.t = 0
         self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
-        self._prefetch_side = os.environ.get("RG_NCF_PREFETCH_SIDE") == "1"
+        self._prefetch_side = _lib.ab_build() and os.environ.get("RG_NCF_PREFETCH_SIDE") == "1"
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
                                     self.U, self.I, E, self.M)
@@ -150,7 +150,7 @@ class NCFEngine:
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
         # no fused dense pass walks the MT words here: 8-step slots on the generator stream (one
         # walk and one cross-stream hop per 8 steps instead of per step)
-        cfg.gen_mode = 0 if os.environ.get("RG_NCF_GEN_INLINE") == "1" else 1
+        cfg.gen_mode = 0 if _lib.ab_build() and os.environ.get("RG_NCF_GEN_INLINE") == "1" else 1
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())

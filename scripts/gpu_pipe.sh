@@ -1,4 +1,5 @@
-# round 4: the pipelined MF step -- bit-identity tests, then the bench A/B (RG_PIPE=0 / 1)
+# GPU box: the pipelined MF step -- bit-identity tests, then the bench A/B against the split step
+# (RG_PIPE=0 / 1, cold-row workgroup counts) and a kernel-stats profile.  Usage: bash scripts/gpu_pipe.sh
 set -o pipefail
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT

@@ -125,7 +125,7 @@ def test_ncf_launch_geometry():
     L = _lib.load()
     assert L.rg_ncf_rows_per_tile() == 32
     assert L.rg_ncf_cols_per_tile(5) == 5 and L.rg_ncf_tiles(8192, 5) == 1639
-    wave = os.environ.get("RG_NCF_TILE") != "1"
+    wave = not (_lib.ab_build() and os.environ.get("RG_NCF_TILE") == "1")
     assert L.rg_ncf_blocks(8192, 5, 64, 0) == (256 if wave else 256)
     assert L.rg_ncf_blocks(1000, 5, 64, 0) == ((200 + 3) // 4 if wave else 200)
     assert L.rg_ncf_blocks(20, 5, 64, 0) == (1 if wave else 4)

@@ -26,6 +26,10 @@ def dev():
     from recommendation_gans_amd import _lib
     _lib.load()
     assert torch.cuda.is_available()
+    if not _lib.ab_build():
+        # the overlapped step (RG_FUSED) is a measured-slower alternative carried only by the A/B build
+        # (DESIGN.md §9): scripts/gpu_ab_tests.sh runs this file with RG_LIB pointing at it
+        pytest.skip("A/B build only (RG_LIB=recommendation_gans_amd/_variants/librg_hip_ab.so)")
     return torch.device("cuda:0")
 
 
