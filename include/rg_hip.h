@@ -676,7 +676,9 @@ typedef struct rg_ncf_work {
     float *dp;                              /* [tiles * rows_per_tile] (given-dp phase) */
     const uint8_t *mask_pos, *mask_neg;     /* recorded dropout masks [rows][rg_ncf_mask_units] or null */
     uint64_t seed;                          /* dropout hash seed when no masks are given */
-    int32_t training, pad_;                 /* 0: eval (no dropout) */
+    int32_t training;                       /* 0: eval (no dropout) */
+    int32_t tile_rows;                      /* rg_ncf_rows_per_tile(dim, mf_dim): the layout of
+                                               contrib / scores / dp (rg_ncf_pairs checks it) */
     /* NeuMF only: per-example GMF gradient rows [tiles * rows_per_tile * 2M] (user | item),
      * overflow rows [(U + I) * M] (zero between steps), planned positive partials [cols * M] */
     float *mf_contrib;
@@ -688,9 +690,11 @@ int64_t rg_ncf_mlp_len(int32_t dim);
 /* NeuMF flat parameters (tower layers, then affine_output (1 x (8 + M)) and its bias) */
 int64_t rg_neumf_param_len(int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_mask_units(int32_t dim);
-int64_t rg_ncf_cols_per_tile(int32_t n_neg);   /* also the plan's units per block */
-int64_t rg_ncf_rows_per_tile(void);
-int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg);
+/* Tile geometry of a model: rows per tile (48 for the E = 64 MLP's wave kernel, 32 for the
+ * other towers and NeuMF), columns per tile (also the plan's units per block), tiles. */
+int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim);
+int64_t rg_ncf_cols_per_tile(int32_t n_neg, int32_t dim, int32_t mf_dim);
+int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim);
 /* workgroups of rg_ncf_pairs (= weight-gradient partials): tiles, capped at 256 x the workgroups
  * per CU that the dim's LDS allows (1 for the E = 64 MLP, up to 4) */
 int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim);

@@ -115,7 +115,7 @@ class NCFModel(ctypes.Structure):
 class NCFWork(ctypes.Structure):
     _fields_ = [("contrib", ctypes.c_void_p), ("mlp_partials", ctypes.c_void_p), ("scores", ctypes.c_void_p),
                 ("dp", ctypes.c_void_p), ("mask_pos", ctypes.c_void_p), ("mask_neg", ctypes.c_void_p),
-                ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("training", ctypes.c_int32), ("tile_rows", ctypes.c_int32),
                 ("mf_contrib", ctypes.c_void_p), ("mf_hot_grad", ctypes.c_void_p), ("mf_part_row", ctypes.c_void_p)]
 
 
@@ -194,9 +194,9 @@ SIGNATURES = [
     ("rg_ncf_mlp_len", ctypes.c_int64, [ctypes.c_int32]),
     ("rg_neumf_param_len", ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_mask_units", ctypes.c_int64, [ctypes.c_int32]),
-    ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32]),
-    ("rg_ncf_rows_per_tile", ctypes.c_int64, []),
-    ("rg_ncf_tiles", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_ncf_cols_per_tile", ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rg_ncf_rows_per_tile", ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    ("rg_ncf_tiles", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_blocks", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_ncf_pairs", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFBatch),
                                     ctypes.POINTER(MFWork), ctypes.POINTER(NCFWork), ctypes.c_int32]),

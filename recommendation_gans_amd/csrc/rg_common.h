@@ -16,6 +16,7 @@
 namespace rg {
 
 constexpr int kWave = 64;
+constexpr int kSc1 = 16;   // buffer-intrinsic cache-policy operand: sc1 (gfx940+ CPol::SC1)
 
 // ---------------------------------------------------------------- errors
 void set_error(const std::string &msg);
@@ -250,40 +251,43 @@ struct RowLayout {
     // write-through store (sc1): the bytes go to memory and the line leaves the XCD's L2, so
     // the pass leaves no dirty lines for the end-of-kernel write-back (MI355X guide: "stores of
     // each flavour")
+    // write-through store (sc1) of a row slice: one 16-byte buffer store per lane, so every
+    // 128-byte row reaches memory as whole lines (two interleaved 8-byte halves would each write
+    // half of every sector).  The table must be < 2 GiB (32-bit offsets; rg_mf_pipe_step checks).
     __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int D, int sub,
                                                     const float (&v)[EPL]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xffffffff, 0x00020000);
         if constexpr (VEC) {
             typedef float v4f __attribute__((ext_vector_type(4)));
-            v4f t = {v[0], v[1], v[2], v[3]};
-            float *p = base + row * (int64_t)(4 * LPU) + sub * 4;
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+            const v4f t = {v[0], v[1], v[2], v[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, kSc1);
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
                 const int c = sub + LPU * e;
-                if (c < D) store1_wt(base + row * (int64_t)D + c, v[e]);
+                if (c < D) __builtin_amdgcn_raw_buffer_store_b32(v[e], rs, (int)((row * D + c) * 4), 0, kSc1);
             }
         }
     }
     __device__ static __forceinline__ void store1_wt(float *p, float v) {
-        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store_dword ... sc1
     }
 
     // load past the CU's L1 (sc1: served by L2 / memory): reads rows another workgroup of the
-    // same launch wrote with write-through stores (the pipelined MF step's pair pass)
+    // same launch wrote with write-through stores (the pipelined MF step's pair pass); < 2 GiB
     __device__ static __forceinline__ void load_sc1(float (&v)[EPL], const float *__restrict__ base,
                                                     int64_t row, int D, int sub) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0xffffffff,
                                                                            0x00020000);
         if constexpr (VEC) {
             typedef float v4f __attribute__((ext_vector_type(4)));
-            const v4f t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, 16);
+            const v4f t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, kSc1);
             v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
         } else {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
                 const int c = sub + LPU * e;
-                v[e] = c < D ? __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((row * D + c) * 4), 0, 16) : 0.0f;
+                v[e] = c < D ? __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((row * D + c) * 4), 0, kSc1) : 0.0f;
             }
         }
     }

@@ -958,26 +958,18 @@ __device__ __forceinline__ void lean_finish(const ApplyArgs &a, const int64_t r,
     if (!valid) return;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) x.p[q] = opt_update(a.opt, x.p[q], g[q], x.m[q], x.v[q]);
-    if (WT) {   // write-through: another workgroup of the launch reads the row (mf_pipe_kernel)
-        L::store_wt(a.w_out[t], lr_, D, sub, x.p);
-        if (adam) L::store_wt(a.w_m[t], lr_, D, sub, x.m);
-        if (has_v) L::store_wt(a.w_v[t], lr_, D, sub, x.v);
-    } else {
-        L::store(a.w_out[t], lr_, D, sub, x.p);
-        if (adam) L::store(a.w_m[t], lr_, D, sub, x.m);
-        if (has_v) L::store(a.w_v[t], lr_, D, sub, x.v);
-    }
+    // WT: the row and bias write-through (another workgroup of the launch reads them:
+    // mf_pipe_kernel's pair pass); the optimizer state is not read there
+    if (WT) L::store_wt(a.w_out[t], lr_, D, sub, x.p);
+    else L::store(a.w_out[t], lr_, D, sub, x.p);
+    if (adam) L::store(a.w_m[t], lr_, D, sub, x.m);
+    if (has_v) L::store(a.w_v[t], lr_, D, sub, x.v);
     if (sub == 0 && a.has_bias) {
         x.pb = opt_update(a.opt, x.pb, gb, x.mb, x.vb);
-        if (WT) {
-            L::store1_wt(a.b_out[t] + lr_, x.pb);
-            if (adam) L::store1_wt(a.b_m[t] + lr_, x.mb);
-            if (has_v) L::store1_wt(a.b_v[t] + lr_, x.vb);
-        } else {
-            a.b_out[t][lr_] = x.pb;
-            if (adam) a.b_m[t][lr_] = x.mb;
-            if (has_v) a.b_v[t][lr_] = x.vb;
-        }
+        if (WT) L::store1_wt(a.b_out[t] + lr_, x.pb);
+        else a.b_out[t][lr_] = x.pb;
+        if (adam) a.b_m[t][lr_] = x.mb;
+        if (has_v) a.b_v[t][lr_] = x.vb;
     }
 }
 
@@ -1576,11 +1568,11 @@ struct PipeArgs {
     uint32_t spin_limit;
 };
 
-template <class L>
+template <class L, bool WT>
 __device__ __forceinline__ void pipe_rows(const ApplyArgs &a, const int64_t r, const bool valid, const int sub) {
     LeanRow<L> x;
     lean_load<L>(a, r, sub, valid, x);
-    lean_finish<L, true>(a, r, sub, valid, x);
+    lean_finish<L, WT>(a, r, sub, valid, x);
 }
 
 template <class L, int NMAX>
@@ -1635,6 +1627,9 @@ __global__ __launch_bounds__(kBlock) void mf_pipe_kernel(ApplyArgs a, PairsArgs 
             cold = blk;
         } else if (blk < pp.cold1_blocks + pp.pair_blocks) {     // pair pass of step t + 1
         const int64_t pb = blk - pp.cold1_blocks;
+#ifdef RG_PIPE_X   // timing experiments only (wrong results): bit 0 no pair pass, bit 1 no wait either
+        if (RG_PIPE_X & 2) return;
+#endif
         if (threadIdx.x == 0) {
             const int target = (int)(pp.item_blocks + pp.huser_blocks);
             uint32_t spins = 0;
@@ -1647,6 +1642,9 @@ __global__ __launch_bounds__(kBlock) void mf_pipe_kernel(ApplyArgs a, PairsArgs 
             }
         }
         __syncthreads();
+#ifdef RG_PIPE_X
+        if (RG_PIPE_X & 1) return;
+#endif
         pairs_body<L, kFused, NMAX, true>(pa, pb);
         return;
         } else {
@@ -1657,7 +1655,10 @@ __global__ __launch_bounds__(kBlock) void mf_pipe_kernel(ApplyArgs a, PairsArgs 
         valid = u < U && pp.counts_next[u] <= 0;
         row = valid ? u : 0;
     }
-    if (__any(valid)) pipe_rows<L>(a, row, valid, sub);
+    if (__any(valid)) {
+        if (hot) pipe_rows<L, true>(a, row, valid, sub);   // read by the pair pass: write-through
+        else pipe_rows<L, false>(a, row, valid, sub);
+    }
     if (hot) {   // publish: every wave's write-through stores done, then one add for the workgroup
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2335,6 +2336,12 @@ extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work
                                const rg_mf_loss_t *loss, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w,
                                const rg_mf_batch_t *next, const rg_mf_work_t *next_w, const rg_mf_pipe_t *pipe,
                                const rg_mt_gen_t *gen) {
+#if !RG_AB
+    (void)stream; (void)t; (void)w; (void)opt; (void)loss; (void)pair_b; (void)pair_w; (void)next; (void)next_w;
+    (void)pipe; (void)gen;
+    // measured 4x slower than the split step: carried by the A/B build only
+    return fail_arg("rg_mf_pipe_step: the pipelined step is an A/B build (build.py --variant NAME -DRG_AB=1)");
+#else
     if (kPairBlock != kBlock) return fail_arg("rg_mf_pipe_step: built with a pair-pass workgroup != 256 threads");
     if (!pipe || !pipe->hot_users || !pipe->nhot || !pipe->counts_next || !pipe->gate || !pipe->gate_next ||
         !pipe->nhot_free || !pipe->err)
@@ -2343,6 +2350,8 @@ extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work
     if (pair_b->loss != RG_LOSS_POINTWISE && pair_b->loss != RG_LOSS_BPR && pair_b->loss != RG_LOSS_HINGE)
         return fail_arg("rg_mf_pipe_step: pointwise, bpr or hinge only (the adaptive hinge needs the max first)");
     if (pair_w->claim_num_users <= 0) return fail_arg("rg_mf_pipe_step: the paired step must carry claimed slots");
+    if ((t->num_users > t->num_items ? t->num_users : t->num_items) * (int64_t)t->dim * 4 >= ((int64_t)1 << 31))
+        return fail_arg("rg_mf_pipe_step: tables of 2 GiB or more (32-bit write-through offsets)");
     if (pair_w->row_list == w->row_list || pair_w->hot_grad == w->hot_grad || pair_w->loss_partials == w->loss_partials ||
         (w->part_row && pair_w->part_row == w->part_row))
         return fail_arg("rg_mf_pipe_step: the paired step's scratch must not alias this step's");
@@ -2382,6 +2391,7 @@ extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work
     PipeLaunchF f{&a, &pa, &prep, prep_out, pp, g, pair_b->cols, (int64_t)(1 + pair_b->n_neg) * pair_b->cols,
                   (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
+#endif
 }
 
 extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,

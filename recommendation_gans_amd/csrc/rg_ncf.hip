@@ -1,7 +1,8 @@
 // NCF MLP training step on gfx950 (spotlight/dnn_models/mlp.py:5-46 trained by
 // implicit.py:347-364; layers [2E, E, ..., 8] -> 1 as ncf_spotlight.py:53-56).
 //
-// One workgroup (4 waves) walks tiles of kRows = 32 examples; a tile holds whole
+// One workgroup (4 waves) walks tiles of kRows = 32 examples (the E = 64 MLP's wave kernel:
+// 48, ncfw::kR); a tile holds whole
 // columns (a positive and its n negatives, pairs prepared by rg_mf_prepare), so
 // pairwise losses are resolved inside the tile.  Everything of a tile lives in
 // LDS: the MLP parameters (loaded once per workgroup), the activations of every
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
 
 // adaptive hinge from forward-only scores: dp of every row (positives: hinge
 // against the max negative; the argmax negative: minus the sum over active positives)
-__global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, float *dp, int64_t rows, int tc,
+__global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, float *dp, int64_t rows, int TR, int tc,
                                                           int NP, int64_t n_pos_cols, int64_t cols, float n_a,
                                                           float *loss_partial) {
     __shared__ float smax[256];
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
     float best = -1.0f;
     int64_t bi = -1;
     for (int64_t r = tid; r < rows; r += 256) {
-        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t tile = r / TR, rr = r % TR;
         const int q = (int)(rr / tc);
         const int64_t s = tile * tc + rr % tc;
         dp[r] = 0.0f;
@@ -798,7 +799,7 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
     const float mx = smax[0];
     float cnt = 0.0f, ls = 0.0f;
     for (int64_t r = tid; r < rows; r += 256) {
-        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t tile = r / TR, rr = r % TR;
         const int64_t s = tile * tc + rr % tc;
         if (rr / tc == 0 && rr < (int64_t)tc && s < n_pos_cols) {
             const float x = (mx - scores[r]) + 1.0f;
@@ -819,49 +820,68 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
 }
 
 // ============================================================================================
-// E = 64 tower (C3, mf_dim = 0): one WAVE per 32-row tile, activations in registers.
+// E = 64 tower (C3, mf_dim = 0): one WAVE per 48-row tile (8 whole columns of 1 + 5 rows at
+// n = 5: 1,024 tiles at B = 8192, one per wave of the 256 x 4-wave grid, no second round).
 //
 // The tile kernel above keeps every activation in LDS and spreads a tile's MFMA tiles over 8
 // waves: ~12 workgroup barriers and an LDS -> MFMA -> LDS round trip per layer, 14 % of the
-// fp32 MFMA peak.  Here a wave owns a whole tile (the same 32 rows, so scores / dp / contrib
-// / list entries / plan partials keep their layouts) and runs the chain with no barrier:
+// fp32 MFMA peak.  Here a wave owns a whole tile and runs the chain with no barrier:
 //
 //   * "T layout": a 16x16 MFMA C tile of a layer's output transposed, Y^T[feature][example]
-//     -- lane (g, j) holds features 16t + 4g + r (r = 0..3) of example j.  Fed back as the
-//     B operand of the next product, k-step r of tile t takes feature 16t + 4g + r from lane
-//     group g, so  Y_{k+1}^T = W_{k+1} Y_k^T  and  dA_k^T = W_k^T delta_k^T  consume the
-//     previous result straight from registers (the A operand, a weight, is read from LDS in
-//     the same permuted k order: one ds_read_b128 per 4 k-steps forward).
+//     -- lane (g, j) holds features 16t + 4g + r (r = 0..3) of example 16 nb + j (3 example
+//     blocks nb).  Fed back as the B operand of the next product, k-step r of tile t takes
+//     feature 16t + 4g + r from lane group g, so  Y_{k+1}^T = W_{k+1} Y_k^T  and
+//     dA_k^T = W_k^T delta_k^T  consume the previous result straight from registers (the A
+//     operand, a weight, is read from LDS in the same permuted k order).
+//   * the forward runs the three example blocks together; the backward one block at a time
+//     (a third of the deltas live), each weight-gradient accumulator still taking the tile's
+//     examples in row order (block 0's k-steps, then block 1's, ...).
 //   * the weight gradients dW_k = sum_e delta_k[e] X_k[e]^T contract over EXAMPLES, which the
-//     T layout keeps on lanes; X_k and delta_k are staged once into the wave's own LDS rows
-//     ([example][feature], float4 stores) and read back with examples on the k axis.  X_0 (the
-//     gathered embeddings) is re-read from L2 in that layout, issued at the start of the
-//     backward.  The wave accumulates dW in MFMA accumulators across its tiles; bias
-//     gradients are per-lane sums of the T-layout deltas.
-//   * one workgroup of 4 waves per CU (135 KB of LDS, 512 registers per lane); at the end the
+//     T layout keeps on lanes; X_k and delta_k are staged into the wave's own LDS rows
+//     ([example][feature], unpadded with a rotated column order: conflict-free both ways) and
+//     read back with examples on the k axis.  X_0 (the gathered embeddings) is re-read from L2
+//     in that layout.  dW accumulates in MFMA accumulators across the wave's tiles; the hidden
+//     biases' gradients are per-lane column sums taken from the same reads (no ones operand).
+//   * one workgroup of 4 waves per CU (151 KB of LDS, 512 registers per lane); at the end the
 //     4 waves' gradients are summed in wave order in LDS into the workgroup's partial.
 // Every sum is a fixed-order f32 chain (MFMA = k-ordered fmaf chain), so results are
 // deterministic; the order differs from the tile kernel's, so the two agree to fp32 rounding.
 // ============================================================================================
 namespace ncfw {
-constexpr int kWaves = 4, kThreads = 64 * kWaves, kR = kRows;   // 32 rows = 2 example blocks of 16
+constexpr int kWaves = 4, kThreads = 64 * kWaves;
+#ifndef RG_NCF_WAVE_ROWS
+#define RG_NCF_WAVE_ROWS 32   // 48 (8 whole columns, one tile per wave) measured 4 % slower per step
+#endif
+constexpr int kR = RG_NCF_WAVE_ROWS, NB = kR / 16;   // 48 rows = 3 example blocks of 16 (n = 5: 8 whole columns)
 // weights in LDS (floats): W_k row-major [out][in + 4] (b128 rows land on distinct 16-B slots),
 // W4 and the output row padded to 16 rows of zeros, biases padded with zeros
 constexpr int S1 = 132, S2 = 68, S3 = 36, S4 = 20, SO = 20;
 constexpr int oW1 = 0, oW2 = oW1 + 64 * S1, oW3 = oW2 + 32 * S2, oW4 = oW3 + 16 * S3, oWo = oW4 + 16 * S4;
 constexpr int oB1 = oWo + 16 * SO, oB2 = oB1 + 64, oB3 = oB2 + 32, oB4 = oB3 + 16, oBo = oB4 + 16;
 constexpr int kWFloats = oBo + 4;
-// per wave: staged activations / deltas [32][stride], stride = 16 mod 64 floats (the
-// example-on-k reads of lane (g, x) hit bank 16g + x), then the tile's small per-row arrays
-constexpr int R1S = 80, R2S = 48, R3S = 16, R4S = 16;
+// per wave: staged activations / deltas [48][F] (F = 64, 32, 16, 16 features, unpadded: the
+// column of row r is rotated by 16 (r & 3) for F = 64 and by 16 ((r >> 1) & 1) for F = 32, so the
+// example-on-k reads of lane (g, x) -- row 4 s + g, column 16 t + x -- hit 64 distinct banks),
+// then the tile's small per-row arrays
+constexpr int R1S = 64, R2S = 32, R3S = 16, R4S = 16;
 constexpr int oR1 = 0, oR2 = oR1 + kR * R1S, oR3 = oR2 + kR * R2S, oR4 = oR3 + kR * R3S, oSm = oR4 + kR * R4S;
 constexpr int kSmall = 11;
 constexpr int kWaveFloats = oSm + kSmall * kR;
 constexpr int kLdsFloats = kWFloats + kWaves * kWaveFloats;
 constexpr int P = NcfShape<64>::P;
 static_assert(kLdsFloats <= kLdsMax, "LDS");
-static_assert(16 * 64 <= kR * R2S, "planned item halves fit the delta2 rows");
+static_assert((kR / 2) * 64 <= kR * R2S, "planned item halves ([tc <= kR / 2][64]) fit the delta2 rows");
 static_assert(kWFloats % 4 == 0 && kWaveFloats % 4 == 0, "16-B alignment");
+static_assert(kR <= 64 && kR % 16 == 0, "one lane per row, whole example blocks");
+
+// float index of (row, column) in a staged [kR][RS] buffer (column a multiple of 4 for float4
+// accesses stays inside its 16-column group)
+template <int RS>
+__device__ __forceinline__ int at(int row, int col) {
+    if constexpr (RS == 64) return row * 64 + ((col + 16 * (row & 3)) & 63);
+    else if constexpr (RS == 32) return row * 32 + ((col + 16 * ((row >> 1) & 1)) & 31);
+    else return row * RS + col;
+}
 
 // orders this wave's LDS traffic for the compiler: DS instructions of one wave execute in
 // order, so a wavefront-scope fence (no wait instruction) is all a cross-lane LDS hand-off
@@ -872,9 +892,11 @@ __device__ __forceinline__ v4f mfma(float a, float b, v4f c) { return __builtin_
 
 // Y^T (TO tiles) = W X^T: W [16 TO][16 TI] (row stride S), X^T T-layout (TI tiles)
 template <int TI, int TO>
-__device__ __forceinline__ void fwd(const v4f (&x)[TI][2], v4f (&y)[TO][2], const float *W, int S, int g, int m) {
+__device__ __forceinline__ void fwd(const v4f (&x)[TI][NB], v4f (&y)[TO][NB], const float *W, int S, int g, int m) {
 #pragma unroll
-    for (int t = 0; t < TO; ++t) y[t][0] = y[t][1] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < TO; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) y[t][nb] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int ti = 0; ti < TI; ++ti) {
         v4f a[TO];
@@ -885,16 +907,18 @@ __device__ __forceinline__ void fwd(const v4f (&x)[TI][2], v4f (&y)[TO][2], cons
 #pragma unroll
             for (int t = 0; t < TO; ++t)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) y[t][nb] = mfma(a[t][r], x[ti][nb][r], y[t][nb]);
+                for (int nb = 0; nb < NB; ++nb) y[t][nb] = mfma(a[t][r], x[ti][nb][r], y[t][nb]);
     }
 }
 
 // dA^T (TI tiles) = W^T delta^T: W [16 TO][16 TI] row-major (stride S), delta^T T-layout (TO
 // tiles); W may point at a column block of a wider matrix (its first of TI column tiles)
 template <int TI, int TO>
-__device__ __forceinline__ void bwd(const v4f (&d)[TO][2], v4f (&da)[TI][2], const float *W, int S, int g, int x) {
+__device__ __forceinline__ void bwd(const v4f (&d)[TO][NB], v4f (&da)[TI][NB], const float *W, int S, int g, int x) {
 #pragma unroll
-    for (int t = 0; t < TI; ++t) da[t][0] = da[t][1] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < TI; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) da[t][nb] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int to = 0; to < TO; ++to)
 #pragma unroll
@@ -905,47 +929,48 @@ __device__ __forceinline__ void bwd(const v4f (&d)[TO][2], v4f (&da)[TI][2], con
 #pragma unroll
             for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) da[ti][nb] = mfma(a[ti], d[to][nb][r], da[ti][nb]);
+                for (int nb = 0; nb < NB; ++nb) da[ti][nb] = mfma(a[ti], d[to][nb][r], da[ti][nb]);
         }
 }
 
-// dW[16 TOo][16 TIi] += sum_e D[e][o] X[e][i] over the tile's 32 examples (staged rows), and the
-// bias gradient sum_e D[e][o] as the same product with a ones operand (every column of gb)
-template <int TOo, int TIi>
-__device__ __forceinline__ void dw(v4f (&acc)[TOo][TIi], v4f (&gb)[TOo], const float *D, int SD, const float *X,
-                                   int SX, int g, int x) {
+// dW[16 TOo][16 TIi] += sum_e D[e][o] X[e][i] over the tile's examples (staged rows), and this
+// lane's share of the bias gradient sum_e D[e][o]: the examples e = g (mod 4) of column 16 to + x,
+// summed in the same pass over the D operand (the four lane groups are added at the end)
+template <int TOo, int TIi, int SD, int SX>
+__device__ __forceinline__ void dw(v4f (&acc)[TOo][TIi], float (&bs)[TOo], const float *D, const float *X, int g,
+                                   int x) {
 #pragma unroll
     for (int s = 0; s < kR / 4; ++s) {
         float a[TOo], b[TIi];
 #pragma unroll
-        for (int to = 0; to < TOo; ++to) a[to] = D[(4 * s + g) * SD + 16 * to + x];
+        for (int to = 0; to < TOo; ++to) a[to] = D[at<SD>(4 * s + g, 16 * to + x)];
 #pragma unroll
-        for (int ti = 0; ti < TIi; ++ti) b[ti] = X[(4 * s + g) * SX + 16 * ti + x];
+        for (int ti = 0; ti < TIi; ++ti) b[ti] = X[at<SX>(4 * s + g, 16 * ti + x)];
 #pragma unroll
         for (int to = 0; to < TOo; ++to) {
 #pragma unroll
             for (int ti = 0; ti < TIi; ++ti) acc[to][ti] = mfma(a[to], b[ti], acc[to][ti]);
-            gb[to] = mfma(a[to], 1.0f, gb[to]);
+            bs[to] += a[to];
         }
     }
 }
 
 // staged rows -> T-layout tiles (the inverse of stage)
-template <int T>
-__device__ __forceinline__ void unstage(v4f (&y)[T][2], const float *R, int RS, int g, int j) {
+template <int T, int RS>
+__device__ __forceinline__ void unstage(v4f (&y)[T][NB], const float *R, int g, int j) {
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) y[t][nb] = *reinterpret_cast<const v4f *>(R + (nb * 16 + j) * RS + 16 * t + 4 * g);
+        for (int nb = 0; nb < NB; ++nb) y[t][nb] = *reinterpret_cast<const v4f *>(R + at<RS>(nb * 16 + j, 16 * t + 4 * g));
 }
 
 // T-layout tiles -> staged rows [example][feature] (float4 per lane)
-template <int T>
-__device__ __forceinline__ void stage(const v4f (&y)[T][2], float *R, int RS, int g, int j) {
+template <int T, int RS>
+__device__ __forceinline__ void stage(const v4f (&y)[T][NB], float *R, int g, int j) {
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<v4f *>(R + (nb * 16 + j) * RS + 16 * t + 4 * g) = y[t][nb];
+        for (int nb = 0; nb < NB; ++nb) *reinterpret_cast<v4f *>(R + at<RS>(nb * 16 + j, 16 * t + 4 * g)) = y[t][nb];
 }
 
 // torch's LeakyReLU(0.1) -> Dropout(0.5) multiplier from the kept bit and the sign of the
@@ -954,6 +979,57 @@ __device__ __forceinline__ float mult(float y, bool keep, bool training) {
     const float m1 = y > 0.0f ? 1.0f : 0.1f;
     return training ? (keep ? 2.0f * m1 : 0.0f) : m1;
 }
+
+// ---- one example block (16 examples, lane j = example 16 nb + j): the backward runs block by
+// block so a third of the tile's activations / deltas is live at a time ----
+// dA^T (TI tiles) = W^T delta^T for one block
+template <int TI, int TO>
+__device__ __forceinline__ void bwd1(const v4f (&d)[TO], v4f (&da)[TI], const float *W, int S, int g, int x) {
+#pragma unroll
+    for (int t = 0; t < TI; ++t) da[t] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int to = 0; to < TO; ++to)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a[TI];
+#pragma unroll
+            for (int ti = 0; ti < TI; ++ti) a[ti] = W[(16 * to + 4 * g + r) * S + 16 * ti + x];
+#pragma unroll
+            for (int ti = 0; ti < TI; ++ti) da[ti] = mfma(a[ti], d[to][r], da[ti]);
+        }
+}
+// dW += the block's examples (k-steps s0 .. s0 + 3 of the tile: rows 4 s + g), bias column sums
+template <int TOo, int TIi, int SD, int SX>
+__device__ __forceinline__ void dw1b(v4f (&acc)[TOo][TIi], float (&bs)[TOo], const float *D, const float *X, int g,
+                                     int x, int s0) {
+#pragma unroll
+    for (int s = s0; s < s0 + 4; ++s) {
+        float a[TOo], b[TIi];
+#pragma unroll
+        for (int to = 0; to < TOo; ++to) a[to] = D[at<SD>(4 * s + g, 16 * to + x)];
+#pragma unroll
+        for (int ti = 0; ti < TIi; ++ti) b[ti] = X[at<SX>(4 * s + g, 16 * ti + x)];
+#pragma unroll
+        for (int to = 0; to < TOo; ++to) {
+#pragma unroll
+            for (int ti = 0; ti < TIi; ++ti) acc[to][ti] = mfma(a[to], b[ti], acc[to][ti]);
+            bs[to] += a[to];
+        }
+    }
+}
+template <int T, int RS>
+__device__ __forceinline__ void unstage1(v4f (&y)[T], const float *R, int row, int g) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) y[t] = *reinterpret_cast<const v4f *>(R + at<RS>(row, 16 * t + 4 * g));
+}
+template <int T, int RS>
+__device__ __forceinline__ void stage1(const v4f (&y)[T], float *R, int row, int g) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) *reinterpret_cast<v4f *>(R + at<RS>(row, 16 * t + 4 * g)) = y[t];
+}
+
+// bit of unit (t, nb, r) of a layer in its keep word
+__device__ __forceinline__ constexpr int kbit(int t, int nb, int r) { return (t * NB + nb) * 4 + r; }
 }  // namespace ncfw
 
 // Diagnostic build only: per-wave phase stamps of its first two tiles (16 slots per tile),
@@ -1045,49 +1121,27 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             wvt[k] = src < 0 ? 0.0f : v;
         }
     }
-    auto store_weights = [&]() {
-#pragma unroll
-        for (int k = 0; k < PT1; ++k) {
-            const int e = tid + k * kThreads;
-            *reinterpret_cast<float4 *>(sw + oW1 + (e / 32) * S1 + (e % 32) * 4) = wv1[k];
-        }
-#pragma unroll
-        for (int k = 0; k < PT2; ++k) {
-            const int e = tid + k * kThreads;
-            *reinterpret_cast<float4 *>(sw + oW2 + (e / 16) * S2 + (e % 16) * 4) = wv2[k];
-        }
-#pragma unroll
-        for (int k = 0; k < PT3; ++k) {
-            const int e = tid + k * kThreads;
-            if (e < 16 * 32 / 4) *reinterpret_cast<float4 *>(sw + oW3 + (e / 8) * S3 + (e % 8) * 4) = wv3[k];
-        }
-#pragma unroll
-        for (int k = 0; k < PTT; ++k)
-            if (tid + k * kThreads < kTail) sw[oW4 + tid + k * kThreads] = wvt[k];
-    };
     const float *W1s = sw + oW1, *W2s = sw + oW2, *W3s = sw + oW3, *W4s = sw + oW4, *Wos = sw + oWo;
     const bool training = a.training != 0;
     const int n = a.n_neg, NP = n + 1, tc = a.tc;
     constexpr int units = S64::mask_units();
     const bool pairwise = a.loss == RG_LOSS_BPR || a.loss == RG_LOSS_HINGE;
 
-    // running gradients of this wave, all MFMA accumulators: weight tiles, bias tiles (every
-    // column holds the bias sum) and the output layer's [w_out | b_out] tile
-    v4f gW1[4][8], gW2[2][4], gW3[1][2], gW4[1][1], gB1[4], gB2[2], gB3[1], gB4[1], gO;
+    // running gradients of this wave: the weight tiles and the output layer's [w_out | b_out]
+    // tile in MFMA accumulators, the hidden biases as per-lane column sums (lane (g, x): the
+    // examples e = g mod 4 of feature 16 t + x)
+    v4f gW1[4][8], gW2[2][4], gW3[1][2], gW4[1][1], gO;
+    float bB1[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bB2[2] = {0.0f, 0.0f}, bB3[1] = {0.0f}, bB4[1] = {0.0f};
     const v4f z4 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int q = 0; q < 8; ++q) gW1[p][q] = z4;
-        gB1[p] = z4;
-    }
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int q = 0; q < 4; ++q) gW2[p][q] = z4;
-        gB2[p] = z4;
-    }
-    gW3[0][0] = gW3[0][1] = gW4[0][0] = gB3[0] = gB4[0] = gO = z4;
+    gW3[0][0] = gW3[0][1] = gW4[0][0] = gO = z4;
 
     // a column's pair record for row r = q * tc + cl of `tile` (lanes 0..31): the loads are
     // issued unconditionally from clamped indices (fetch) and resolved when the values are
@@ -1132,8 +1186,8 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     RowRaw nxt{};   // the next tile's record (lanes 0..31), in flight during this tile
     if (lane < kR) nxt = fetch_row(first, lane);
     // a tile's start: its record resolved into the wave's row arrays, the gather of X0 issued
-    auto begin_tile = [&](int tcl, int &ru, int &ri, int &rps, int (&ue)[2], int (&ie)[2], int (&re)[2],
-                          uint32_t (&ke)[2], v4f (&x0)[8][2]) {
+    auto begin_tile = [&](int tcl, int &ru, int &ri, int &rps, int (&ue)[NB], int (&ie)[NB], int (&re)[NB],
+                          uint32_t (&ke)[NB], v4f (&x0)[8][NB]) {
         int64_t ngj = 0;
         if (lane < kR) {
             finish_row(nxt, ru, ri, rps, ngj);
@@ -1147,7 +1201,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         }
         wave_sync();
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
+        for (int nb = 0; nb < NB; ++nb) {
             ue[nb] = sU[nb * 16 + j];
             ie[nb] = sI[nb * 16 + j];
             re[nb] = sR[nb * 16 + j];
@@ -1157,14 +1211,33 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         // that is not a valid pair reads row 0 (its dz is 0, so none of its values reach a
         // gradient, and its score is never used) ----
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
+        for (int nb = 0; nb < NB; ++nb) {
             const float *pu = a.user_w + (int64_t)(ue[nb] >= 0 ? ue[nb] : 0) * 64 + 4 * g;
             const float *pi = a.item_w + (int64_t)(ue[nb] >= 0 ? ie[nb] : 0) * 64 + 4 * g;
 #pragma unroll
             for (int t = 0; t < 8; ++t) x0[t][nb] = *reinterpret_cast<const v4f *>(t < 4 ? pu + 16 * t : pi + 16 * (t - 4));
         }
     };
-    store_weights();   // (the first record's loads above are in flight meanwhile)
+    // the weights into LDS (the first record's loads above are in flight meanwhile; inline, not
+    // a lambda: a captured register array would live in scratch)
+#pragma unroll
+    for (int k = 0; k < PT1; ++k) {
+        const int e = tid + k * kThreads;
+        *reinterpret_cast<float4 *>(sw + oW1 + (e / 32) * S1 + (e % 32) * 4) = wv1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PT2; ++k) {
+        const int e = tid + k * kThreads;
+        *reinterpret_cast<float4 *>(sw + oW2 + (e / 16) * S2 + (e % 16) * 4) = wv2[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PT3; ++k) {
+        const int e = tid + k * kThreads;
+        if (e < 16 * 32 / 4) *reinterpret_cast<float4 *>(sw + oW3 + (e / 8) * S3 + (e % 8) * 4) = wv3[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PTT; ++k)
+        if (tid + k * kThreads < kTail) sw[oW4 + tid + k * kThreads] = wvt[k];
     __syncthreads();
     float warm = 0.0f;   // the next tile's embedding lines, touched during this tile's backward
     for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
@@ -1173,22 +1246,22 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         const int tl_ = (int)((tile - first) / waves_total);
         (void)tl_;
         WS(0);
-        int ru = -1, ri = -1, rps = -1, ue[2], ie[2], re[2];
-        uint32_t ke[2];
-        v4f x0[8][2];
+        int ru = -1, ri = -1, rps = -1, ue[NB], ie[NB], re[NB];
+        uint32_t ke[NB];
+        v4f x0[8][NB];
         begin_tile(tc, ru, ri, rps, ue, ie, re, ke, x0);
         if (warm == 1.0e30f && a.n_pos < 0) a.scores[0] = warm;   // keeps the warm-up loads (never taken)
         WS(1);
         // dropout bits of every unit of the tile, computed while the gather is in flight
-        // (bit (t * 2 + nb) * 4 + r of a layer's word: feature 16 t + 4 g + r, example nb * 16 + j)
-        auto keep_bits = [&](auto tc_, int out, int mask_base) -> uint32_t {
+        // (bit kbit(t, nb, r) of a layer's word: feature 16 t + 4 g + r, example nb * 16 + j)
+        auto keep_bits = [&](auto tc_, int out, int mask_base) -> uint64_t {
             constexpr int T = decltype(tc_)::value;
-            uint32_t keep = 0;
+            uint64_t keep = 0;
             if (!training) return keep;
             if (a.mask_pos) {   // recorded masks (parity tests): every byte load first
-                uint8_t mv[T][2][4];
+                uint8_t mv[T][NB][4];
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
+                for (int nb = 0; nb < NB; ++nb) {
                     const uint8_t *mk = (nb * 16 + j < tc ? a.mask_pos : a.mask_neg) +
                                         (int64_t)(ue[nb] >= 0 ? re[nb] : 0) * units + mask_base;
 #pragma unroll
@@ -1199,29 +1272,32 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                 for (int t = 0; t < T; ++t)
 #pragma unroll
-                    for (int nb = 0; nb < 2; ++nb)
+                    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            keep |= (uint32_t)(mv[t][nb][r] != 0 && ue[nb] >= 0 && 16 * t + 4 * g + r < out)
-                                    << ((t * 2 + nb) * 4 + r);
+                            keep |= (uint64_t)(mv[t][nb][r] != 0 && ue[nb] >= 0 && 16 * t + 4 * g + r < out)
+                                    << kbit(t, nb, r);
             } else {
 #pragma unroll
                 for (int t = 0; t < T; ++t)
 #pragma unroll
-                    for (int nb = 0; nb < 2; ++nb)
+                    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int f = 16 * t + 4 * g + r;
                             const uint32_t h = mix32(ke[nb] + (uint32_t)(mask_base + f) * 0x85EBCA6BU);
-                            keep |= (((h >> 7) & 1U) & (uint32_t)(f < out)) << ((t * 2 + nb) * 4 + r);
+                            keep |= (uint64_t)(((h >> 7) & 1U) & (uint32_t)(f < out)) << kbit(t, nb, r);
                         }
             }
             return keep;
         };
-        const uint64_t kb = (uint64_t)keep_bits(std::integral_constant<int, 4>{}, 64, S64::mask_off(0)) |
-                            (uint64_t)keep_bits(std::integral_constant<int, 2>{}, 32, S64::mask_off(1)) << 32 |
-                            (uint64_t)keep_bits(std::integral_constant<int, 1>{}, 16, S64::mask_off(2)) << 48 |
-                            (uint64_t)keep_bits(std::integral_constant<int, 1>{}, 8, S64::mask_off(3)) << 56;
+        // layer 1 (4 x NB x 4 = 48 bits) in kb1; layers 2, 3, 4 (24 + 12 + 12 bits) in kb2
+        const uint64_t kb1 = keep_bits(std::integral_constant<int, 4>{}, 64, S64::mask_off(0));
+        const uint64_t kb2 = keep_bits(std::integral_constant<int, 2>{}, 32, S64::mask_off(1)) |
+                             keep_bits(std::integral_constant<int, 1>{}, 16, S64::mask_off(2)) << 24 |
+                             keep_bits(std::integral_constant<int, 1>{}, 8, S64::mask_off(3)) << 36;
+        static_assert(kbit(3, NB - 1, 3) < 64 && kbit(1, NB - 1, 3) + 1 + 2 * (kbit(0, NB - 1, 3) + 1) <= 64,
+                      "keep words");
         // list slots claimed behind the gather (their round trip overlaps it and the first layer;
         // the entries are written after it)
         int lu = -1, li = -1;
@@ -1232,7 +1308,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         WS(2);
         // ---- forward ----
         // bias, LeakyReLU(0.1), Dropout(0.5) as one multiplier per unit
-        auto activate = [&](auto &y, const float *b, int bit0) {
+        auto activate = [&](auto &y, const float *b, uint64_t kw, int bit0) {
             constexpr int T = sizeof(y) / sizeof(y[0]);
             v4f bv[T];
 #pragma unroll
@@ -1240,39 +1316,43 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
             for (int t = 0; t < T; ++t)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb)
+                for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float z = y[t][nb][r] + bv[t][r];
                         const float m1 = z > 0.0f ? 1.0f : 0.1f;
-                        const float m = training ? (((kb >> (bit0 + (t * 2 + nb) * 4 + r)) & 1U) ? 2.0f * m1 : 0.0f) : m1;
+                        const float m = training ? (((kw >> (bit0 + kbit(t, nb, r))) & 1U) ? 2.0f * m1 : 0.0f) : m1;
                         y[t][nb][r] = z * m;
                     }
         };
-        v4f y1[4][2], y2[2][2], y3[1][2], y4[1][2];
+        v4f y1[4][NB], y2[2][NB], y3[1][NB], y4[1][NB];
         fwd<8, 4>(x0, y1, W1s, S1, g, j);
         WS(3);
-        activate(y1, sw + oB1, 0);
-        stage<4>(y1, R1, R1S, g, j);
+        activate(y1, sw + oB1, kb1, 0);
+        stage<4, R1S>(y1, R1, g, j);
         fwd<4, 2>(y1, y2, W2s, S2, g, j);
-        activate(y2, sw + oB2, 32);
-        stage<2>(y2, R2, R2S, g, j);
+        activate(y2, sw + oB2, kb2, 0);
+        stage<2, R2S>(y2, R2, g, j);
         fwd<2, 1>(y2, y3, W3s, S3, g, j);
-        activate(y3, sw + oB3, 48);
-        stage<1>(y3, R3, R3S, g, j);
+        activate(y3, sw + oB3, kb2, 24);
+        stage<1, R3S>(y3, R3, g, j);
         fwd<1, 1>(y3, y4, W4s, S4, g, j);
-        activate(y4, sw + oB4, 56);
+        activate(y4, sw + oB4, kb2, 36);
         if (kBackward) {   // A_4 rows with a ones feature (8) for the output layer's bias gradient
-            v4f y4s[1][2] = {{y4[0][0], y4[0][1]}};
-            if (g == 2) y4s[0][0][0] = y4s[0][1][0] = 1.0f;
-            stage<1>(y4s, R4, R4S, g, j);
+            v4f y4s[1][NB];
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+                y4s[0][nb] = y4[0][nb];
+                if (g == 2) y4s[0][nb][0] = 1.0f;
+            }
+            stage<1, R4S>(y4s, R4, g, j);
         }
-        v4f zo[1][2];
+        v4f zo[1][NB];
         fwd<1, 1>(y4, zo, Wos, SO, g, j);
         if (g == 0) {
             const float bo = sw[oBo];
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
+            for (int nb = 0; nb < NB; ++nb) {
                 const float p = sigmoidf_ref(zo[0][nb][0] + bo);
                 sP[nb * 16 + j] = p;
                 if (PHASE == kNcfScores) a.scores[tile * kR + nb * 16 + j] = ue[nb] >= 0 ? p : 0.0f;
@@ -1363,15 +1443,16 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         }
         wave_sync();
         if (lane == 0) {   // column order, as the one-thread loop summed them
-            float va[16], vb[16];
+            constexpr int CM = kR / 2;   // columns per tile at most (n >= 1)
+            float va[CM], vb[CM];
 #pragma unroll
-            for (int cl = 0; cl < 16; ++cl) {
+            for (int cl = 0; cl < CM; ++cl) {
                 va[cl] = cl < tc ? sLa[cl] : 0.0f;
                 vb[cl] = cl < tc ? sLb[cl] : 0.0f;
             }
             float la = 0.0f, lb = 0.0f;
 #pragma unroll
-            for (int cl = 0; cl < 16; ++cl)
+            for (int cl = 0; cl < CM; ++cl)
                 if (cl < tc) { la += va[cl]; lb += vb[cl]; }
             a.loss_partials[2 * tile] = la;
             a.loss_partials[2 * tile + 1] = lb;
@@ -1384,138 +1465,120 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             warm += (pu[0] + pu[32]) + (pi[0] + pi[32]);
         }
         WS(5);
-        // ---- backward ----
-        float dz[2];
+        // ---- backward, one example block at a time (lane j: example 16 nb + j).  Every weight-
+        // gradient accumulator still takes the tile's examples in row order (block 0's k-steps,
+        // then block 1's, ...), so the sums are those of one pass over the tile ----
+        auto mult4 = [&](v4f &d, const v4f &y, uint64_t kw, int bit) {
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) dz[nb] = sDz[nb * 16 + j];
-        // output layer: [dW_out | db_out] += sum_e [A_4 | 1][e] dz[e]; delta_4 = (dz w_out) m_4
+            for (int r = 0; r < 4; ++r) d[r] = d[r] * mult(y[r], (kw >> (bit + r)) & 1, training);
+        };
+        WS(6);
+#pragma unroll 1
+        for (int nb = 0; nb < NB; ++nb) {
+            const int row = nb * 16 + j, s0 = 4 * nb;
+            // X0 of the block with examples on the k axis for dW1 (lane (g, x): X0[4 s + g][16 t + x],
+            // user columns t < 4, item columns t >= 4), re-read from L2 now for use after three
+            // layers; rows that are not valid pairs read row 0 (their delta is 0)
+            float xn[4][8];
 #pragma unroll
-        for (int s = 0; s < kR / 4; ++s) gO = mfma(R4[(4 * s + g) * R4S + j], sDz[4 * s + g], gO);
-        v4f d4[1][2];
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int e = 4 * (s0 + s2) + g, u = sU[e], i = sI[e];
+                const float *pu = a.user_w + (int64_t)(u >= 0 ? u : 0) * 64 + j;
+                const float *pi = a.item_w + (int64_t)(u >= 0 ? i : 0) * 64 + j;
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+                for (int t = 0; t < 4; ++t) {
+                    xn[s2][t] = pu[16 * t];
+                    xn[s2][4 + t] = pi[16 * t];
+                }
+            }
+            const float dzb = sDz[row];
+            // output layer: [dW_out | db_out] += sum_e [A_4 | 1][e] dz[e]; delta_4 = (dz w_out) m_4
+            // (A_4's feature 8 is the ones column: its output weight is 0, so its delta is too)
+#pragma unroll
+            for (int s = s0; s < s0 + 4; ++s) gO = mfma(R4[(4 * s + g) * R4S + j], sDz[4 * s + g], gO);
+            v4f y4b[1], d4b[1], y3b[1], d3b[1];
+            unstage1<1, R4S>(y4b, R4, row, g);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                d4[0][nb][r] = (dz[nb] * Wos[4 * g + r]) * mult(y4[0][nb][r], (kb >> (56 + nb * 4 + r)) & 1, training);
-        auto apply_mult = [&](auto &da, const auto &y, int bit0) {
-            constexpr int T = sizeof(da) / sizeof(da[0]);
+                d4b[0][r] = (dzb * Wos[4 * g + r]) * mult(y4b[0][r], (kb2 >> (36 + kbit(0, nb, r))) & 1, training);
+            unstage1<1, R3S>(y3b, R3, row, g);                  // A_3 back from its staged rows
+            bwd1<1, 1>(d4b, d3b, W4s, S4, g, j);
+            mult4(d3b[0], y3b[0], kb2, 24 + kbit(0, nb, 0));
+            wave_sync();                                        // A_4 reads done before delta_4 lands there
+            stage1<1, R4S>(d4b, R4, row, g);
+            wave_sync();
+            dw1b<1, 1, R4S, R3S>(gW4, bB4, R4, R3, g, j, s0);   // dW4 += delta4^T A_3
+            v4f y2b[2], d2b[2];
+            unstage1<2, R2S>(y2b, R2, row, g);
+            bwd1<2, 1>(d3b, d2b, W3s, S3, g, j);
 #pragma unroll
-            for (int t = 0; t < T; ++t)
+            for (int t = 0; t < 2; ++t) mult4(d2b[t], y2b[t], kb2, kbit(t, nb, 0));
+            wave_sync();                                        // A_3 reads done before delta_3 lands there
+            stage1<1, R3S>(d3b, R3, row, g);
+            wave_sync();
+            dw1b<1, 2, R3S, R2S>(gW3, bB3, R3, R2, g, j, s0);
+            v4f y1b[4], d1b[4];
+            unstage1<4, R1S>(y1b, R1, row, g);
+            bwd1<4, 2>(d2b, d1b, W2s, S2, g, j);
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb)
+            for (int t = 0; t < 4; ++t) mult4(d1b[t], y1b[t], kb1, kbit(t, nb, 0));
+            wave_sync();
+            stage1<2, R2S>(d2b, R2, row, g);
+            wave_sync();
+            WS(7);
+            dw1b<2, 4, R2S, R1S>(gW2, bB2, R2, R1, g, j, s0);
+            WS(8);
+            wave_sync();
+            stage1<4, R1S>(d1b, R1, row, g);
+            wave_sync();
+            WS(9);
+            // dW1 += delta1^T X0 (the block's k-steps), db1 alongside
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        da[t][nb][r] = da[t][nb][r] * mult(y[t][nb][r], (kb >> (bit0 + (t * 2 + nb) * 4 + r)) & 1, training);
-        };
-        v4f d3[1][2];
-        bwd<1, 1>(d4, d3, W4s, S4, g, j);
-        wave_sync();                                           // A_4 reads done before delta_4 lands there
-        stage<1>(d4, R4, R4S, g, j);
-        unstage<1>(y3, R3, R3S, g, j);                         // A_3 back from its staged rows
-        apply_mult(d3, y3, 48);
-        wave_sync();
-        dw<1, 1>(gW4, gB4, R4, R4S, R3, R3S, g, j);            // dW4 += delta4^T A_3
-        v4f d2[2][2];
-        bwd<2, 1>(d3, d2, W3s, S3, g, j);
-        wave_sync();                                           // A_3 reads done before delta_3 lands there
-        stage<1>(d3, R3, R3S, g, j);
-        unstage<2>(y2, R2, R2S, g, j);
-        apply_mult(d2, y2, 32);
-        wave_sync();
-        dw<1, 2>(gW3, gB3, R3, R3S, R2, R2S, g, j);
-        WS(6);
-        // X0 with examples on the k axis for dW1 (lane (g, x): X0[4 s + g][16 t + x]), re-read
-        // from L2 in two halves (user columns now, item columns behind the first half of dW1);
-        // rows that are not valid pairs read row 0 (their delta is 0)
-        auto load_xn = [&](float (&xv)[8][4], int h) {
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) {
-                const int e = 4 * s2 + g, u = sU[e], i = sI[e];
-                const float *p = h == 0 ? a.user_w + (int64_t)(u >= 0 ? u : 0) * 64 + j
-                                        : a.item_w + (int64_t)(u >= 0 ? i : 0) * 64 + j;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) xv[s2][t] = p[16 * t];
-            }
-        };
-        float xn[8][4];
-        load_xn(xn, 0);
-        v4f d1[4][2];
-        bwd<4, 2>(d2, d1, W2s, S2, g, j);
-        wave_sync();
-        stage<2>(d2, R2, R2S, g, j);
-        unstage<4>(y1, R1, R1S, g, j);
-        apply_mult(d1, y1, 0);
-        wave_sync();
-        WS(7);
-        dw<2, 4>(gW2, gB2, R2, R2S, R1, R1S, g, j);
-        WS(8);
-        wave_sync();
-        stage<4>(d1, R1, R1S, g, j);
-        wave_sync();
-        WS(9);
-        // dW1 += delta1^T X0 (X0 rows from the registers loaded above), db1 alongside
-        auto dw1_half = [&](int h) {
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) {
+            for (int s2 = 0; s2 < 4; ++s2) {
                 float av[4];
 #pragma unroll
-                for (int to = 0; to < 4; ++to) av[to] = R1[(4 * s2 + g) * R1S + 16 * to + j];
+                for (int to = 0; to < 4; ++to) av[to] = R1[at<R1S>(4 * (s0 + s2) + g, 16 * to + j)];
 #pragma unroll
                 for (int to = 0; to < 4; ++to) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) gW1[to][4 * h + t] = mfma(av[to], xn[s2][t], gW1[to][4 * h + t]);
-                    if (h == 0) gB1[to] = mfma(av[to], 1.0f, gB1[to]);
+                    for (int t = 0; t < 8; ++t) gW1[to][t] = mfma(av[to], xn[s2][t], gW1[to][t]);
+                    bB1[to] += av[to];
                 }
             }
-        };
-        dw1_half(0);
-        load_xn(xn, 1);   // item columns, in flight during the dX0 halves
-        WS(10);
-        // dX0^T = W1^T delta1^T: the per-example input gradient rows, in two halves (user
-        // columns, item columns: 32 accumulators each beside the gradient accumulators), each
-        // stored at once, overflow rows (lists full) in fixed point
+            WS(10);
+            // dX0^T = W1^T delta1^T: the block's input gradient rows, in four quarters of 32
+            // columns (user 0-31, 32-63, item 0-31, 32-63), each stored at once, overflow rows
+            // (lists full) in fixed point
+            const int lu = sLu[row], li = sLi[row], ur = sU[row], ir = sI[row];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            v4f dx[4][2];
-            bwd<4, 4>(d1, dx, W1s + 64 * h, S1, g, j);
-            if (h == 0) WS(11);
+            for (int qq = 0; qq < 4; ++qq) {
+                const int hh = qq >> 1, c0 = 32 * (qq & 1);   // table half, first column in the row
+                v4f dx[2];
+                bwd1<2, 4>(d1b, dx, W1s + 32 * qq, S1, g, j);
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < 2; ++t)
+                    *reinterpret_cast<v4f *>(a.contrib + (tile * kR + row) * (int64_t)128 + 32 * qq + 16 * t + 4 * g) = dx[t];
+                if ((hh == 0 ? lu : li) >= kNcfCap) {
+                    const int64_t orow = hh == 0 ? (int64_t)ur : a.num_users + ir;
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const int e = nb * 16 + j;
-                    *reinterpret_cast<v4f *>(a.contrib + (tile * kR + e) * (int64_t)128 + 64 * h + 16 * t + 4 * g) = dx[t][nb];
-                }
+                    for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const int e = nb * 16 + j;
-                if ((h == 0 ? sLu[e] : sLi[e]) >= kNcfCap) {
-                    const int64_t row = h == 0 ? (int64_t)ue[nb] : a.num_users + ie[nb];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) fix_add(a.hot_grad + row * 64 + 16 * t + 4 * g + r, dx[t][nb][r]);
+                        for (int r = 0; r < 4; ++r) fix_add(a.hot_grad + orow * 64 + c0 + 16 * t + 4 * g + r, dx[t][r]);
                 }
             }
-            if (h == 1 && a.pos_slot != nullptr && j < tc) {
-                // the positives' (rows 0..tc-1, example block 0) item halves into R2 as [16][64]
-                // (delta2 is consumed; R1 still holds delta1 for the second half of dW1)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) *reinterpret_cast<v4f *>(R2 + j * 64 + 16 * t + 4 * g) = dx[t][0];
-            }
+            WS(11);
         }
-        dw1_half(1);
         WS(12);
         if (a.pos_slot != nullptr) {
             // planned positives: lane c runs the segments of equal plan slots in column order (the
-            // same sums as a per-segment loop)
-            wave_sync();
+            // same sums as a per-segment loop) over the positives' item halves just stored
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this wave's contrib stores visible
             float acc = 0.0f;
             int prev = -2;
             for (int cl = 0; cl < tc; ++cl) {
                 const int slot = sPs[cl];
                 if (slot != prev) acc = 0.0f;
-                acc += R2[cl * 64 + lane];
+                acc += a.contrib[(tile * kR + cl) * (int64_t)128 + 64 + lane];
                 prev = slot;
                 if (slot >= 0 && (cl + 1 == tc || sPs[cl + 1] != slot)) a.part_row[(int64_t)slot * 64 + lane] = acc;
             }
@@ -1529,6 +1592,25 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
     // sums are deterministic), and the global write adds the two images ----
     float *red = lds;   // every wave is past its tiles (barrier below): weights and scratch are free
     static_assert(2 * P <= kLdsFloats, "two gradient images");
+    // the hidden biases: the four lane groups' column sums, (g0 + g1) + (g2 + g3) on every lane
+    auto gsum = [](float v) {
+        v += __shfl_xor(v, 16);
+        return v + __shfl_xor(v, 32);
+    };
+    float sB1[4], sB2[2];
+#pragma unroll
+    for (int to = 0; to < 4; ++to) sB1[to] = gsum(bB1[to]);
+#pragma unroll
+    for (int to = 0; to < 2; ++to) sB2[to] = gsum(bB2[to]);
+    const float sB3 = gsum(bB3[0]), sB4 = gsum(bB4[0]);
+    auto each_bias = [&](auto &&f) {   // lanes of group 0, one per feature
+#pragma unroll
+        for (int to = 0; to < 4; ++to) f(S64::w_off(0) + 64 * 128 + 16 * to + j, sB1[to], g == 0);
+#pragma unroll
+        for (int to = 0; to < 2; ++to) f(S64::w_off(1) + 32 * 64 + 16 * to + j, sB2[to], g == 0);
+        f(S64::w_off(2) + 16 * 32 + j, sB3, g == 0);
+        f(S64::w_off(3) + 8 * 16 + min(j, 7), sB4, g == 0 && j < 8);
+    };
     WSK(1);   // tiles done
     __syncthreads();
     WSK(2);   // the workgroup's last wave is done
@@ -1551,19 +1633,14 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                     for (int t = 0; t < 2; ++t) f(S64::w_off(2) + orow * 32 + 16 * t + j, gW3[0][t][r], true);
                     f(S64::w_off(3) + min(orow, 7) * 16 + j, gW4[0][0][r], orow < 8);
-                    // bias tiles: every column holds the sum (taken from column 0)
-#pragma unroll
-                    for (int to = 0; to < 4; ++to) f(S64::w_off(0) + 64 * 128 + 16 * to + orow, gB1[to][r], j == 0);
-#pragma unroll
-                    for (int to = 0; to < 2; ++to) f(S64::w_off(1) + 32 * 64 + 16 * to + orow, gB2[to][r], j == 0);
-                    f(S64::w_off(2) + 16 * 32 + orow, gB3[0][r], j == 0);
-                    f(S64::w_off(3) + 8 * 16 + min(orow, 7), gB4[0][r], j == 0 && orow < 8);
                     f(WO + min(orow, 8), gO[r], j == 0 && orow <= 8);   // w_out (8), then b_out
                 }
             };
             if (round == 0) {
                 each([&](int idx, float v, bool ok) { if (ok) img[idx] = v; });
-            } else {   // one adder per image and address: read a group, add, store (a round trip per group)
+                each_bias([&](int idx, float v, bool ok) { if (ok) img[idx] = v; });
+            } else {
+                each_bias([&](int idx, float v, bool ok) { if (ok) img[idx] = img[idx] + v; });   // one adder per image and address: read a group, add, store (a round trip per group)
                 auto group = [&](auto nv, auto &&idx_of, auto &&val_of, auto &&ok_of) {
                     constexpr int N = decltype(nv)::value;
                     float cur[N];
@@ -1590,18 +1667,9 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                       [&](int q) { return gW3[0][q >> 2][q & 3]; }, yes);
                 group(I4{}, [&](int q) { return S64::w_off(3) + min(4 * g + q, 7) * 16 + j; },
                       [&](int q) { return gW4[0][0][q]; }, [&](int q) { return 4 * g + q < 8; });
-                if (j == 0) {   // bias tiles (column 0) and the output row
-                    group(I16{}, [&](int q) { return S64::w_off(0) + 64 * 128 + 16 * (q >> 2) + 4 * g + (q & 3); },
-                          [&](int q) { return gB1[q >> 2][q & 3]; }, yes);
-                    group(I8{}, [&](int q) { return S64::w_off(1) + 32 * 64 + 16 * (q >> 2) + 4 * g + (q & 3); },
-                          [&](int q) { return gB2[q >> 2][q & 3]; }, yes);
-                    group(I4{}, [&](int q) { return S64::w_off(2) + 16 * 32 + 4 * g + q; },
-                          [&](int q) { return gB3[0][q]; }, yes);
-                    group(I4{}, [&](int q) { return S64::w_off(3) + 8 * 16 + min(4 * g + q, 7); },
-                          [&](int q) { return gB4[0][q]; }, [&](int q) { return 4 * g + q < 8; });
+                if (j == 0)   // the output row
                     group(I4{}, [&](int q) { return WO + min(4 * g + q, 8); },
                           [&](int q) { return gO[q]; }, [&](int q) { return 4 * g + q <= 8; });
-                }
             }
         }
         __syncthreads();
@@ -1696,12 +1764,30 @@ static int64_t ncf_param_len(const rg_ncf_model_t *m) {
     return m->mf_dim == 0 ? ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
 }
 extern "C" int64_t rg_ncf_mask_units(int32_t dim) { return ncf_mask_units(dim); }
-extern "C" int64_t rg_ncf_cols_per_tile(int32_t n_neg) { return n_neg < 0 || n_neg >= kRows ? -1 : kRows / (n_neg + 1); }
-extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg) {
-    const int64_t tc = rg_ncf_cols_per_tile(n_neg);
+// rows per tile: 48 for the wave kernel (E = 64 MLP: 8 columns of 1 + 5 rows, one tile per wave),
+// 32 for the tile kernel (the other towers, NeuMF)
+extern "C" int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim) {
+    if (ncf_mlp_len(dim) < 0 || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
+    return ncf_use_wave(dim, mf_dim) ? ncfw::kR : kRows;
+}
+extern "C" int64_t rg_ncf_cols_per_tile(int32_t n_neg, int32_t dim, int32_t mf_dim) {
+    const int64_t R = rg_ncf_rows_per_tile(dim, mf_dim);
+    return R < 0 || n_neg < 0 || n_neg >= R ? -1 : R / (n_neg + 1);
+}
+extern "C" int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim) {
+    const int64_t tc = rg_ncf_cols_per_tile(n_neg, dim, mf_dim);
     return tc <= 0 ? -1 : (cols + tc - 1) / tc;
 }
-extern "C" int64_t rg_ncf_rows_per_tile(void) { return kRows; }
+// the scores / dp layout of an adaptive-hinge launch: the work's tile_rows (the model's
+// rg_ncf_rows_per_tile, checked by rg_ncf_pairs)
+static int ncf_geometry(const rg_ncf_work_t *nw, const rg_mf_batch_t *b, int &TR, int &tc, int64_t &tiles) {
+    TR = nw->tile_rows;
+    if (TR != kRows && TR != ncfw::kR) return fail_arg("rg_ncf: ncf_work.tile_rows must be rg_ncf_rows_per_tile(dim, mf_dim)");
+    if (b->n_neg < 1 || b->n_neg >= TR) return fail_arg("rg_ncf: n_neg out of range");
+    tc = TR / (b->n_neg + 1);
+    tiles = (b->cols + tc - 1) / tc;
+    return RG_OK;
+}
 // workgroups resident per CU by LDS (at most 4): the E = 64 MLP takes a CU's LDS alone,
 // the small towers (and NeuMF's) leave room for several tiles in flight per CU, which is
 // what hides their gather / barrier latency
@@ -1716,7 +1802,7 @@ static int ncf_lds_floats(int E, int M) {
 }
 
 extern "C" int64_t rg_ncf_blocks(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim) {
-    const int64_t t = rg_ncf_tiles(cols, n_neg);
+    const int64_t t = rg_ncf_tiles(cols, n_neg, dim, mf_dim);
     const int lds = ncf_lds_floats(dim, mf_dim);
     if (t <= 0 || lds <= 0 || lds > kLdsMax || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
     if (ncf_use_wave(dim, mf_dim)) {   // one wave per tile, 4 waves per workgroup, one workgroup per CU
@@ -1763,8 +1849,10 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
     a.pairs = reinterpret_cast<const int2 *>(b->pairs);
     a.n_pos = b->n_pos; a.cols = b->cols; a.global_cols = b->global_cols; a.col_offset = b->col_offset;
     a.n_neg = b->n_neg; a.loss = b->loss;
-    a.tc = (int)rg_ncf_cols_per_tile(b->n_neg);
-    a.tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    if (nw->tile_rows != rg_ncf_rows_per_tile(m->dim, m->mf_dim))
+        return fail_arg("rg_ncf_pairs: ncf_work.tile_rows must be rg_ncf_rows_per_tile(dim, mf_dim)");
+    a.tc = (int)rg_ncf_cols_per_tile(b->n_neg, m->dim, m->mf_dim);
+    a.tiles = rg_ncf_tiles(b->cols, b->n_neg, m->dim, m->mf_dim);
     const int64_t negc = b->neg_cols > 0 ? b->neg_cols : b->global_cols;
     switch (b->loss) {
         case RG_LOSS_POINTWISE: a.n_a = (float)b->global_pos; a.n_b = (float)((int64_t)b->n_neg * negc); break;
@@ -1800,10 +1888,11 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
 
 extern "C" int rg_ncf_adapt_dp(void *stream, const rg_mf_batch_t *b, rg_ncf_work_t *nw, float *loss_partials) {
     if (!b || !nw || !nw->scores || !nw->dp || !loss_partials) return fail_arg("rg_ncf_adapt_dp: null argument");
-    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    int TR = 0, tc = 0;
+    int64_t tiles = 0;
+    if (ncf_geometry(nw, b, TR, tc, tiles)) return RG_E_ARG;
     hipLaunchKernelGGL(ncf_adapt_dp_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, nw->dp,
-                       tiles * kRows, (int)rg_ncf_cols_per_tile(b->n_neg), b->n_neg + 1, b->n_pos, b->cols,
-                       (float)b->global_pos, loss_partials);
+                       tiles * TR, TR, tc, b->n_neg + 1, b->n_pos, b->cols, (float)b->global_pos, loss_partials);
     return check_launch("rg_ncf_adapt_dp");
 }
 
@@ -1830,7 +1919,7 @@ __device__ __forceinline__ int adapt_winner(const float *slots, int world) {
     return w;
 }
 
-__global__ __launch_bounds__(256) void ncf_adapt_local_kernel(const float *scores, int64_t rows, int tc, int NP,
+__global__ __launch_bounds__(256) void ncf_adapt_local_kernel(const float *scores, int64_t rows, int TR, int tc, int NP,
                                                              int64_t cols, const int32_t *perm, int64_t global_cols,
                                                              int64_t col_offset, float *slots, int rank, int world,
                                                              int32_t *local_row) {
@@ -1840,7 +1929,7 @@ __global__ __launch_bounds__(256) void ncf_adapt_local_kernel(const float *score
     float best = -1.0f;
     int64_t bj = INT64_MAX, br = -1;
     for (int64_t r = tid; r < rows; r += 256) {
-        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t tile = r / TR, rr = r % TR;
         const int q = (int)(rr / tc);
         const int64_t s = tile * tc + rr % tc;
         if (q >= 1 && q < NP && s < cols) {
@@ -1867,7 +1956,7 @@ __global__ __launch_bounds__(256) void ncf_adapt_local_kernel(const float *score
     }
 }
 
-__global__ __launch_bounds__(256) void ncf_adapt_global_kernel(const float *scores, float *dp, int64_t rows, int tc,
+__global__ __launch_bounds__(256) void ncf_adapt_global_kernel(const float *scores, float *dp, int64_t rows, int TR, int tc,
                                                               int64_t n_pos_cols, float n_a, const float *slots,
                                                               int world, float *count, float *loss_partial) {
     __shared__ float scnt[256], sloss[256];
@@ -1875,7 +1964,7 @@ __global__ __launch_bounds__(256) void ncf_adapt_global_kernel(const float *scor
     const float mx = slots[4 * adapt_winner(slots, world)];
     float cnt = 0.0f, ls = 0.0f;
     for (int64_t r = tid; r < rows; r += 256) {
-        const int64_t tile = r / kRows, rr = r % kRows;
+        const int64_t tile = r / TR, rr = r % TR;
         const int64_t s = tile * tc + rr % tc;
         dp[r] = 0.0f;
         if (rr < (int64_t)tc && s < n_pos_cols) {
@@ -1906,10 +1995,12 @@ extern "C" int rg_ncf_adapt_local(void *stream, const rg_mf_batch_t *b, const rg
                                   float *slots, int32_t rank, int32_t world, int32_t *local_row) {
     if (!b || !w || !nw || !nw->scores || !slots || !local_row || world < 1 || rank < 0 || rank >= world)
         return fail_arg("rg_ncf_adapt_local: bad argument");
-    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
-    hipLaunchKernelGGL(ncf_adapt_local_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, tiles * kRows,
-                       (int)rg_ncf_cols_per_tile(b->n_neg), b->n_neg + 1, b->cols, w->plan_perm, b->global_cols,
-                       b->col_offset, slots, rank, world, local_row);
+    int TR = 0, tc = 0;
+    int64_t tiles = 0;
+    if (ncf_geometry(nw, b, TR, tc, tiles)) return RG_E_ARG;
+    hipLaunchKernelGGL(ncf_adapt_local_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, tiles * TR, TR,
+                       tc, b->n_neg + 1, b->cols, w->plan_perm, b->global_cols, b->col_offset, slots, rank, world,
+                       local_row);
     return check_launch("rg_ncf_adapt_local");
 }
 
@@ -1917,10 +2008,11 @@ extern "C" int rg_ncf_adapt_global(void *stream, const rg_mf_batch_t *b, rg_ncf_
                                    int32_t world, float *count, float *loss_partials) {
     if (!b || !nw || !nw->scores || !nw->dp || !slots || !count || !loss_partials || world < 1)
         return fail_arg("rg_ncf_adapt_global: bad argument");
-    const int64_t tiles = rg_ncf_tiles(b->cols, b->n_neg);
+    int TR = 0, tc = 0;
+    int64_t tiles = 0;
+    if (ncf_geometry(nw, b, TR, tc, tiles)) return RG_E_ARG;
     hipLaunchKernelGGL(ncf_adapt_global_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nw->scores, nw->dp,
-                       tiles * kRows, (int)rg_ncf_cols_per_tile(b->n_neg), b->n_pos, (float)b->global_pos, slots,
-                       world, count, loss_partials);
+                       tiles * TR, TR, tc, b->n_pos, (float)b->global_pos, slots, world, count, loss_partials);
     return check_launch("rg_ncf_adapt_global");
 }
 

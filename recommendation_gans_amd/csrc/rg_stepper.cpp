@@ -1363,7 +1363,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     st->prep_in_pairs = ab_flag("RG_PREP_IN_PAIRS", false);
     // pipelined step (rg_mf_pipe_step): single rank, claimed slots, pointwise / bpr / hinge, a
     // float4 row layout of >= 8 lanes (dim a multiple of 4, 32..256)
-    st->pipe = env_flag("RG_PIPE", RG_PIPE_DEFAULT) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
+    st->pipe = ab_flag("RG_PIPE", RG_PIPE_DEFAULT) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
                (cfg->loss == RG_LOSS_POINTWISE || cfg->loss == RG_LOSS_BPR || cfg->loss == RG_LOSS_HINGE) &&
                t0.dim % 4 == 0 && t0.dim >= 32 && t0.dim <= 256 && cfg->work.part_row && cfg->work.part_bias &&
                cfg->work.loss_partials && cfg->n_partials > 0;
@@ -1372,7 +1372,8 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         // holds (>= 4 workgroups per CU at the launch's register count), so the rows they wait
         // for always have room to run whatever the dispatch order
         const int64_t upb = rg_mf_plan_units_per_block(t0.dim);
-        st->pipe = upb > 0 && (cfg->cols + upb - 1) / upb <= 2 * (int64_t)rg::num_cus();
+        st->pipe = upb > 0 && (cfg->cols + upb - 1) / upb <= 2 * (int64_t)rg::num_cus() &&
+                   std::max(t0.num_users, t0.num_items) * (int64_t)t0.dim * 4 < ((int64_t)1 << 31);
     }
     if (st->pipe) {
         const int64_t rows = t0.num_users + t0.num_items;

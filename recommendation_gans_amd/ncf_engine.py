@@ -84,9 +84,10 @@ class NCFEngine:
         self.pool = torch.from_numpy(np.stack([pu, pi], 1).astype(np.int32)).to(dev).contiguous()
         self.loss, self.n_neg, self.batch_size = loss, int(n_neg), int(batch_size)
         B, n = self.batch_size, self.n_neg
-        self.tc = int(lib.rg_ncf_cols_per_tile(n))
-        self.tiles = int(lib.rg_ncf_tiles(B, n))
-        self.rows = self.tiles * int(lib.rg_ncf_rows_per_tile())
+        self.tile_rows = int(lib.rg_ncf_rows_per_tile(E, self.M))
+        self.tc = int(lib.rg_ncf_cols_per_tile(n, E, self.M))
+        self.tiles = int(lib.rg_ncf_tiles(B, n, E, self.M))
+        self.rows = self.tiles * self.tile_rows
         self.blocks = int(lib.rg_ncf_blocks(B, n, E, self.M))
         self.units = int(lib.rg_ncf_mask_units(E))
         rows = self.U + self.I
@@ -199,7 +200,7 @@ class NCFEngine:
 
     def _work(self, masks, training):
         nw = _lib.NCFWork(ptr(self.contrib), ptr(self.mlp_partials), ptr(self.scores_buf), ptr(self.dp_buf),
-                          None, None, 0, 1 if training else 0, 0)
+                          None, None, 0, 1 if training else 0, self.tile_rows)
         if masks is not None:
             mp, mn = masks
             nw.mask_pos, nw.mask_neg = ptr(mp), ptr(mn)

@@ -118,16 +118,23 @@ def test_no_gpu_means_loud_failure():
 
 
 def test_ncf_launch_geometry():
-    """Host-side shape functions (no GPU): the E = 64 MLP runs one wave per 32-row tile,
-    4 waves per workgroup, at most 256 workgroups (= weight-gradient partials); the other
-    towers keep the tile kernel's workgroup-per-tile count (capped by LDS residency)."""
+    """Host-side shape functions (no GPU): the E = 64 MLP runs one wave per tile of
+    rg_ncf_rows_per_tile(64, 0) rows (32 in the product; 48 = 8 whole columns of 1 + 5 rows in the
+    -DRG_NCF_WAVE_ROWS=48 build), 4 waves per workgroup, at most 256 workgroups; the other towers
+    and NeuMF keep the tile kernel's 32-row tiles and workgroup-per-tile count (capped by LDS)."""
     from recommendation_gans_amd import _lib
     L = _lib.load()
-    assert L.rg_ncf_rows_per_tile() == 32
-    assert L.rg_ncf_cols_per_tile(5) == 5 and L.rg_ncf_tiles(8192, 5) == 1639
     wave = not (_lib.ab_build() and os.environ.get("RG_NCF_TILE") == "1")
-    assert L.rg_ncf_blocks(8192, 5, 64, 0) == (256 if wave else 256)
-    assert L.rg_ncf_blocks(1000, 5, 64, 0) == ((200 + 3) // 4 if wave else 200)
+    R = int(L.rg_ncf_rows_per_tile(64, 0))
+    assert R in ((32, 48) if wave else (32,))
+    assert L.rg_ncf_rows_per_tile(32, 0) == 32 and L.rg_ncf_rows_per_tile(16, 50) == 32
+    tc = R // 6
+    assert L.rg_ncf_cols_per_tile(5, 64, 0) == tc and L.rg_ncf_tiles(8192, 5, 64, 0) == -(-8192 // tc)
+    assert L.rg_ncf_cols_per_tile(5, 32, 0) == 5 and L.rg_ncf_tiles(8192, 5, 32, 0) == 1639
+    assert L.rg_ncf_cols_per_tile(1, 64, 0) == R // 2
+    assert L.rg_ncf_blocks(8192, 5, 64, 0) == 256
+    t1000 = -(-1000 // tc)
+    assert L.rg_ncf_blocks(1000, 5, 64, 0) == ((t1000 + 3) // 4 if wave else 200)
     assert L.rg_ncf_blocks(20, 5, 64, 0) == (1 if wave else 4)
     assert L.rg_ncf_blocks(1000, 5, 16, 50) == 200   # NeuMF: the tile kernel, one workgroup per tile
     assert L.rg_ncf_blocks(8192, 5, 48, 0) == -1     # unsupported width
