@@ -468,7 +468,8 @@ def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None,
     element), or -- an element on which two fp32 restatements of the same step differ
     (Adam's g / (|g| + eps) of a cancelled gradient sum) -- |got - ref64| <= band *
     |ref32 - ref64| + rtol / 10 * |ref64| + floor (the larger of that distance and
-    ``alt32``'s, a second fp32 restatement summing in another order); given ``noise`` (MFOracle(noise=True)'s
+    ``alt32``'s: further fp32 restatements summing in other orders, one or a list); given ``noise``
+    (MFOracle(noise=True)'s
     per-element bound on an fp32 step's rounding noise, accumulated over the steps) instead:
     |got - ref64| <= rtol * |ref64| + 2 noise + floor.  Returns (ok, stats) with ok = no element
     failing both, and stats: n, n_out (elements outside rtol of ref32), frac_out, n_fail,
@@ -497,12 +498,18 @@ def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None,
             # the fp32 restatement's distance from float64 (and a second fp32 order's, ``alt32``)
             # samples the rounding noise of the element
             dist = (r - r64).abs()
-            if alt32 is not None:
-                dist = torch.maximum(dist, (torch.as_tensor(alt32).double().reshape(-1) - r64).abs())
+            alts = alt32 if isinstance(alt32, (list, tuple)) else ([] if alt32 is None else [alt32])
+            for alt in alts:
+                dist = torch.maximum(dist, (torch.as_tensor(alt).double().reshape(-1) - r64).abs())
             ok_e |= (g - r64).abs() <= band * dist + 0.1 * rtol * r64.abs() + floor
     n = int(r.numel())
     n_out = int((~in_tol).sum())
+    bad = (~ok_e).nonzero().flatten()[:4].tolist()
+    worst = [{"i": i, "got": float(g[i]), "ref32": float(r[i]),
+              "ref64": float(ref64.reshape(-1)[i]) if ref64 is not None else None,
+              "before": float(torch.as_tensor(before).reshape(-1)[i]) if before is not None else None} for i in bad]
     stats = {"n": n, "n_out": n_out, "frac_out": n_out / max(n, 1), "n_fail": int((~ok_e).sum()), "n_ill": n_ill,
+             "fails": worst,
              "max_rel": float(d.max()) / max(mx, 1e-30) if n else 0.0,
              "max_elem_rel": float((d / (r.abs() + max(floor, 1e-38))).max()) if n else 0.0}
     return stats["n_fail"] == 0, stats

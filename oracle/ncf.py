@@ -50,10 +50,13 @@ class MLPParams:
         return [(self.t[k], self.t[k + 1]) for k in range(2, len(self.t), 2)]
 
 
-def forward(P, u, i, masks):
-    """Returns p (N,1) and the cache for backward.  ``masks``: per hidden layer (N, out) 0/1."""
+def forward(P, u, i, masks, xperm=None):
+    """Returns p (N,1) and the cache for backward.  ``masks``: per hidden layer (N, out) 0/1.
+    ``xperm``: the input features in that order (P's first layer permuted to match)."""
     Ue, Ie = P.emb()
     x = torch.cat([Ue[u], Ie[i]], dim=-1)
+    if xperm is not None:
+        x = x[:, xperm]
     lin = P.linears()
     cache = {"x": x, "z": [], "a": [x]}
     a = x
@@ -70,7 +73,7 @@ def forward(P, u, i, masks):
     return p, cache
 
 
-def backward(P, u, i, masks, cache, dp):
+def backward(P, u, i, masks, cache, dp, xperm=None):
     """dp: dL/dp (N,1).  Returns dense grads in parameter order."""
     p = cache["p"]
     dz = dp * (1 - p) * p
@@ -92,6 +95,8 @@ def backward(P, u, i, masks, cache, dp):
     grads_lin.reverse()
     Ue, Ie = P.emb()
     E = Ue.shape[1]
+    if xperm is not None:
+        dx = dx[:, torch.argsort(xperm)]
     dU = torch.zeros_like(Ue).index_add_(0, u, dx[:, :E])
     dI = torch.zeros_like(Ie).index_add_(0, i, dx[:, E:])
     out = [dU, dI]
@@ -106,9 +111,10 @@ class NCFOracle:
     def __init__(self, tensors, names, pool_u, pool_i, mt_state, loss="pointwise", lr=1e-2, weight_decay=1e-5,
                  n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None):
         self.P = MLPParams(tensors, names)
-        # order_seed (pointwise, test infrastructure): run the step over the examples in a
-        # seeded permuted order -- the same arithmetic summed in another fp32 order, a second
-        # sample of the rounding noise for tests/parity_report.py's elementwise band
+        # order_seed (pointwise, test infrastructure): run the step over the examples, the input
+        # features and every hidden layer's units in seeded orders -- the same arithmetic summed
+        # in other fp32 orders (batch sums and every product's inner sum), a further sample of
+        # the rounding noise for tests/parity_report.py's elementwise band
         assert order_seed is None or loss == "pointwise"
         self.order = None if order_seed is None else torch.Generator().manual_seed(order_seed)
         self.loss_kind = loss
@@ -130,19 +136,51 @@ class NCFOracle:
         pr = torch.randperm(len(u), generator=self.order)
         return u[pr], i[pr], [m[pr] for m in masks]
 
+    def _unit_orders(self):
+        """order_seed: the input features and every hidden layer's units in a seeded order (the
+        same function; every product sums over its inner dimension in another order).  Returns
+        (P', masks -> masks', grads' -> grads, xperm); identity without order_seed."""
+        if self.order is None:
+            return self.P, (lambda m: m), (lambda g: g), None
+        lin = self.P.linears()
+        E2 = lin[0][0].shape[1]
+        xperm = torch.randperm(E2, generator=self.order)
+        hperm = [torch.randperm(W.shape[0], generator=self.order) for W, _ in lin[:-1]]
+        ins = [xperm] + hperm                                 # input order of linear k
+        t = list(self.P.t[:2])
+        for k, (W, b) in enumerate(lin):
+            rows = hperm[k] if k < len(hperm) else torch.arange(W.shape[0])
+            t += [W[rows][:, ins[k]], b[rows]]
+        Pp = MLPParams(t, self.P.names)
+
+        def masks_p(ms):
+            return [m[:, hperm[k]] for k, m in enumerate(ms)]
+
+        def grads_back(g):
+            out = list(g[:2])
+            for k in range(len(lin)):
+                dW, db = g[2 + 2 * k], g[3 + 2 * k]
+                rows = torch.argsort(hperm[k]) if k < len(hperm) else torch.arange(dW.shape[0])
+                out += [dW[rows][:, torch.argsort(ins[k])], db[rows]]
+            return out
+        return Pp, masks_p, grads_back, xperm
+
     def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
         u = torch.as_tensor(pos_u).long()
         i = torch.as_tensor(pos_i).long()
         u, i, masks_pos = self._permuted(u, i, masks_pos)
-        p_pos, c_pos = forward(self.P, u, i, masks_pos)
+        P, mperm, gback, xperm = self._unit_orders()
+        masks_pos = mperm(masks_pos)
+        p_pos, c_pos = forward(P, u, i, masks_pos, xperm)
         idx, nu, ni = self.draw(self.n * self.batch_size)
         nu, ni, masks_neg = self._permuted(nu, ni, masks_neg)
-        p_neg, c_neg = forward(self.P, nu, ni, masks_neg)
+        masks_neg = mperm(masks_neg)
+        p_neg, c_neg = forward(P, nu, ni, masks_neg, xperm)
         kind = self.loss_kind
         loss, dpp, dpn = omf.loss_and_dp(kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n, self.batch_size)
-        g1 = backward(self.P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1))
-        g2 = backward(self.P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1))
-        grads = [a + b for a, b in zip(g1, g2)]
+        g1 = backward(P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1), xperm)
+        g2 = backward(P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1), xperm)
+        grads = gback([a + b for a, b in zip(g1, g2)])
         self.opt.step(self.P.t, grads)
         if return_all:
             return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx, neg_u=nu, neg_i=ni, grads=grads)

@@ -128,16 +128,16 @@ static int nccl_after(Comm *c, hipStream_t stream, ncclResult_t r, const char *w
     return RG_OK;
 }
 
-// host-staged all-reduce: D2H -> host callback -> H2D, all on the communicator stream
-static int host_allreduce(Comm *c, float *buf, int64_t n) {
+// host-staged all-reduce: D2H -> host callback -> H2D, all on `stream`
+static int host_allreduce(Comm *c, hipStream_t stream, float *buf, int64_t n) {
     if (n > c->pinned_floats) return fail_arg("rg_comm (host): buffer larger than the staging area");
     if (c->host_error) return fail_arg("rg_comm (host): an earlier host all-reduce failed");
     Comm::HostCall *hc = new (std::nothrow) Comm::HostCall{c, n};
     if (!hc) return fail_arg("rg_comm (host): out of memory");
-    hipError_t e = hipMemcpyAsync(c->pinned, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipLaunchHostFunc(c->stream, host_trampoline, hc);
+    hipError_t e = hipMemcpyAsync(c->pinned, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipLaunchHostFunc(stream, host_trampoline, hc);
     else delete hc;
-    if (e == hipSuccess) e = hipMemcpyAsync(buf, c->pinned, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(buf, c->pinned, (size_t)n * sizeof(float), hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) {
         set_error(std::string("rg_comm (host): ") + hipGetErrorString(e));
         return RG_E_LAUNCH;
@@ -186,7 +186,7 @@ int comm_begin(void *h, hipStream_t stream, float *buf, int64_t n) {
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
     if (e != hipSuccess) return hip_fail("rg_comm_allreduce_begin", e);
     if (c->local) return local_roundtrip(c, c->stream, buf, n);
-    if (c->host_fn) return host_allreduce(c, buf, n);
+    if (c->host_fn) return host_allreduce(c, c->stream, buf, n);
     return nccl_after(c, c->stream, ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream),
                       "ncclAllReduce");
 }
@@ -196,10 +196,9 @@ hipStream_t comm_stream(void *h) { return h ? static_cast<Comm *>(h)->stream : n
 int comm_allreduce_on(void *h, hipStream_t stream, float *buf, int64_t n) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || !buf || n < 0) return fail_arg("rg_comm allreduce: bad argument");
-    if (c->host_fn) {                      // staged through the host on the communicator stream
-        const int rc = comm_begin(h, stream, buf, n);
-        return rc ? rc : comm_end(h, stream);
-    }
+    // staged through the host on the caller's stream, where RCCL would run it (the stepper's
+    // placement: the owner step's exchanges on the compute stream beside the user update)
+    if (c->host_fn) return host_allreduce(c, stream, buf, n);
     if (c->local) return local_roundtrip(c, stream, buf, n);
     if (c->world == 1) return RG_OK;       // a one-rank sum is the buffer itself: no RCCL launch
     return nccl_after(c, stream, ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, stream),

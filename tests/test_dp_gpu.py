@@ -365,11 +365,13 @@ def test_owner_native_rccl_world1():
 
 @pytest.mark.parametrize("loss", ["bpr", "adaptive_hinge"])
 def test_owner_native_concurrent_step_world2(loss):
-    """The whole native owner step (rg_mf_stepper_train: the score all-reduce fenced on the main
-    stream, the item gradient and its all-reduce on the communicator stream beside the user
-    update and the next owner prepare) at world 2 -- two processes on cuda:0, the all-reduces
-    host-staged through gloo in stream order (comm.HostComm; RCCL refuses two ranks on one GPU)
-    -- == one process at batch 2B."""
+    """The whole native owner step (rg_mf_stepper_train, train_owner's stream placement: the score
+    all-reduce and the item-gradient all-reduce on the main stream, where RCCL takes them; the
+    user update and the next owner prepare on the communicator stream beside the item exchange
+    and update) at world 2 -- two processes on cuda:0, each all-reduce host-staged through gloo
+    on the main stream in stream order (comm.HostComm: D2H, host callback, H2D on the caller's
+    stream, as RCCL would be enqueued; RCCL refuses two ranks on one GPU) -- == one process at
+    batch 2B."""
     out = mp.Manager().dict()
     mp.spawn(_worker_own_host, args=(2, _free_port(), loss, out), nprocs=2, join=True)
     _own_check(out, 2, loss)

@@ -92,13 +92,16 @@ def test_ncf_two_order_band_covers_a_third_order():
     b = oncf.NCFOracle([t.clone() for t in params], names, pool_u, pool_i, st.copy(), order_seed=1, **kw)
     c = oncf.NCFOracle([t.clone() for t in params], names, pool_u, pool_i, st.copy(), order_seed=2, **kw)
     r = oncf.NCFOracle([t.double() for t in params], names, pool_u, pool_i, st.copy(), **kw)
+    # the reordered restatement is the same function: in float64 it lands on the canonical one
+    r2 = oncf.NCFOracle([t.double() for t in params], names, pool_u, pool_i, st.copy(), order_seed=3, **kw)
     widths = sizes[1:]
     for s in range(3):
         pu, pi = rs.randint(0, U, B), np.minimum(rs.zipf(1.3, B) - 1, I - 1)
         mp = [torch.from_numpy((rs.rand(B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
         mn = [torch.from_numpy((rs.rand(n * B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
-        for o in (a, b, c, r):
+        for o in (a, b, c, r, r2):
             o.step(pu, pi, mp, mn)
         for k in range(len(params)):
             ok, st_ = omf.elementwise_parity(c.P.t[k], a.P.t[k], r.P.t[k], alt32=b.P.t[k])
             assert ok, (s, k, st_)
+            assert torch.allclose(r2.P.t[k], r.P.t[k], rtol=1e-9, atol=1e-12), (s, k)
