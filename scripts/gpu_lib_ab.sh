@@ -27,7 +27,7 @@ for name in "$@"; do
 import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "mf_pairs" in r["Name"] or "mf_back" in r["Name"]:
+        if "mf_pairs" in r["Name"] or "mf_back" in r["Name"] or "mf_prepare" in r["Name"]:
             print(sys.argv[2], r["Name"].split("(")[0][-60:], r["Calls"], round(float(r["AverageNs"]) / 1e3, 2), "us")
 EOF
 done
