@@ -1027,7 +1027,8 @@ int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
 
 // part 2 (after the score exchange): dL/dz, contribution lists, the item rows' data gradient
 // (grad_stream: where the item gradient runs, ordered after the backward on s)
-int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr) {
+int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr,
+              hipEvent_t after_back = nullptr) {
     if (st.own_stage != 1) return rg::fail_arg("rg_mf_stepper_owner_mid: owner_begin must come first");
     const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
     rg_mf_work_t w = owner_work(st, st.own_in, st.own_unit);
@@ -1036,6 +1037,10 @@ int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stre
     if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = rg_mf_owner_adapt(s, &b))) return rc;   // global max, count
     rc = rg_mf_owner_back(s, tb, &b, &w);
     if (rc) return rc;
+    if (after_back) {   // the user rows' lists are complete: their update need not wait for the items'
+        const hipError_t e = hipEventRecord(after_back, s);
+        if (e != hipSuccess) return hip_fail("stepper: record the backward", e);
+    }
     if (grad_stream && grad_stream != s) {
         hipError_t e = hipSuccess;
         if (!st.own_back) e = hipEventCreateWithFlags(&st.own_back, hipEventDisableTiming | hipEventDisableSystemFence);
@@ -1105,7 +1110,6 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         const int64_t len = (int64_t)(1 + st.cfg.n_neg) * st.cfg.global_cols;
         if ((rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.owner_scores[st.own_unit % 2], len))) return rc;
     }
-    if ((rc = owner_mid(st, s, loss_out))) return rc;
     // one rank: nothing to overlap (the exchanges are no-ops), so no cross-stream hops
     const bool side = st.cfg.world > 1;
     hipStream_t u = side ? rg::comm_stream(st.cfg.comm) : s;
@@ -1113,10 +1117,13 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     if (side) {
         if (!st.own_grads) e = hipEventCreateWithFlags(&st.own_grads, hipEventDisableTiming);
         if (e == hipSuccess && !st.own_users) e = hipEventCreateWithFlags(&st.own_users, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(st.own_grads, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(u, st.own_grads, 0);
-        if (e != hipSuccess) return hip_fail("stepper: order the user update", e);
+        if (e != hipSuccess) return hip_fail("stepper: owner events", e);
     }
+    // the user update starts after the backward (its lists), beside the item-gradient pull, the
+    // item exchange and the item update (they touch item rows; it touches user rows)
+    if ((rc = owner_mid(st, s, loss_out, nullptr, side ? st.own_grads : nullptr))) return rc;
+    if (side && (e = hipStreamWaitEvent(u, st.own_grads, 0)) != hipSuccess)
+        return hip_fail("stepper: order the user update", e);
     if ((rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
         return rc;
     st.cfg.step += 1;
