@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -138,3 +140,21 @@ def test_ncf_launch_geometry():
     assert L.rg_ncf_blocks(20, 5, 64, 0) == (1 if wave else 4)
     assert L.rg_ncf_blocks(1000, 5, 16, 50) == 200   # NeuMF: the tile kernel, one workgroup per tile
     assert L.rg_ncf_blocks(8192, 5, 48, 0) == -1     # unsupported width
+
+
+def test_product_library_is_not_the_ab_build():
+    """The shipped librg_hip.so carries none of the measured-slower alternatives (DESIGN §7, A/B
+    build): rg_build_flags() is 0, the pipelined step refuses before touching the GPU, and the
+    A/B variant (when built) says so about itself."""
+    from recommendation_gans_amd import _lib
+    if os.environ.get("RG_LIB"):
+        pytest.skip("RG_LIB points at a variant")
+    L = _lib.load()
+    assert L.rg_build_flags() == 0 and not _lib.ab_build()
+    rc = L.rg_mf_pipe_step(None, None, None, None, None, None, None, None, None, None, None)
+    assert rc != 0 and b"A/B build" in L.rg_last_error()
+    ab = os.path.join(os.path.dirname(_lib.LIB_PATH), "_variants", "librg_hip_ab.so")
+    if os.path.exists(ab):
+        A = ctypes.CDLL(ab, mode=ctypes.RTLD_LOCAL)
+        A.rg_build_flags.restype = ctypes.c_int32
+        assert A.rg_build_flags() & _lib.RG_BUILD_AB
