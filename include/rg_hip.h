@@ -602,6 +602,11 @@ int rg_mf_stepper_prefetch(void *stepper, void *stream, const rg_mf_step_in_t *n
 /* The same prepare enqueued on `stream` itself (no side stream, no events): for callers that
  * enqueue it after their step's last kernel (the NCF / NeuMF engines). */
 int rg_mf_stepper_prefetch_inline(void *stepper, void *stream, const rg_mf_step_in_t *next);
+/* The bookkeeping of rg_mf_stepper_prefetch_inline without its launch: fills the batch / work
+ * of the next unit's prepare, which the caller launches on `stream` inside another kernel
+ * (rg_ncf_tail).  Returns 1 (launch it), 0 (already prepared) or an error status. */
+int rg_mf_stepper_prefetch_args(void *stepper, void *stream, const rg_mf_step_in_t *next, rg_mf_batch_t *batch_out,
+                                rg_mf_work_t *work_out);
 /* The replicated data-parallel step (dp_mode 1) in two halves around a caller-run
  * exchange (comm == NULL; tests, gloo): dp_begin = prepare / pairs / release / the next
  * step's prepare / rg_mf_grads_sharded into grad_buf; the caller reduce-scatters grad_buf;
@@ -738,6 +743,13 @@ int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *model, const float *g
 /* Embedding rows [row_begin, row_end) (users then items): pull + optimizer, in place. */
 int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
                  const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
+/* The tail of a single-GPU NCF step (MLP towers, mf_dim = 0) in ONE launch: the next step's
+ * prepare (rg_mf_prepare of next / next_work; next = NULL: none), rg_ncf_update (the MLP
+ * weight-gradient reduce + optimizer, with the step's loss) and rg_ncf_apply (every embedding
+ * row's pull + optimizer) -- the same sums as the three separate calls. */
+int rg_ncf_tail(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
+                int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
+                const rg_mf_batch_t *next, const rg_mf_work_t *next_work);
 /* NeuMF (spotlight/dnn_models/neuMF.py:7-55): rg_ncf_pairs / rg_ncf_update run with
  * model->mf_dim > 0 (the affine_output sees cat(tower, U_mf[u] * I_mf[i])); this applies
  * the GMF tables, then the MLP tables (as rg_ncf_apply). */

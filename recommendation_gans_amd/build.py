@@ -21,7 +21,7 @@ ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["rg_api.cpp", "rg_sampler.hip", "rg_mf.hip", "rg_stepper.cpp", "rg_comm.cpp", "rg_mtjump.cpp", "rg_ncf.hip",
            "rg_gemm.hip", "rg_gan.hip", "rg_eval.hip", "rg_plan.hip", "rg_owner.hip", "rg_uniform.hip", "rg_membw.hip",
            "rg_pool.cpp"]
-HEADERS = ["rg_common.h", "rg_gemm.h", "rg_mt.h", "rg_owner.h"]
+HEADERS = ["rg_common.h", "rg_gemm.h", "rg_mt.h", "rg_owner.h", "rg_mlp_update.h"]
 
 
 def _hipcc():

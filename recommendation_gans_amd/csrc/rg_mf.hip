@@ -30,6 +30,7 @@
 #include "rg_common.h"
 #include "rg_mt.h"
 #include "rg_owner.h"
+#include "rg_mlp_update.h"
 
 namespace rg {
 
@@ -1398,6 +1399,7 @@ struct MtGenArgs {
 struct BackGrid {
     int64_t prep_blocks, apply_start, apply_padded;
     int32_t prep_first, xcd_map;
+    int64_t upd_blocks;   // NCF step: MLP update workgroups after the prepare's (rg_ncf_tail)
 };
 
 template <class L, int NT, bool SPEC = false, bool OWN = false, bool LAZY = false, bool LSPEC = false>
@@ -1408,7 +1410,7 @@ template <class L, int NT, bool SPEC = false, bool OWN = false, bool LAZY = fals
 #endif
 __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs a, PairsArgs prep, int2 *prep_out,
                                                         int64_t apply_blocks, MtGenArgs gen, BackGrid bg,
-                                                        OwnerArgs own) {
+                                                        OwnerArgs own, MlpUpdArgs upd) {
     static_assert(kBlock == kOwnSeg, "an owner prepare segment is one workgroup");
     static_assert(kBlock == kGenThreads, "the MT walk runs on one full workgroup");
     const int64_t B = blockIdx.x;
@@ -1430,6 +1432,11 @@ __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs 
 #endif
             if (OWN) owner_prepare_block(own, blk);
             else prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+            return;
+        }
+        if (blk < bg.prep_blocks + bg.upd_blocks) {             // the NCF step's MLP update
+            __shared__ float red[kMlpSlices][64];
+            mlp_update_block<kBlock / kWave>(upd, blk - bg.prep_blocks, red);
             return;
         }
         if (B < bg.apply_start) return;                         // alignment padding
@@ -2206,6 +2213,7 @@ struct BackLaunchF {
     hipStream_t s;
     const OwnerArgs *own = nullptr;   // owner-sharded DP: the next step's owner prepare
     bool lazy = false;                // lazy dense pass (rg_mf_apply_lazy)
+    const MlpUpdArgs *upd = nullptr;  // NCF step: the MLP update in the same launch (rg_ncf_tail)
     template <class L>
     int operator()() {
         const int64_t rows = a->row_end - a->row_begin;
@@ -2225,8 +2233,10 @@ struct BackLaunchF {
 #else
         constexpr int prep_first = 1, xcd_map = 0;
 #endif
-        BackGrid bg{prep_blocks, 0, 0, prep_first, prep_first ? xcd_map : 0};
-        const int64_t head = prep_blocks + (gen.nwords > 0 ? 1 : 0);
+        if (upd && !prep_first) return fail_arg("rg_ncf_tail: the MLP update workgroups need the prepare-first grid");
+        const int64_t upd_blocks = upd ? ((int64_t)upd->P + 63) / 64 : 0;
+        BackGrid bg{prep_blocks, 0, 0, prep_first, prep_first ? xcd_map : 0, upd_blocks};
+        const int64_t head = prep_blocks + upd_blocks + (gen.nwords > 0 ? 1 : 0);
         int64_t total = nb + head;
         if (prep_first) {
             bg.apply_start = (head + 7) / 8 * 8;
@@ -2235,14 +2245,16 @@ struct BackLaunchF {
         }
         const dim3 grid((unsigned)total);
         const OwnerArgs oa = own ? *own : OwnerArgs{};
+        const MlpUpdArgs ua = upd ? *upd : MlpUpdArgs{};
         LaunchEvents &le = launch_events();
         const hipEvent_t e0 = le.start, e1 = le.stop;
         le = LaunchEvents{};
         auto go = [&](auto kernel) {
             if (e0 || e1)
-                hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, e0, e1, 0, *a, *prep, prep_out, nb, gen, bg, oa);
+                hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, e0, e1, 0, *a, *prep, prep_out, nb, gen, bg, oa,
+                                      ua);
             else
-                hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa);
+                hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa, ua);
         };
         if (own) {
             go(mf_back_kernel<L, 0, true, true>);
@@ -2250,7 +2262,7 @@ struct BackLaunchF {
         }
 #if RG_AB
         if constexpr (L::LPU >= kCap) {
-            if (!lazy && dense_v2 && a->contrib == nullptr) {
+            if (!lazy && dense_v2 && a->contrib == nullptr && upd == nullptr) {
                 // a few workgroups per CU, each wave walking a chunk of row groups (mf_dense_kernel)
                 static const int per_cu = [] { const char *e = getenv("RG_DENSE_PER_CU"); return e ? atoi(e) : 4; }();
                 int64_t db = (int64_t)num_cus() * per_cu;
@@ -2631,8 +2643,69 @@ extern "C" int rg_mf_step_hot(void *stream, const rg_mf_tables_t *t, const rg_mf
     return dispatch_dim(t->dim, f);
 }
 
+static int ncf_apply_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib, const rg_opt_t *opt,
+                          int64_t row_begin, int64_t row_end, ApplyArgs &a);
+
 extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib,
                             const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+    ApplyArgs a{};
+    const int rc = ncf_apply_args(m, w, contrib, opt, row_begin, row_end, a);
+    if (rc) return rc;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
+    return dispatch_dim(m->dim, f);
+}
+
+// The tail of a single-GPU NCF step in one launch (mf_back_kernel's grid): the next step's
+// prepare (next = NULL: none), the MLP update from the pair kernel's weight-gradient partials
+// (rg_ncf_update's reduction and optimizer, the same sums) with the step's loss, and the
+// embedding rows' update (rg_ncf_apply) -- three launches and their tails in one; the three
+// parts touch disjoint data.  MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply).
+extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                           int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
+                           const rg_mf_batch_t *next, const rg_mf_work_t *next_w) {
+    if (!m || !w || !nw || !opt || !nw->contrib || !nw->mlp_partials || !m->mlp)
+        return fail_arg("rg_ncf_tail: null argument");
+    if (m->mf_dim != 0) return fail_arg("rg_ncf_tail: MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply)");
+    if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_tail: Adam needs m state");
+    if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_tail: optimizer needs v state");
+    const int64_t P = rg_ncf_mlp_len(m->dim);
+    if (P < 0 || nparts < 1) return fail_arg("rg_ncf_tail: bad dim / partial count");
+    if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_tail: loss needs partials");
+    ApplyArgs a{};
+    int rc = ncf_apply_args(m, w, nw->contrib, opt, 0, -1, a);
+    if (rc) return rc;
+    if (loss && loss->out) {   // finalized by the dense blocks' first workgroup (rg_ncf_update's sums)
+        a.partials = loss_partials;
+        a.n_partials = loss->n_partials;
+        a.inv_a = loss->inv_a;
+        a.inv_b = loss->inv_b;
+        a.loss_out = loss->out;
+    }
+    MlpUpdArgs u{};
+    u.mlp = m->mlp;
+    u.m = opt->kind == RG_OPT_ADAM ? m->mlp_m : nullptr;
+    u.v = opt->kind == RG_OPT_SGD ? nullptr : m->mlp_v;
+    u.wpart = nw->mlp_partials;
+    u.nparts = (int)nparts;
+    u.P = (int)P;
+    u.opt = *opt;
+    u.mode = 0;
+    PairsArgs prep{};
+    int2 *prep_out = nullptr;
+    int64_t prep_blocks = 0;
+    if (next) {
+        if ((rc = prepare_args(next, next_w, nullptr, prep))) return rc;
+        if (next->pairs == nullptr) return fail_arg("rg_ncf_tail: null next pairs");
+        prep_out = reinterpret_cast<int2 *>(next->pairs);
+        prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
+    }
+    BackLaunchF f{&a, &prep, prep_out, prep_blocks, MtGenArgs{}, (hipStream_t)stream};
+    f.upd = &u;
+    return dispatch_dim(m->dim, f);
+}
+
+static int ncf_apply_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib, const rg_opt_t *opt,
+                          int64_t row_begin, int64_t row_end, ApplyArgs &a) {
     if (!m || !w || !opt || !contrib || !m->user_w || !m->item_w) return fail_arg("rg_ncf_apply: null argument");
     if (!w->row_count || !w->row_list || !w->hot_grad) return fail_arg("rg_ncf_apply: null scratch");
     if (opt->kind == RG_OPT_ADAM && (!m->user_w_m || !m->item_w_m)) return fail_arg("rg_ncf_apply: Adam needs m");
@@ -2642,7 +2715,7 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
     if (row_begin < 0) row_begin = 0;
     if (row_end < 0 || row_end > nrows) row_end = nrows;
     if (row_begin > row_end) return fail_arg("rg_ncf_apply: row_begin > row_end");
-    ApplyArgs a{};
+    a = ApplyArgs{};
     a.w_in[0] = m->user_w; a.w_in[1] = m->item_w;
     a.w_out[0] = m->user_w; a.w_out[1] = m->item_w;          // in place: no partner rows are read
     a.w_m[0] = m->user_w_m; a.w_m[1] = m->item_w_m; a.w_v[0] = m->user_w_v; a.w_v[1] = m->item_w_v;
@@ -2655,8 +2728,7 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
     a.contrib = contrib;
     a.contrib_stride = 2 * (int64_t)m->dim;
     a.has_bias = false;
-    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
-    return dispatch_dim(m->dim, f);
+    return RG_OK;
 }
 
 // Data-parallel NCF / NeuMF step (replicated, reference-exact): the embedding rows' data

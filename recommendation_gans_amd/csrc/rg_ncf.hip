@@ -26,6 +26,7 @@
 #include <utility>
 
 #include "rg_common.h"
+#include "rg_mlp_update.h"
 
 namespace rg {
 
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
                                                         int nparts, int P, rg_opt_t opt, const float *loss_partials,
                                                         int64_t n_partials, double inv_a, double inv_b,
                                                         float *loss_out, int mode, float *grad) {
-    __shared__ float red[kUpdWaves][64];
+    __shared__ float red[kMlpSlices][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (mode == 2) {
         const int e = blockIdx.x * 64 + lane;
@@ -729,43 +730,9 @@ __global__ __launch_bounds__(kUpdWaves * 64) void ncf_update_kernel(float *mlp, 
             if (mode == 1) grad[P] = lv;
         }
     }
-    const int e = blockIdx.x * 64 + lane;
-    const int q = (nparts + kUpdWaves - 1) / kUpdWaves, k0 = wave * q, k1 = min(nparts, k0 + q);
-    float g = 0.0f;
-    if (e < P) {
-        float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        int k = k0;
-        // batches of 16 partials: every load of a batch in flight before the (unchanged)
-        // four-chain sums consume them
-        for (; k + 16 <= k1; k += 16) {
-            float v[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = wpart[(int64_t)(k + q) * P + e];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) c[q & 3] += v[q];
-        }
-        for (; k + 4 <= k1; k += 4) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) c[j] += wpart[(int64_t)(k + j) * P + e];
-        }
-        for (; k < k1; ++k) c[0] += wpart[(int64_t)k * P + e];
-        g = (c[0] + c[1]) + (c[2] + c[3]);
-    }
-    red[wave][lane] = g;
-    __syncthreads();
-    if (wave != 0 || e >= P) return;
-    g = red[0][lane];
-#pragma unroll
-    for (int w = 1; w < kUpdWaves; ++w) g += red[w][lane];
-    if (mode == 1) {
-        grad[e] = g;
-        return;
-    }
-    float mm = m ? m[e] : 0.0f, vv = v ? v[e] : 0.0f;
-    const float p = opt_update(opt, mlp[e], g, mm, vv);
-    mlp[e] = p;
-    if (m) m[e] = mm;
-    if (v) v[e] = vv;
+    static_assert(kUpdWaves == kMlpSlices, "one slice per wave");
+    const MlpUpdArgs u{mlp, m, v, wpart, nparts, P, opt, mode, grad};
+    mlp_update_block<kUpdWaves>(u, blockIdx.x, red);
 }
 
 // adaptive hinge from forward-only scores: dp of every row (positives: hinge

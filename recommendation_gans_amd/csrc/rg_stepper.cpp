@@ -1584,6 +1584,32 @@ extern "C" int rg_mf_stepper_prefetch_inline(void *h, void *stream, const rg_mf_
     return prepare_inline(*st, (hipStream_t)stream, st->taken, *next);
 }
 
+// prefetch_inline's bookkeeping without its launch: the caller launches the prepare of the
+// returned batch / work on `stream` itself, inside another kernel (rg_ncf_tail).
+// Returns 1 when a prepare is to be launched, 0 when the unit is already prepared.
+extern "C" int rg_mf_stepper_prefetch_args(void *h, void *stream, const rg_mf_step_in_t *next,
+                                           rg_mf_batch_t *batch_out, rg_mf_work_t *work_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !next || !batch_out || !work_out) return rg::fail_arg("rg_mf_stepper_prefetch_args: null argument");
+    if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next) && !st->prep_claimed) return 0;
+    const int64_t unit = st->taken;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = keep_ahead(*st, unit);
+    if (rc) return rc;
+    const int b = (int)(unit % 2);
+    if ((rc = wait_side(*st, s, b))) return rc;   // an earlier side write of this buffer
+    if ((rc = wait_words(*st, s, unit))) return rc;
+    *work_out = work_for(*st, *next);
+    *batch_out = make_batch(*st, *next, unit);
+    st->side_pending[b] = false;
+    st->prepared = true;
+    st->prep_unit = unit;
+    st->prep_in = *next;
+    st->prep_serial = 0;
+    st->prep_claimed = false;
+    return 1;
+}
+
 extern "C" int rg_mf_stepper_opt(void *h, int64_t step, rg_opt_t *out) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !out) return rg::fail_arg("rg_mf_stepper_opt: null argument");

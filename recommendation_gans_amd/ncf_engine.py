@@ -302,16 +302,27 @@ class NCFEngine:
         out = self.loss_out if loss_out is None else loss_out
         if self.world > 1:
             return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce, next_step)
-        check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
-                                     ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
-              "rg_ncf_update")
-        if self.neumf:
+        if not self.neumf:
+            # one launch: the next step's prepare, the MLP update (with the loss) and the
+            # embedding update (rg_ncf_tail; the same sums as the three separate calls)
+            nb, nwk, need = _lib.MFBatch(), _lib.MFWork(), 0
+            if next_step is not None and not self._prefetch_side:
+                need = self.lib.rg_mf_stepper_prefetch_args(self._stepper, stream, ctypes.byref(self._next_in),
+                                                            ctypes.byref(nb), ctypes.byref(nwk))
+                if need < 0:
+                    check(need, "rg_mf_stepper_prefetch_args")
+            check(self.lib.rg_ncf_tail(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
+                                       self.blocks, ctypes.byref(o), ptr(parts),
+                                       ctypes.byref(self._loss(global_pos, out)),
+                                       ctypes.byref(nb) if need else None, ctypes.byref(nwk) if need else None),
+                  "rg_ncf_tail")
+        else:
+            check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
+                                         ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
+                  "rg_ncf_update")
             check(self.lib.rg_neumf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
                                           ctypes.byref(o), 0, -1), "rg_neumf_apply")
-        else:
-            check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ptr(self.contrib),
-                                        ctypes.byref(o), 0, -1), "rg_ncf_apply")
-        self._prefetch_tail(next_step, stream)
+            self._prefetch_tail(next_step, stream)
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out
 
