@@ -127,6 +127,10 @@ class NCFEngine:
         self.t = 0
         self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
         self._prefetch_side = _lib.ab_build() and os.environ.get("RG_NCF_PREFETCH_SIDE") == "1"
+        # single-rank MLP towers: the step's tail in one launch (rg_ncf_tail); False runs the
+        # three separate calls it replaces (rg_ncf_update, rg_ncf_apply, the inline prefetch) --
+        # the same bits, checked by tests/test_ncf_gpu.py
+        self.fused_tail = True
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
                                     self.U, self.I, E, self.M)
@@ -302,7 +306,7 @@ class NCFEngine:
         out = self.loss_out if loss_out is None else loss_out
         if self.world > 1:
             return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce, next_step)
-        if not self.neumf:
+        if not self.neumf and self.fused_tail:
             # one launch: the next step's prepare, the MLP update (with the loss) and the
             # embedding update (rg_ncf_tail; the same sums as the three separate calls)
             nb, nwk, need = _lib.MFBatch(), _lib.MFWork(), 0
@@ -320,8 +324,12 @@ class NCFEngine:
             check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
                                          ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),
                   "rg_ncf_update")
-            check(self.lib.rg_neumf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
-                                          ctypes.byref(o), 0, -1), "rg_neumf_apply")
+            if self.neumf:
+                check(self.lib.rg_neumf_apply(stream, ctypes.byref(self._model), ctypes.byref(work),
+                                              ctypes.byref(nw), ctypes.byref(o), 0, -1), "rg_neumf_apply")
+            else:
+                check(self.lib.rg_ncf_apply(stream, ctypes.byref(self._model), ctypes.byref(work), nw.contrib,
+                                            ctypes.byref(o), 0, -1), "rg_ncf_apply")
             self._prefetch_tail(next_step, stream)
         check(self.lib.rg_mf_stepper_advance(self._stepper, 0, 1), "rg_mf_stepper_advance")
         return out

@@ -91,10 +91,9 @@ def test_ncf_device_dropout_trains():
 
 def test_prefetched_negatives_leave_the_trajectory_unchanged():
     """rg_mf_stepper_prefetch (next step's negatives prepared during this step's updates)
-    draws the same negatives (MT stream bit-exact) and gives the unprefetched trajectory:
-    losses and parameters within 1e-5 relative (a row's listed contributions are summed
-    in the order their slots were claimed by atomics, so repeated runs differ in the last
-    bits with or without prefetch)."""
+    draws the same negatives (MT stream bit-exact) and gives the unprefetched trajectory
+    bit for bit: a row's listed contributions are summed in sorted order and the overflow in
+    fixed point (round 2), so where the negatives were prepared cannot change a sum."""
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from oracle import rng as orng
     dev = torch.device("cuda:0")
@@ -127,9 +126,53 @@ def test_prefetched_negatives_leave_the_trajectory_unchanged():
         out.append((ls, [t.detach().cpu().clone() for t in e.params()], e.mt_state()))
     for m in (1, 2):
         assert (out[0][2] == out[m][2]).all()
-        np.testing.assert_allclose(out[m][0], out[0][0], rtol=1e-5)
+        assert out[m][0] == out[0][0], (m, out[m][0], out[0][0])
         for a, b in zip(out[0][1], out[m][1]):
-            assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-12
+            assert torch.equal(a, b), (m, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("loss,optimizer,E,U,I", [("pointwise", "adam", 64, 400, 300),
+                                                  ("bpr", "adam", 64, 40000, 30000),
+                                                  ("adaptive_hinge", "sgd", 16, 3000, 2000)])
+def test_fused_tail_matches_the_separate_calls(loss, optimizer, E, U, I):
+    """rg_ncf_tail (the next step's prepare, the MLP update with the loss and the embedding update
+    in one launch) against the three calls it replaces (rg_ncf_update, rg_ncf_apply,
+    rg_mf_stepper_prefetch_inline): losses, every parameter and the MT state bit for bit over
+    steps with and without a prefetched next batch -- small tables (every row's list overflows)
+    and large ones (mostly single contributions)."""
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from oracle import rng as orng
+    dev = torch.device("cuda:0")
+    B, n, steps = 512, 5, 4
+    torch.manual_seed(5)
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E) / E, torch.randn(I, E) / E]
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+        w = torch.empty(b_, a_)
+        torch.nn.init.xavier_uniform_(w)
+        params += [w, torch.full((b_,), 0.01)]
+    rs = np.random.RandomState(6)
+    pool_u, pool_i = rs.randint(0, U, 20000), rs.randint(0, I, 20000)
+    batches = [(torch.from_numpy(rs.randint(0, U, B)).to(dev), torch.from_numpy(rs.randint(0, I, B)).to(dev))
+               for _ in range(steps)]
+    out = []
+    for fused in (True, False):
+        e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, orng.py_seed_state(8), loss=loss,
+                      optimizer=optimizer, lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=9)
+        e.fused_tail = fused
+        plans = [e.make_plan(b[1]) for b in batches]
+        ls = []
+        for s, (u, i) in enumerate(batches):
+            # steps 0 and 2 hand over the next batch (prepared in the tail), 1 and 3 do not
+            nxt = (batches[s + 1][0], batches[s + 1][1], plans[s + 1]) if s % 2 == 0 else None
+            ls.append(float(e.train_step(u, i, plan=plans[s], next_step=nxt)[0]))
+        torch.cuda.synchronize()
+        out.append((ls, [t.detach().cpu().clone() for t in e.params()], e.mt_state()))
+    assert out[0][0] == out[1][0], (out[0][0], out[1][0])
+    assert all(np.isfinite(out[0][0]))
+    assert (out[0][2] == out[1][2]).all()
+    for k, (a, b) in enumerate(zip(out[0][1], out[1][1])):
+        assert torch.equal(a, b), (k, float((a - b).abs().max()))
 
 
 def test_ncf_rejects_the_positives_only_loss(tmp_path, monkeypatch):
