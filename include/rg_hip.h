@@ -545,7 +545,10 @@ typedef struct rg_mf_stepper_config {
     int32_t current_set;
     int32_t gen_mode;               /* 0: MT words walked inside the step's dense pass when that hides
                                        them (rg_mf_stepper_train); 1: the consumer has no such pass
-                                       (NCF / NeuMF): 8-step slots on the generator stream */
+                                       (NeuMF, data-parallel NCF): 8-step slots on the generator
+                                       stream; 2: the consumer's own tail launch walks them when
+                                       that hides them (single-GPU NCF: rg_mf_stepper_tail_gen +
+                                       rg_ncf_tail), otherwise as 1 */
     /* dp_mode 1: the replicated, reference-exact data-parallel step (rg_mf_grads_sharded ->
      * reduce-scatter -> rg_mf_apply_shard -> all-gather), rank `rank` of `world`; every rank
      * consumes columns [col_offset, col_offset + cols) of one global draw of global_cols
@@ -607,6 +610,11 @@ int rg_mf_stepper_prefetch_inline(void *stepper, void *stream, const rg_mf_step_
  * (rg_ncf_tail).  Returns 1 (launch it), 0 (already prepared) or an error status. */
 int rg_mf_stepper_prefetch_args(void *stepper, void *stream, const rg_mf_step_in_t *next, rg_mf_batch_t *batch_out,
                                 rg_mf_work_t *work_out);
+/* After a step's release, gen_mode 2: when the MT words of the unit after the next one are due,
+ * fills *gen_out with their walk -- which the caller enqueues on `stream` before any other
+ * work there (rg_ncf_tail's first workgroup) -- and returns 1; returns 0 (nothing to walk:
+ * *gen_out zeroed) or an error status. */
+int rg_mf_stepper_tail_gen(void *stepper, void *stream, rg_mt_gen_t *gen_out);
 /* The replicated data-parallel step (dp_mode 1) in two halves around a caller-run
  * exchange (comm == NULL; tests, gloo): dp_begin = prepare / pairs / release / the next
  * step's prepare / rg_mf_grads_sharded into grad_buf; the caller reduce-scatters grad_buf;
@@ -746,10 +754,11 @@ int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, 
 /* The tail of a single-GPU NCF step (MLP towers, mf_dim = 0) in ONE launch: the next step's
  * prepare (rg_mf_prepare of next / next_work; next = NULL: none), rg_ncf_update (the MLP
  * weight-gradient reduce + optimizer, with the step's loss) and rg_ncf_apply (every embedding
- * row's pull + optimizer) -- the same sums as the three separate calls. */
+ * row's pull + optimizer) -- the same sums as the three separate calls; gen (optional, from
+ * rg_mf_stepper_tail_gen): a later unit's MT walk in the launch's first workgroup. */
 int rg_ncf_tail(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
                 int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
-                const rg_mf_batch_t *next, const rg_mf_work_t *next_work);
+                const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mt_gen_t *gen);
 /* NeuMF (spotlight/dnn_models/neuMF.py:7-55): rg_ncf_pairs / rg_ncf_update run with
  * model->mf_dim > 0 (the affine_output sees cat(tower, U_mf[u] * I_mf[i])); this applies
  * the GMF tables, then the MLP tables (as rg_ncf_apply). */

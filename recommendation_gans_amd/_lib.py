@@ -225,7 +225,8 @@ SIGNATURES = [
                                     ctypes.c_void_p, ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_ncf_tail", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                    ctypes.POINTER(NCFWork), ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p,
-                                   ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
+                                   ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                   ctypes.POINTER(MTGen)]),
     ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                       ctypes.POINTER(NCFWork), ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_pool_build", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -235,6 +236,7 @@ SIGNATURES = [
     ("rg_mf_stepper_prefetch_inline", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn)]),
     ("rg_mf_stepper_prefetch_args", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                                    ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork)]),
+    ("rg_mf_stepper_tail_gen", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MTGen)]),
     ("rg_topk_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_void_p]),
     ("rg_mt_window_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

@@ -2660,11 +2660,18 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
 // (rg_ncf_update's reduction and optimizer, the same sums) with the step's loss, and the
 // embedding rows' update (rg_ncf_apply) -- three launches and their tails in one; the three
 // parts touch disjoint data.  MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply).
+// gen (optional, rg_mf_stepper_tail_gen): workgroup 0 walks a later step's MT words, as in the
+// MF split step's dense pass -- no generator-stream kernel beside the pair kernel.
 extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
                            int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
-                           const rg_mf_batch_t *next, const rg_mf_work_t *next_w) {
+                           const rg_mf_batch_t *next, const rg_mf_work_t *next_w, const rg_mt_gen_t *gen) {
     if (!m || !w || !nw || !opt || !nw->contrib || !nw->mlp_partials || !m->mlp)
         return fail_arg("rg_ncf_tail: null argument");
+    MtGenArgs g{};
+    if (gen && gen->nwords > 0) {
+        if (!gen->state || !gen->out) return fail_arg("rg_ncf_tail: null MT state / output");
+        g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
+    }
     if (m->mf_dim != 0) return fail_arg("rg_ncf_tail: MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply)");
     if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_tail: Adam needs m state");
     if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_tail: optimizer needs v state");
@@ -2699,7 +2706,7 @@ extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *
         prep_out = reinterpret_cast<int2 *>(next->pairs);
         prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
-    BackLaunchF f{&a, &prep, prep_out, prep_blocks, MtGenArgs{}, (hipStream_t)stream};
+    BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
     f.upd = &u;
     return dispatch_dim(m->dim, f);
 }

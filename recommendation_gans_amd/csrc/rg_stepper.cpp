@@ -415,7 +415,9 @@ int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t 
     if (rc) return rc;
     rc = lazy_flush(st, stream);          // external consumers read every row
     if (rc) return rc;
-    rc = keep_ahead(st, unit);
+    // the consumer's tail walks (gen_mode 2): only a missing slot on the generator stream
+    // (running ahead there would leave the in-launch walks nothing to do)
+    rc = st.inline_gen && st.cfg.gen_mode == 2 ? generate_upto(st, unit, 0) : keep_ahead(st, unit);
     if (rc) return rc;
     // an external consumer's pair pass claims in cfg.work.row_count (= counts[0]) by itself
     if ((rc = clean_counts(st, stream, 0))) return rc;
@@ -1287,8 +1289,9 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         // RG_MT_INLINE: 0 off, 1 (default) when it hides, 2 always (tests at small sizes)
         const char *im = getenv("RG_MT_INLINE");
         const int mode = im ? atoi(im) : 1;
+        // gen_mode 2: the consumer's tail launch walks (rg_mf_stepper_tail_gen), under the same test
         st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
-                         (cfg->gen_mode == 0 || mode == 2) &&
+                         (cfg->gen_mode == 0 || cfg->gen_mode == 2 || mode == 2) &&
                          cfg->dp_mode == 0 && (mode == 2 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
         st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
@@ -1594,7 +1597,7 @@ extern "C" int rg_mf_stepper_prefetch_args(void *h, void *stream, const rg_mf_st
     if (st->prepared && st->prep_unit == st->taken && same_input(st->prep_in, *next) && !st->prep_claimed) return 0;
     const int64_t unit = st->taken;
     hipStream_t s = (hipStream_t)stream;
-    int rc = keep_ahead(*st, unit);
+    int rc = st->inline_gen ? generate_upto(*st, unit, 0) : keep_ahead(*st, unit);
     if (rc) return rc;
     const int b = (int)(unit % 2);
     if ((rc = wait_side(*st, s, b))) return rc;   // an earlier side write of this buffer
@@ -1607,6 +1610,25 @@ extern "C" int rg_mf_stepper_prefetch_args(void *h, void *stream, const rg_mf_st
     st->prep_in = *next;
     st->prep_serial = 0;
     st->prep_claimed = false;
+    return 1;
+}
+
+// gen_mode 2 (single-GPU NCF): the walk of unit taken + 1 -- two after the step just released --
+// rides in the caller's tail launch on `stream`, as the MF split step's dense pass carries it
+extern "C" int rg_mf_stepper_tail_gen(void *h, void *stream, rg_mt_gen_t *gen_out) {
+    Stepper *st = static_cast<Stepper *>(h);
+    if (!st || !gen_out) return rg::fail_arg("rg_mf_stepper_tail_gen: null argument");
+    *gen_out = rg_mt_gen_t{};
+    if (!st->inline_gen || st->cfg.gen_mode != 2 || st->gen_slots != rel_slot(*st, st->taken + 1)) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int slot = (int)(st->gen_slots % kSlots);
+    int rc = begin_production(*st, s, slot);
+    if (rc) return rc;
+    gen_out->state = st->cfg.mt_state;
+    gen_out->out = st->words[slot];
+    gen_out->state_before = st->start_state[slot];
+    gen_out->nwords = st->G * st->W;
+    end_production(*st, s, slot);    // the caller's launch is the next work on `stream`
     return 1;
 }
 

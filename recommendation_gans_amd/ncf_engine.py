@@ -153,9 +153,14 @@ class NCFEngine:
         cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, self.rank * B, B * self.world, B * self.world
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
-        # no fused dense pass walks the MT words here: 8-step slots on the generator stream (one
-        # walk and one cross-stream hop per 8 steps instead of per step)
-        cfg.gen_mode = 0 if _lib.ab_build() and os.environ.get("RG_NCF_GEN_INLINE") == "1" else 1
+        # single-GPU MLP towers: the step's tail launch (rg_ncf_tail) walks the MT words two steps
+        # ahead in its first workgroup, as the MF split step's dense pass does (gen_mode 2: no
+        # generator-stream kernel beside the pair kernel); NeuMF and data-parallel steps have no
+        # such launch: 8-step slots on the generator stream (one walk and one hop per 8 steps)
+        if _lib.ab_build() and os.environ.get("RG_NCF_GEN_INLINE") == "1":
+            cfg.gen_mode = 0
+        else:
+            cfg.gen_mode = 2 if (self.world == 1 and not self.neumf) else 1
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())
@@ -309,16 +314,20 @@ class NCFEngine:
         if not self.neumf and self.fused_tail:
             # one launch: the next step's prepare, the MLP update (with the loss) and the
             # embedding update (rg_ncf_tail; the same sums as the three separate calls)
-            nb, nwk, need = _lib.MFBatch(), _lib.MFWork(), 0
+            nb, nwk, need, gen = _lib.MFBatch(), _lib.MFWork(), 0, _lib.MTGen()
             if next_step is not None and not self._prefetch_side:
                 need = self.lib.rg_mf_stepper_prefetch_args(self._stepper, stream, ctypes.byref(self._next_in),
                                                             ctypes.byref(nb), ctypes.byref(nwk))
                 if need < 0:
                     check(need, "rg_mf_stepper_prefetch_args")
+            walk = self.lib.rg_mf_stepper_tail_gen(self._stepper, stream, ctypes.byref(gen))
+            if walk < 0:
+                check(walk, "rg_mf_stepper_tail_gen")
             check(self.lib.rg_ncf_tail(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
                                        self.blocks, ctypes.byref(o), ptr(parts),
                                        ctypes.byref(self._loss(global_pos, out)),
-                                       ctypes.byref(nb) if need else None, ctypes.byref(nwk) if need else None),
+                                       ctypes.byref(nb) if need else None, ctypes.byref(nwk) if need else None,
+                                       ctypes.byref(gen) if walk else None),
                   "rg_ncf_tail")
         else:
             check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
