@@ -751,7 +751,8 @@ int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *model, const float *g
 /* Embedding rows [row_begin, row_end) (users then items): pull + optimizer, in place. */
 int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const float *contrib,
                  const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
-/* The tail of a single-GPU NCF step (MLP towers, mf_dim = 0) in ONE launch: the next step's
+/* The tail of a single-GPU NCF / NeuMF step in ONE launch (NeuMF: after its GMF tables' pass,
+ * a launch of its own, as in rg_neumf_apply): the next step's
  * prepare (rg_mf_prepare of next / next_work; next = NULL: none), rg_ncf_update (the MLP
  * weight-gradient reduce + optimizer, with the step's loss) and rg_ncf_apply (every embedding
  * row's pull + optimizer) -- the same sums as the three separate calls; gen (optional, from

@@ -2645,6 +2645,8 @@ extern "C" int rg_mf_step_hot(void *stream, const rg_mf_tables_t *t, const rg_mf
 
 static int ncf_apply_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib, const rg_opt_t *opt,
                           int64_t row_begin, int64_t row_end, ApplyArgs &a);
+static int neumf_gmf_pass(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
 
 extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib,
                             const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
@@ -2659,7 +2661,8 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
 // prepare (next = NULL: none), the MLP update from the pair kernel's weight-gradient partials
 // (rg_ncf_update's reduction and optimizer, the same sums) with the step's loss, and the
 // embedding rows' update (rg_ncf_apply) -- three launches and their tails in one; the three
-// parts touch disjoint data.  MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply).
+// parts touch disjoint data.  NeuMF (mf_dim > 0): the GMF tables' pass runs first, in a launch
+// of its own (it keeps the per-row counts the MLP tables' pass then consumes), as rg_neumf_apply.
 // gen (optional, rg_mf_stepper_tail_gen): workgroup 0 walks a later step's MT words, as in the
 // MF split step's dense pass -- no generator-stream kernel beside the pair kernel.
 extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
@@ -2672,15 +2675,15 @@ extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *
         if (!gen->state || !gen->out) return fail_arg("rg_ncf_tail: null MT state / output");
         g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
     }
-    if (m->mf_dim != 0) return fail_arg("rg_ncf_tail: MLP towers only (NeuMF: rg_ncf_update + rg_neumf_apply)");
     if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_tail: Adam needs m state");
     if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_tail: optimizer needs v state");
-    const int64_t P = rg_ncf_mlp_len(m->dim);
-    if (P < 0 || nparts < 1) return fail_arg("rg_ncf_tail: bad dim / partial count");
+    const int64_t P = m->mf_dim == 0 ? rg_ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
+    if (P < 0 || nparts < 1) return fail_arg("rg_ncf_tail: bad dim / mf_dim / partial count");
     if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_tail: loss needs partials");
     ApplyArgs a{};
     int rc = ncf_apply_args(m, w, nw->contrib, opt, 0, -1, a);
     if (rc) return rc;
+    if (m->mf_dim != 0 && (rc = neumf_gmf_pass(stream, m, w, nw, opt, 0, -1))) return rc;
     if (loss && loss->out) {   // finalized by the dense blocks' first workgroup (rg_ncf_update's sums)
         a.partials = loss_partials;
         a.n_partials = loss->n_partials;
@@ -2804,8 +2807,10 @@ extern "C" int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *m, const f
 // NeuMF (spotlight/dnn_models/neuMF.py:7-55): the GMF tables take their gradient rows
 // from ncf_work->mf_contrib through the same per-row lists (kept), then the MLP tables
 // pull theirs and reset the lists (rg_ncf_apply).
-extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
-                              const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+// NeuMF's GMF tables: pull + optimizer through the same per-row lists, keeping the counts for
+// the MLP tables' pass that follows (rg_ncf_apply or rg_ncf_tail resets them)
+static int neumf_gmf_pass(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
     if (!m || !w || !nw || !opt) return fail_arg("rg_neumf_apply: null argument");
     if (m->mf_dim < 1 || m->mf_dim > RG_NEUMF_MAX_MF_DIM) return fail_arg("rg_neumf_apply: mf_dim out of range");
     if (!m->mf_user_w || !m->mf_item_w || !nw->mf_contrib || !nw->mf_hot_grad)
@@ -2832,7 +2837,12 @@ extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_
     a.has_bias = false;
     a.keep_count = true;
     ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
-    int rc = dispatch_dim(m->mf_dim, f);
+    return dispatch_dim(m->mf_dim, f);
+}
+
+extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                              const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+    const int rc = neumf_gmf_pass(stream, m, w, nw, opt, row_begin, row_end);
     if (rc) return rc;
     return rg_ncf_apply(stream, m, w, nw->contrib, opt, row_begin, row_end);
 }

@@ -127,9 +127,9 @@ class NCFEngine:
         self.t = 0
         self.kernel_events = None     # optional (start, end) torch.cuda.Event pair around rg_ncf_pairs
         self._prefetch_side = _lib.ab_build() and os.environ.get("RG_NCF_PREFETCH_SIDE") == "1"
-        # single-rank MLP towers: the step's tail in one launch (rg_ncf_tail); False runs the
-        # three separate calls it replaces (rg_ncf_update, rg_ncf_apply, the inline prefetch) --
-        # the same bits, checked by tests/test_ncf_gpu.py
+        # single rank: the step's tail in one launch (rg_ncf_tail); False runs the three separate
+        # calls it replaces (rg_ncf_update, rg_ncf_apply / rg_neumf_apply, the inline prefetch)
+        # -- the same bits, checked by tests/test_ncf_gpu.py
         self.fused_tail = True
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
@@ -153,14 +153,16 @@ class NCFEngine:
         cfg.cols, cfg.col_offset, cfg.global_cols, cfg.neg_cols = B, self.rank * B, B * self.world, B * self.world
         cfg.opt = self._opt_base()
         cfg.lr_d, cfg.beta1_d, cfg.beta2_d = float(lr), float(betas[0]), float(betas[1])
-        # single-GPU MLP towers: the step's tail launch (rg_ncf_tail) walks the MT words two steps
-        # ahead in its first workgroup, as the MF split step's dense pass does (gen_mode 2: no
-        # generator-stream kernel beside the pair kernel); NeuMF and data-parallel steps have no
-        # such launch: 8-step slots on the generator stream (one walk and one hop per 8 steps)
+        # single GPU: the step's tail launch (rg_ncf_tail) walks the MT words two steps ahead in
+        # its first workgroup, as the MF split step's dense pass does (gen_mode 2: no
+        # generator-stream kernel beside the pair kernel) when the launch hides the walk (the
+        # stepper's test: the E = 64 tower's tables do, NeuMF's E = 16 ones do not); the
+        # data-parallel step has no such launch: 8-step slots on the generator stream (one walk
+        # and one hop per 8 steps)
         if _lib.ab_build() and os.environ.get("RG_NCF_GEN_INLINE") == "1":
             cfg.gen_mode = 0
         else:
-            cfg.gen_mode = 2 if (self.world == 1 and not self.neumf) else 1
+            cfg.gen_mode = 2 if self.world == 1 else 1
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())
@@ -311,7 +313,7 @@ class NCFEngine:
         out = self.loss_out if loss_out is None else loss_out
         if self.world > 1:
             return self._dp_update(work, nw, o, parts, global_pos, out, stream, allreduce, next_step)
-        if not self.neumf and self.fused_tail:
+        if self.fused_tail:
             # one launch: the next step's prepare, the MLP update (with the loss) and the
             # embedding update (rg_ncf_tail; the same sums as the three separate calls)
             nb, nwk, need, gen = _lib.MFBatch(), _lib.MFWork(), 0, _lib.MTGen()

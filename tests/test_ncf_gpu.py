@@ -131,15 +131,18 @@ def test_prefetched_negatives_leave_the_trajectory_unchanged():
             assert torch.equal(a, b), (m, float((a - b).abs().max()))
 
 
-@pytest.mark.parametrize("loss,optimizer,E,U,I", [("pointwise", "adam", 64, 400, 300),
-                                                  ("bpr", "adam", 64, 40000, 30000),
-                                                  ("adaptive_hinge", "sgd", 16, 3000, 2000)])
-def test_fused_tail_matches_the_separate_calls(loss, optimizer, E, U, I):
-    """rg_ncf_tail (the next step's prepare, the MLP update with the loss and the embedding update
-    in one launch) against the three calls it replaces (rg_ncf_update, rg_ncf_apply,
-    rg_mf_stepper_prefetch_inline): losses, every parameter and the MT state bit for bit over
-    steps with and without a prefetched next batch -- small tables (every row's list overflows)
-    and large ones (mostly single contributions)."""
+@pytest.mark.parametrize("loss,optimizer,E,M,U,I", [("pointwise", "adam", 64, 0, 400, 300),
+                                                    ("bpr", "adam", 64, 0, 40000, 30000),
+                                                    ("adaptive_hinge", "sgd", 16, 0, 3000, 2000),
+                                                    ("pointwise", "adam", 16, 50, 40000, 30000),
+                                                    ("hinge", "rms", 32, 20, 60, 25)])
+def test_fused_tail_matches_the_separate_calls(loss, optimizer, E, M, U, I):
+    """rg_ncf_tail (the next step's prepare, the MLP update with the loss, the embedding update
+    and, when due, the MT walk in one launch; NeuMF's GMF pass before it) against the calls it
+    replaces (rg_ncf_update, rg_ncf_apply / rg_neumf_apply, rg_mf_stepper_prefetch_inline, the
+    generator-stream walk): losses, every parameter and the MT state bit for bit over steps with
+    and without a prefetched next batch -- small tables (every row's list overflows) and large
+    ones (mostly single contributions); NCF towers (M = 0) and NeuMF (M > 0)."""
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from oracle import rng as orng
     dev = torch.device("cuda:0")
@@ -147,7 +150,10 @@ def test_fused_tail_matches_the_separate_calls(loss, optimizer, E, U, I):
     torch.manual_seed(5)
     sizes = oncf.layer_sizes(E)
     params = [torch.randn(U, E) / E, torch.randn(I, E) / E]
-    for a_, b_ in zip(sizes[:-1] + [sizes[-1]], sizes[1:] + [1]):
+    extra = {}
+    if M:
+        extra = dict(mf_user_w=torch.randn(U, M) / M, mf_item_w=torch.randn(I, M) / M)
+    for a_, b_ in zip(sizes[:-1] + [sizes[-1] + M], sizes[1:] + [1]):
         w = torch.empty(b_, a_)
         torch.nn.init.xavier_uniform_(w)
         params += [w, torch.full((b_,), 0.01)]
@@ -158,7 +164,8 @@ def test_fused_tail_matches_the_separate_calls(loss, optimizer, E, U, I):
     out = []
     for fused in (True, False):
         e = NCFEngine(params[0], params[1], params[2:], pool_u, pool_i, orng.py_seed_state(8), loss=loss,
-                      optimizer=optimizer, lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=9)
+                      optimizer=optimizer, lr=1e-2, weight_decay=1e-5, n_neg=n, batch_size=B, device=dev, seed=9,
+                      **extra)
         e.fused_tail = fused
         plans = [e.make_plan(b[1]) for b in batches]
         ls = []
