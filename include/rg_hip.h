@@ -548,7 +548,8 @@ typedef struct rg_mf_stepper_config {
                                        (NeuMF, data-parallel NCF): 8-step slots on the generator
                                        stream; 2: the consumer's own tail launch walks them when
                                        that hides them (single-GPU NCF: rg_mf_stepper_tail_gen +
-                                       rg_ncf_tail), otherwise as 1 */
+                                       rg_ncf_tail), otherwise as 1; 3: as 2 without the stepper's
+                                       test, made by the caller (NeuMF: the GMF tables' pass) */
     /* dp_mode 1: the replicated, reference-exact data-parallel step (rg_mf_grads_sharded ->
      * reduce-scatter -> rg_mf_apply_shard -> all-gather), rank `rank` of `world`; every rank
      * consumes columns [col_offset, col_offset + cols) of one global draw of global_cols
@@ -610,7 +611,7 @@ int rg_mf_stepper_prefetch_inline(void *stepper, void *stream, const rg_mf_step_
  * (rg_ncf_tail).  Returns 1 (launch it), 0 (already prepared) or an error status. */
 int rg_mf_stepper_prefetch_args(void *stepper, void *stream, const rg_mf_step_in_t *next, rg_mf_batch_t *batch_out,
                                 rg_mf_work_t *work_out);
-/* After a step's release, gen_mode 2: when the MT words of the unit after the next one are due,
+/* After a step's release, gen_mode 2 / 3: when the MT words of the unit after the next one are due,
  * fills *gen_out with their walk -- which the caller enqueues on `stream` before any other
  * work there (rg_ncf_tail's first workgroup) -- and returns 1; returns 0 (nothing to walk:
  * *gen_out zeroed) or an error status. */

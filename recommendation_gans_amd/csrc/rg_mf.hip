@@ -2646,7 +2646,7 @@ extern "C" int rg_mf_step_hot(void *stream, const rg_mf_tables_t *t, const rg_mf
 static int ncf_apply_args(const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib, const rg_opt_t *opt,
                           int64_t row_begin, int64_t row_end, ApplyArgs &a);
 static int neumf_gmf_pass(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
-                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end);
+                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end, const MtGenArgs &gen);
 
 extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const float *contrib,
                             const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
@@ -2683,7 +2683,12 @@ extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *
     ApplyArgs a{};
     int rc = ncf_apply_args(m, w, nw->contrib, opt, 0, -1, a);
     if (rc) return rc;
-    if (m->mf_dim != 0 && (rc = neumf_gmf_pass(stream, m, w, nw, opt, 0, -1))) return rc;
+    // NeuMF: the GMF tables' pass first; the walk (if any) rides in that launch -- the longer of
+    // the two passes at the reference's sizes (mf 50 vs mlp 16 floats per row)
+    if (m->mf_dim != 0) {
+        if ((rc = neumf_gmf_pass(stream, m, w, nw, opt, 0, -1, g))) return rc;
+        g = MtGenArgs{};
+    }
     if (loss && loss->out) {   // finalized by the dense blocks' first workgroup (rg_ncf_update's sums)
         a.partials = loss_partials;
         a.n_partials = loss->n_partials;
@@ -2810,7 +2815,7 @@ extern "C" int rg_ncf_apply_dense(void *stream, const rg_ncf_model_t *m, const f
 // NeuMF's GMF tables: pull + optimizer through the same per-row lists, keeping the counts for
 // the MLP tables' pass that follows (rg_ncf_apply or rg_ncf_tail resets them)
 static int neumf_gmf_pass(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
-                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
+                          const rg_opt_t *opt, int64_t row_begin, int64_t row_end, const MtGenArgs &gen) {
     if (!m || !w || !nw || !opt) return fail_arg("rg_neumf_apply: null argument");
     if (m->mf_dim < 1 || m->mf_dim > RG_NEUMF_MAX_MF_DIM) return fail_arg("rg_neumf_apply: mf_dim out of range");
     if (!m->mf_user_w || !m->mf_item_w || !nw->mf_contrib || !nw->mf_hot_grad)
@@ -2836,13 +2841,18 @@ static int neumf_gmf_pass(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w
     a.contrib_stride = 2 * (int64_t)m->mf_dim;
     a.has_bias = false;
     a.keep_count = true;
+    if (gen.nwords > 0) {   // with an MT walk: mf_back_kernel's grid (walk block + the same pull)
+        PairsArgs prep{};
+        BackLaunchF f{&a, &prep, nullptr, 0, gen, (hipStream_t)stream};
+        return dispatch_dim(m->mf_dim, f);
+    }
     ApplyLaunchF f{&a, (hipStream_t)stream, kApplyPull};
     return dispatch_dim(m->mf_dim, f);
 }
 
 extern "C" int rg_neumf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
                               const rg_opt_t *opt, int64_t row_begin, int64_t row_end) {
-    const int rc = neumf_gmf_pass(stream, m, w, nw, opt, row_begin, row_end);
+    const int rc = neumf_gmf_pass(stream, m, w, nw, opt, row_begin, row_end, MtGenArgs{});
     if (rc) return rc;
     return rg_ncf_apply(stream, m, w, nw->contrib, opt, row_begin, row_end);
 }

@@ -417,7 +417,7 @@ int acquire(Stepper &st, hipStream_t stream, const rg_mf_step_in_t &in, int64_t 
     if (rc) return rc;
     // the consumer's tail walks (gen_mode 2): only a missing slot on the generator stream
     // (running ahead there would leave the in-launch walks nothing to do)
-    rc = st.inline_gen && st.cfg.gen_mode == 2 ? generate_upto(st, unit, 0) : keep_ahead(st, unit);
+    rc = st.inline_gen && st.cfg.gen_mode >= 2 ? generate_upto(st, unit, 0) : keep_ahead(st, unit);
     if (rc) return rc;
     // an external consumer's pair pass claims in cfg.work.row_count (= counts[0]) by itself
     if ((rc = clean_counts(st, stream, 0))) return rc;
@@ -1289,10 +1289,12 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         // RG_MT_INLINE: 0 off, 1 (default) when it hides, 2 always (tests at small sizes)
         const char *im = getenv("RG_MT_INLINE");
         const int mode = im ? atoi(im) : 1;
-        // gen_mode 2: the consumer's tail launch walks (rg_mf_stepper_tail_gen), under the same test
+        // gen_mode 2: the consumer's tail launch walks (rg_mf_stepper_tail_gen), under the same test;
+        // 3: the same, the caller having made the test against a pass these tables do not show
+        // (NeuMF's GMF tables)
         st->inline_gen = mode != 0 && !st->fused && !env_flag("RG_MT_JUMP", false) && !cfg->item_grad &&
-                         (cfg->gen_mode == 0 || cfg->gen_mode == 2 || mode == 2) &&
-                         cfg->dp_mode == 0 && (mode == 2 || walk_us <= 0.85 * dense_us);
+                         (cfg->gen_mode == 0 || cfg->gen_mode >= 2 || mode == 2) &&
+                         cfg->dp_mode == 0 && (mode == 2 || cfg->gen_mode == 3 || walk_us <= 0.85 * dense_us);
         const char *g = getenv("RG_MT_UNITS");
         st->G = st->inline_gen ? 1 : (g ? atoi(g) : 8);
         if (st->G < 1) st->G = 1;
@@ -1619,7 +1621,7 @@ extern "C" int rg_mf_stepper_tail_gen(void *h, void *stream, rg_mt_gen_t *gen_ou
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !gen_out) return rg::fail_arg("rg_mf_stepper_tail_gen: null argument");
     *gen_out = rg_mt_gen_t{};
-    if (!st->inline_gen || st->cfg.gen_mode != 2 || st->gen_slots != rel_slot(*st, st->taken + 1)) return 0;
+    if (!st->inline_gen || st->cfg.gen_mode < 2 || st->gen_slots != rel_slot(*st, st->taken + 1)) return 0;
     hipStream_t s = (hipStream_t)stream;
     const int slot = (int)(st->gen_slots % kSlots);
     int rc = begin_production(*st, s, slot);

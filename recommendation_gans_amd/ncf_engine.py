@@ -163,6 +163,13 @@ class NCFEngine:
             cfg.gen_mode = 0
         else:
             cfg.gen_mode = 2 if self.world == 1 else 1
+            if self.world == 1 and self.neumf:
+                # NeuMF: the walk rides in the GMF tables' launch when that pass hides it (the
+                # stepper's test, rg_stepper.cpp, against the GMF rows instead of the MLP ones, at
+                # the ~4.5 TB/s the odd-width 16-lane rows stream at: 42 us for mf 50 on ML-20M)
+                walk_us = 0.47e-3 * 2 * n * B
+                gmf_us = 6.0 * (self.U + self.I) * 4.0 * self.M / 4.5e6
+                cfg.gen_mode = 3 if walk_us <= gmf_us else 2
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
             raise RuntimeError("rg_mf_stepper_create: " + lib.rg_last_error().decode())
