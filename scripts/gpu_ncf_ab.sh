@@ -1,6 +1,7 @@
 # GPU box: same-box A/B of the E = 64 NCF wave kernel's tile height (32 rows: the product; 48
 # rows: variant ncf48, -DRG_NCF_WAVE_ROWS=48), interleaved, with the NCF tests against the
-# 48-row build first.
+# 48-row build first.  Build the variant here first (it is not kept in the tree):
+#   python -m recommendation_gans_amd.build --variant ncf48 -DRG_NCF_WAVE_ROWS=48
 set -o pipefail
 mkdir -p gpurun_out
 RG_LIB=recommendation_gans_amd/_variants/librg_hip_ncf48.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 \
