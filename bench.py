@@ -755,10 +755,19 @@ def main():
     if multi:
         dist.barrier()
     el = time.perf_counter() - t0
+    rccl = None
     if multi:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        # every rank's own time and what its native communicator reports (ncclCommCount /
+        # ncclCommUserRank): the line shows the ranks RCCL itself saw, not only WORLD_SIZE
+        cnt, urank, is_rccl = comm.info() if comm is not None else (world, rank, False)
+        mine = torch.tensor([el, float(cnt), float(urank), float(is_rccl)], dtype=torch.float64, device=dev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        allv = [v.tolist() for v in allv]
+        el = max(v[0] for v in allv)
+        rccl = {"comm_count": sorted({int(v[1]) for v in allv}), "user_ranks": [int(v[2]) for v in allv],
+                "native_rccl": all(v[3] > 0 for v in allv),
+                "per_rank_ms_per_step": [v[0] / args.steps * 1e3 for v in allv]}
     loss_last = float(eng.loss_out[0])
     if getattr(eng, "pipelined", False) and eng.pipe_error():
         raise RuntimeError("pipelined MF step: a pair workgroup's bounded wait ran out (results invalid)")
@@ -797,6 +806,8 @@ def main():
                "plan_build_note": f"item-sorted plans of all {nbatches} batches of an epoch in one HIP launch "
                                   "(rg_mf_plans_build), built once per fit (the reference shuffles once, "
                                   "implicit.py:262); not in the timed region"}
+        if rccl is not None:
+            out["rccl"] = rccl
         step_bytes = gather + ids + adam
         out["step_roofline"] = {"bytes_per_step": step_bytes,
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,

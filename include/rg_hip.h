@@ -311,7 +311,9 @@ int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *tables, rg_mf_wo
                             int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
                             const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mt_gen_t *gen);
 
-/* Pipelined single-GPU step (the stepper's default): ONE launch that runs
+/* Pipelined single-GPU step (A/B build only, -DRG_AB=1: measured 4x slower than the split
+ * step; the product library refuses it and the stepper never selects it): ONE
+ * launch that runs
  *   the dense update of step t (tables t -> tables' out set, as rg_mf_apply),
  *   the pair pass of step t+1 (pair_b / pair_w, prepared with claimed slots; it reads the
  *     rows this launch writes and waits, in the launch, until every row it reads is written),
@@ -502,6 +504,10 @@ typedef int (*rg_host_allreduce_fn)(void *ctx, float *host_buf, int64_t n);
 void *rg_comm_create_host(int32_t world, int32_t rank, int32_t device, int64_t max_floats,
                           rg_host_allreduce_fn fn, void *ctx);
 int rg_comm_destroy(void *comm);
+/* What the native communicator reports: ncclCommCount / ncclCommUserRank of an RCCL
+ * communicator (is_rccl = 1), or the configured world / rank of a local / host-staged stand-in
+ * (is_rccl = 0). */
+int rg_comm_info(void *comm, int32_t *count, int32_t *user_rank, int32_t *is_rccl);
 /* In-place sum over ranks, stream-ordered with respect to `stream` (runs on the
  * communicator's own stream between two events). */
 int rg_comm_allreduce_sum_f32(void *comm, void *stream, float *buf_dev, int64_t n);
@@ -704,8 +710,11 @@ int64_t rg_ncf_mlp_len(int32_t dim);
 /* NeuMF flat parameters (tower layers, then affine_output (1 x (8 + M)) and its bias) */
 int64_t rg_neumf_param_len(int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_mask_units(int32_t dim);
-/* Tile geometry of a model: rows per tile (48 for the E = 64 MLP's wave kernel, 32 for the
- * other towers and NeuMF), columns per tile (also the plan's units per block), tiles. */
+/* Tile geometry of a model: rows per tile (32 for every tower in the product build, the E = 64
+ * MLP's wave kernel included; the 48-row wave tile exists only in the ncf48 A/B variant built
+ * with -DRG_NCF_WAVE_ROWS=48), columns per tile (also the plan's units per block), tiles.
+ * ABI 2 (rg_version "abi=2"): these three take (dim, mf_dim) / (n_neg, dim, mf_dim) /
+ * (cols, n_neg, dim, mf_dim); ABI 1 took fewer arguments. */
 int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_cols_per_tile(int32_t n_neg, int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_tiles(int64_t cols, int32_t n_neg, int32_t dim, int32_t mf_dim);
@@ -761,6 +770,12 @@ int rg_ncf_apply(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, 
 int rg_ncf_tail(void *stream, const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
                 int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
                 const rg_mf_batch_t *next, const rg_mf_work_t *next_work, const rg_mt_gen_t *gen);
+/* Every check rg_ncf_tail makes that does not depend on the stepper's outputs (next, gen), with no
+ * launch: call it BEFORE rg_mf_stepper_prefetch_args / rg_mf_stepper_tail_gen, which commit the
+ * next unit and the MT ring slot, so a tail that would be refused never leaves the stepper holding
+ * a prepare or a walk that was not launched.  RG_OK or the status rg_ncf_tail would return. */
+int rg_ncf_tail_validate(const rg_ncf_model_t *model, rg_mf_work_t *work, const rg_ncf_work_t *ncf_work,
+                         int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss);
 /* NeuMF (spotlight/dnn_models/neuMF.py:7-55): rg_ncf_pairs / rg_ncf_update run with
  * model->mf_dim > 0 (the affine_output sees cat(tower, U_mf[u] * I_mf[i])); this applies
  * the GMF tables, then the MLP tables (as rg_ncf_apply). */

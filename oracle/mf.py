@@ -247,9 +247,14 @@ class MFOracle:
 
     def __init__(self, U, I, ub, ib, pool_u, pool_i, mt_state, loss="pointwise",
                  optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=5, batch_size=256,
-                 betas=(0.5, 0.999), python_sampler=False, noise=False):
+                 betas=(0.5, 0.999), python_sampler=False, noise=False, order_seed=None):
         assert loss in LOSSES
         self.params = [U, I, ub, ib]
+        # order_seed: a second fp32 restatement of the same step whose gradient sums take the
+        # pairs in a seeded permuted order (torch's index_add_ sums them in pair order): how far
+        # the reference's own fp32 arithmetic moves an element under another summation order
+        self.order_seed = order_seed
+        self.t = 0
         # noise=True (run it in float64): per element, a bound on how far an fp32 implementation
         # summing the same gradient terms in another order can land (self.noise, accumulated over
         # the steps; see gradient_noise / Optim.sensitivity) -- the band of elementwise_parity
@@ -293,7 +298,14 @@ class MFOracle:
         dzn = dpn * (1.0 - p_neg) * p_neg
         u = torch.cat([pos_u, nu])
         i = torch.cat([pos_i, ni])
-        grads = self.grads_fn(U, I, ub, ib, u, i, torch.cat([dzp, dzn]))
+        dz = torch.cat([dzp, dzn])
+        self.t += 1
+        if self.order_seed is not None:
+            g = torch.Generator().manual_seed(int(self.order_seed) * 1000003 + self.t)
+            perm = torch.randperm(len(u), generator=g)
+            grads = self.grads_fn(U, I, ub, ib, u[perm], i[perm], dz[perm])
+        else:
+            grads = self.grads_fn(U, I, ub, ib, u, i, dz)
         if exchange is not None:
             grads = exchange(grads)
         if self.noise is not None:

@@ -227,6 +227,9 @@ SIGNATURES = [
                                    ctypes.POINTER(NCFWork), ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p,
                                    ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
                                    ctypes.POINTER(MTGen)]),
+    ("rg_ncf_tail_validate", ctypes.c_int, [ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork), ctypes.POINTER(NCFWork),
+                                            ctypes.c_int64, ctypes.POINTER(Opt), ctypes.c_void_p,
+                                            ctypes.POINTER(MFLoss)]),
     ("rg_neumf_apply", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(NCFModel), ctypes.POINTER(MFWork),
                                       ctypes.POINTER(NCFWork), ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64]),
     ("rg_pool_build", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -253,6 +256,8 @@ SIGNATURES = [
     ("rg_comm_create_host", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                               ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("rg_comm_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                    ctypes.POINTER(ctypes.c_int32)]),
     ("rg_comm_allreduce_sum_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     ("rg_mt_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_void_p]),

@@ -54,6 +54,13 @@ class RcclComm:
         check(self.lib.rg_comm_allgather_f32(self.handle, _lib.stream_handle(), len(bufs), arr, cnt),
               "rg_comm_allgather_f32")
 
+    def info(self):
+        """(count, user_rank, is_rccl) as the native communicator reports them: ncclCommCount /
+        ncclCommUserRank for RCCL, the configured world / rank for a stand-in."""
+        n, r, k = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(self.lib.rg_comm_info(self.handle, ctypes.byref(n), ctypes.byref(r), ctypes.byref(k)), "rg_comm_info")
+        return int(n.value), int(r.value), bool(k.value)
+
     def close(self):
         if getattr(self, "handle", None):
             self.lib.rg_comm_destroy(self.handle)

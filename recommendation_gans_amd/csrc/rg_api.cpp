@@ -43,6 +43,6 @@ extern "C" int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms) {
     return RG_OK;
 }
 
-extern "C" const char *rg_version(void) { return "librg_hip 0.1 gfx950 abi=1"; }
+extern "C" const char *rg_version(void) { return "librg_hip 0.2 gfx950 abi=2"; }
 
 extern "C" int32_t rg_build_flags(void) { return RG_AB ? RG_BUILD_AB : 0; }

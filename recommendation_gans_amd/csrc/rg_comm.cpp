@@ -56,13 +56,16 @@ struct Comm {
     std::thread watchdog;
     std::atomic<bool> stop{false};
     std::mutex mu;
-    hipEvent_t ev_track = nullptr;          // recorded after every kTrackEvery-th collective
+    // recorded after EVERY collective (re-recorded while still pending, so it always covers the
+    // newest one); track_t0 = when the oldest collective not yet seen complete was enqueued, so any
+    // collective that stalls -- the first of a run included -- reaches the deadline even when the
+    // host then blocks on a sync and enqueues nothing more
+    hipEvent_t ev_track = nullptr;
     std::chrono::steady_clock::time_point track_t0;
     bool tracking = false;
-    int64_t ncoll = 0;
+    int64_t ncoll = 0, track_first = 0;
     double timeout_s = 600.0;
 };
-constexpr int kTrackEvery = 16;
 
 // each in-flight host exchange owns its call record (freed by the callback): any number of
 // exchanges may be enqueued before the callbacks drain
@@ -98,13 +101,14 @@ static void watchdog_loop(Comm *c) {
         if (hipEventQuery(c->ev_track) == hipSuccess) { c->tracking = false; continue; }
         const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->track_t0).count();
         if (waited > c->timeout_s)
-            comm_die(c, "collective #" + std::to_string(c->ncoll) + " not complete after " + std::to_string((int)waited) +
+            comm_die(c, "collective #" + std::to_string(c->track_first) + " (of " + std::to_string(c->ncoll) +
+                            " enqueued) not complete after " + std::to_string((int)waited) +
                             " s (RG_COMM_TIMEOUT_S; a peer rank failed or diverged)");
     }
 }
 
 // after an RCCL call on `stream`: wait out ncclInProgress (non-blocking communicator) within
-// the deadline, and every kTrackEvery-th collective arm the watchdog on its completion
+// the deadline, and arm the watchdog on the collective's completion (every collective)
 static int nccl_after(Comm *c, hipStream_t stream, ncclResult_t r, const char *what) {
     const auto t0 = std::chrono::steady_clock::now();
     while (r == ncclInProgress) {
@@ -119,11 +123,12 @@ static int nccl_after(Comm *c, hipStream_t stream, ncclResult_t r, const char *w
         return RG_E_LAUNCH;
     }
     std::lock_guard<std::mutex> g(c->mu);
-    if (++c->ncoll % kTrackEvery == 0 && !c->tracking && c->ev_track) {
-        if (hipEventRecord(c->ev_track, stream) == hipSuccess) {
-            c->tracking = true;
-            c->track_t0 = std::chrono::steady_clock::now();
-        }
+    ++c->ncoll;
+    if (c->tracking && hipEventQuery(c->ev_track) == hipSuccess) c->tracking = false;   // caught up
+    if (c->ev_track && hipEventRecord(c->ev_track, stream) == hipSuccess && !c->tracking) {
+        c->tracking = true;                 // pending already: keep the older start time
+        c->track_t0 = std::chrono::steady_clock::now();
+        c->track_first = c->ncoll;
     }
     return RG_OK;
 }
@@ -383,6 +388,28 @@ extern "C" int rg_comm_destroy(void *h) {
     if (c->ev_out) hipEventDestroy(c->ev_out);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
+    return RG_OK;
+}
+
+// what the native communicator itself reports: ncclCommCount / ncclCommUserRank for an RCCL
+// communicator (bench.py prints them in the N > 1 line: the ranks RCCL saw, not WORLD_SIZE),
+// the configured world / rank for the local and host-staged stand-ins (is_rccl = 0)
+extern "C" int rg_comm_info(void *comm, int32_t *count, int32_t *user_rank, int32_t *is_rccl) {
+    rg::Comm *c = static_cast<rg::Comm *>(comm);
+    if (!c || !count || !user_rank || !is_rccl) return rg::fail_arg("rg_comm_info: null argument");
+    if (!c->comm) {
+        *count = c->world;
+        *user_rank = c->rank;
+        *is_rccl = 0;
+        return RG_OK;
+    }
+    int n = 0, r = 0;
+    ncclResult_t e = ncclCommCount(c->comm, &n);
+    if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);
+    if (e != ncclSuccess) return rg::nccl_fail("rg_comm_info", e);
+    *count = n;
+    *user_rank = r;
+    *is_rccl = 1;
     return RG_OK;
 }
 

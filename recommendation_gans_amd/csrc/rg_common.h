@@ -316,6 +316,105 @@ struct RowLayout {
     }
 };
 
+// A row of D = 4 * LPU * K floats over LPU lanes, K float4 chunks per lane, chunk c of lane
+// `sub` at floats (c * LPU + sub) * 4: each chunk is one fully coalesced wave instruction
+// (LPU lanes x 16 B contiguous per row).  Used by the dense pass (mf_back_kernel), whose per-row
+// arithmetic is element-wise, so any partition of a row over lanes gives the same bits: more
+// rows per wave (64 / LPU) and K loads in flight per lane and array instead of one.
+template <int LPU_, int K_>
+struct RowLayoutV {
+    static constexpr int LPU = LPU_;
+    static constexpr int K = K_;
+    static constexpr int EPL = 4 * K_;
+    static constexpr bool VEC = true;
+    static constexpr int UPW = kWave / LPU;
+    static constexpr int D = 4 * LPU_ * K_;
+    __device__ static __forceinline__ int elem(int sub, int e) { return ((e >> 2) * LPU + sub) * 4 + (e & 3); }
+    __device__ static __forceinline__ void load(float (&v)[EPL], const float *__restrict__ base, int64_t row, int,
+                                                int sub) {
+        load_strided(v, base, row, D, 0, sub);
+    }
+    __device__ static __forceinline__ void load_strided(float (&v)[EPL], const float *__restrict__ base, int64_t row,
+                                                        int64_t stride, int, int sub) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const float4 t = *reinterpret_cast<const float4 *>(base + row * stride + (c * LPU + sub) * 4);
+            v[4 * c] = t.x; v[4 * c + 1] = t.y; v[4 * c + 2] = t.z; v[4 * c + 3] = t.w;
+        }
+    }
+    __device__ static __forceinline__ void store(float *__restrict__ base, int64_t row, int, int sub,
+                                                 const float (&v)[EPL]) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+            *reinterpret_cast<float4 *>(base + row * (int64_t)D + (c * LPU + sub) * 4) =
+                make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+    }
+    __device__ static __forceinline__ void store_nt(float *__restrict__ base, int64_t row, int, int sub,
+                                                    const float (&v)[EPL]) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            v4f t = {v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+            __builtin_nontemporal_store(t, reinterpret_cast<v4f *>(base + row * (int64_t)D + (c * LPU + sub) * 4));
+        }
+    }
+    __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base, int64_t row, int,
+                                                   int sub) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const v4f t = __builtin_nontemporal_load(
+                reinterpret_cast<const v4f *>(base + row * (int64_t)D + (c * LPU + sub) * 4));
+            v[4 * c] = t.x; v[4 * c + 1] = t.y; v[4 * c + 2] = t.z; v[4 * c + 3] = t.w;
+        }
+    }
+    __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int, int sub,
+                                                    const float (&v)[EPL]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xffffffff, 0x00020000);
+        typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const v4f t = {v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)((row * D + (c * LPU + sub) * 4) * 4), 0, kSc1);
+        }
+    }
+    __device__ static __forceinline__ void store1_wt(float *p, float v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static __forceinline__ void zero(float (&v)[EPL]) {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) v[e] = 0.0f;
+    }
+};
+
+// The dense pass's layout for a dim's pair-pass layout L (mf_back_kernel, single-GPU MF):
+// RG_BACK_V64 / RG_BACK_V128 = lanes per row of a RowLayoutV for d = 64 / 128 (0: L itself).
+// Measured (round 5, profiles/r5/attr/): d = 64 on 8 lanes x 2 float4 (8 rows per wave) instead of
+// 16 lanes x 1 float4: 55.1 -> 51.2 us per dense pass; d = 128 on 16 lanes x 2 float4 instead of
+// 32 x 1: 111.7 -> 104.3 us -- twice the bytes in flight per wave at a similar occupancy.
+#ifndef RG_BACK_V64
+#define RG_BACK_V64 8
+#endif
+#ifndef RG_BACK_V128
+#define RG_BACK_V128 16
+#endif
+template <class L>
+struct BackLayout {
+    using type = L;
+};
+#if RG_BACK_V64
+template <>
+struct BackLayout<RowLayout<16, 4, true>> {
+    using type = RowLayoutV<RG_BACK_V64, 64 / (4 * RG_BACK_V64)>;
+};
+#endif
+#if RG_BACK_V128
+template <>
+struct BackLayout<RowLayout<32, 4, true>> {
+    using type = RowLayoutV<RG_BACK_V128, 128 / (4 * RG_BACK_V128)>;
+};
+#endif
+
 // Dispatch on dim: calls f.template operator()<Layout>() for the layout of `dim`.
 template <typename F>
 inline int dispatch_dim(int dim, F &&f) {

@@ -23,6 +23,7 @@
 //             weight_decay * p; Adam / SGD / RMSprop; p', m, v out; the list
 //             counter and overflow accumulators are reset in the same pass.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include <hip/hip_ext.h>
@@ -606,6 +607,11 @@ struct ApplyArgs {
 #ifndef RG_DENSE_WT
 #define RG_DENSE_WT 0
 #endif
+#ifdef RG_X_STREAMONLY
+#define RG_X_SO 1
+#else
+#define RG_X_SO 0
+#endif
 #ifndef RG_MF_SORTED_PULL
 #define RG_MF_SORTED_PULL 1
 #endif
@@ -1081,7 +1087,9 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         L::load(g, gbase, gkk, D, sub);
         if (sub == 0) gb = a.grad[gbi];
     } else if (!COLD) {
-#ifdef RG_X_NOPULL   // timing experiments only (wrong results): the pass without the pulls
+#if defined(RG_X_STREAMONLY)   // timing experiments only (wrong results): p, m, v and biases alone
+        const int c = 0;
+#elif defined(RG_X_NOPULL)   // timing experiments only (wrong results): the pass without the pulls
         const int c = a.row_count[r] < 0 ? 1 : 0;
 #else
         const int c = lz ? cnt : (COLD ? 0 : a.row_count[r]);
@@ -1091,7 +1099,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         // rows are its only dependent round trip
         int2 spec[SPEC ? kCap : 1];
         int s0 = 0, s1 = 0;
-        if (SPEC && !lz) {
+        if (SPEC && !lz && !RG_X_SO) {
             const int4 *lst = reinterpret_cast<const int4 *>(a.row_list + r * kCap);
 #pragma unroll
             for (int e = 0; e < kCap / 2; ++e) {
@@ -1108,7 +1116,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         constexpr bool kOneTrip = MODE == kGradOnly && SPEC;
         float h0[kOneTrip ? 4 : 1][EPL];
         float hb0[kOneTrip ? 4 : 1];
-        const bool parts = t == 1 && a.item_slot_off != nullptr;
+        const bool parts = !RG_X_SO && t == 1 && a.item_slot_off != nullptr;
         if (kOneTrip && parts && s1 > s0) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -2216,6 +2224,16 @@ struct BackLaunchF {
     const MlpUpdArgs *upd = nullptr;  // NCF step: the MLP update in the same launch (rg_ncf_tail)
     template <class L>
     int operator()() {
+        using LB = typename BackLayout<L>::type;
+        if constexpr (!std::is_same<LB, L>::value) {
+            // the single-GPU MF dense pass on its own row layout (RG_BACK_V64 / _V128)
+            if (!own && !upd && !lazy && a->contrib == nullptr) return run<LB, true>();
+        }
+        return run<L, false>();
+    }
+    // V: the dense-pass layout of a plain MF launch (no owner / NCF / lazy / A/B variants)
+    template <class L, bool V>
+    int run() {
         const int64_t rows = a->row_end - a->row_begin;
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
         int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
@@ -2256,6 +2274,10 @@ struct BackLaunchF {
             else
                 hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa, ua);
         };
+        if constexpr (V) {
+            go(mf_back_kernel<L, 0, true>);
+            return check_launch("rg_mf_apply_prepare");
+        } else {
         if (own) {
             go(mf_back_kernel<L, 0, true, true>);
             return check_launch("rg_mf_apply_prepare");
@@ -2294,6 +2316,7 @@ struct BackLaunchF {
         go(mf_back_kernel<L, 0, true>);   // the list loaded beside the count
 #endif
         return check_launch("rg_mf_apply_prepare");
+        }
     }
 };
 }  // namespace
@@ -2432,6 +2455,16 @@ extern "C" int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *t, rg
         prep_out = reinterpret_cast<int2 *>(next->pairs);
         prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
+#ifdef RG_X_PREP_SPLIT   // timing experiments only: the next prepare as its own launch in front
+    if (prep_blocks > 0) {
+        hipLaunchKernelGGL(mf_prepare_kernel, dim3((unsigned)prep_blocks), dim3(kBlock), 0, (hipStream_t)stream, prep,
+                           prep_out, 0);
+        prep_blocks = 0;
+    }
+#endif
+#ifdef RG_X_NOGEN   // timing experiments only (wrong results: the ring slot is never walked)
+    g.nwords = 0;
+#endif
     BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }
@@ -2665,24 +2698,44 @@ extern "C" int rg_ncf_apply(void *stream, const rg_ncf_model_t *m, rg_mf_work_t 
 // of its own (it keeps the per-row counts the MLP tables' pass then consumes), as rg_neumf_apply.
 // gen (optional, rg_mf_stepper_tail_gen): workgroup 0 walks a later step's MT words, as in the
 // MF split step's dense pass -- no generator-stream kernel beside the pair kernel.
+// every check of rg_ncf_tail that does not depend on the stepper's outputs (next batch, MT walk):
+// the engine runs it BEFORE the stepper bookkeeping calls (rg_mf_stepper_prefetch_args /
+// rg_mf_stepper_tail_gen commit the next unit and the ring slot), so a refused tail never
+// leaves the stepper believing a prepare or a walk was launched
+static int ncf_tail_checks(const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw, int64_t nparts,
+                           const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss, ApplyArgs &a,
+                           int64_t &P) {
+    if (!m || !w || !nw || !opt || !nw->contrib || !nw->mlp_partials || !m->mlp)
+        return fail_arg("rg_ncf_tail: null argument");
+    if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_tail: Adam needs m state");
+    if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_tail: optimizer needs v state");
+    P = m->mf_dim == 0 ? rg_ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
+    if (P < 0 || nparts < 1) return fail_arg("rg_ncf_tail: bad dim / mf_dim / partial count");
+    if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_tail: loss needs partials");
+    if (m->dim < 1 || m->dim > 256) return fail_arg("rg_ncf_tail: dim must be in [1, 256]");
+    return ncf_apply_args(m, w, nw->contrib, opt, 0, -1, a);
+}
+
+extern "C" int rg_ncf_tail_validate(const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
+                                    int64_t nparts, const rg_opt_t *opt, const float *loss_partials,
+                                    const rg_mf_loss_t *loss) {
+    ApplyArgs a{};
+    int64_t P = 0;
+    return ncf_tail_checks(m, w, nw, nparts, opt, loss_partials, loss, a, P);
+}
+
 extern "C" int rg_ncf_tail(void *stream, const rg_ncf_model_t *m, rg_mf_work_t *w, const rg_ncf_work_t *nw,
                            int64_t nparts, const rg_opt_t *opt, const float *loss_partials, const rg_mf_loss_t *loss,
                            const rg_mf_batch_t *next, const rg_mf_work_t *next_w, const rg_mt_gen_t *gen) {
-    if (!m || !w || !nw || !opt || !nw->contrib || !nw->mlp_partials || !m->mlp)
-        return fail_arg("rg_ncf_tail: null argument");
+    ApplyArgs a{};
+    int64_t P = 0;
+    int rc = ncf_tail_checks(m, w, nw, nparts, opt, loss_partials, loss, a, P);
+    if (rc) return rc;
     MtGenArgs g{};
     if (gen && gen->nwords > 0) {
         if (!gen->state || !gen->out) return fail_arg("rg_ncf_tail: null MT state / output");
         g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
     }
-    if (opt->kind == RG_OPT_ADAM && !m->mlp_m) return fail_arg("rg_ncf_tail: Adam needs m state");
-    if (opt->kind != RG_OPT_SGD && !m->mlp_v) return fail_arg("rg_ncf_tail: optimizer needs v state");
-    const int64_t P = m->mf_dim == 0 ? rg_ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
-    if (P < 0 || nparts < 1) return fail_arg("rg_ncf_tail: bad dim / mf_dim / partial count");
-    if (loss && loss->out && !loss_partials) return fail_arg("rg_ncf_tail: loss needs partials");
-    ApplyArgs a{};
-    int rc = ncf_apply_args(m, w, nw->contrib, opt, 0, -1, a);
-    if (rc) return rc;
     // NeuMF: the GMF tables' pass first; the walk (if any) rides in that launch -- the longer of
     // the two passes at the reference's sizes (mf 50 vs mlp 16 floats per row)
     if (m->mf_dim != 0) {

@@ -2,7 +2,7 @@
 // implicit.py:347-364; layers [2E, E, ..., 8] -> 1 as ncf_spotlight.py:53-56).
 //
 // One workgroup (4 waves) walks tiles of kRows = 32 examples (the E = 64 MLP's wave kernel:
-// 48, ncfw::kR); a tile holds whole
+// ncfw::kR = RG_NCF_WAVE_ROWS, 32 in the product build, 48 in the ncf48 A/B variant); a tile holds whole
 // columns (a positive and its n negatives, pairs prepared by rg_mf_prepare), so
 // pairwise losses are resolved inside the tile.  Everything of a tile lives in
 // LDS: the MLP parameters (loaded once per workgroup), the activations of every
@@ -787,8 +787,9 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
 }
 
 // ============================================================================================
-// E = 64 tower (C3, mf_dim = 0): one WAVE per 48-row tile (8 whole columns of 1 + 5 rows at
-// n = 5: 1,024 tiles at B = 8192, one per wave of the 256 x 4-wave grid, no second round).
+// E = 64 tower (C3, mf_dim = 0): one WAVE per tile of RG_NCF_WAVE_ROWS rows -- 32 in the product
+// build (1,639 tiles at B = 8192, n = 5); the ncf48 A/B variant's 48-row tile (8 whole columns of
+// 1 + 5 rows: 1,024 tiles, one per wave of the 256 x 4-wave grid) measured no faster.
 //
 // The tile kernel above keeps every activation in LDS and spreads a tile's MFMA tiles over 8
 // waves: ~12 workgroup barriers and an LDS -> MFMA -> LDS round trip per layer, 14 % of the
@@ -1731,8 +1732,9 @@ static int64_t ncf_param_len(const rg_ncf_model_t *m) {
     return m->mf_dim == 0 ? ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
 }
 extern "C" int64_t rg_ncf_mask_units(int32_t dim) { return ncf_mask_units(dim); }
-// rows per tile: 48 for the wave kernel (E = 64 MLP: 8 columns of 1 + 5 rows, one tile per wave),
-// 32 for the tile kernel (the other towers, NeuMF)
+// rows per tile: RG_NCF_WAVE_ROWS for the wave kernel (E = 64 MLP; 32 in the product build, 48 --
+// 8 columns of 1 + 5 rows, one tile per wave -- only in the ncf48 A/B variant), 32 for the tile
+// kernel (the other towers, NeuMF)
 extern "C" int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim) {
     if (ncf_mlp_len(dim) < 0 || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
     return ncf_use_wave(dim, mf_dim) ? ncfw::kR : kRows;

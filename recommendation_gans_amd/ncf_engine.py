@@ -131,6 +131,7 @@ class NCFEngine:
         # calls it replaces (rg_ncf_update, rg_ncf_apply / rg_neumf_apply, the inline prefetch)
         # -- the same bits, checked by tests/test_ncf_gpu.py
         self.fused_tail = True
+        self._broken = None           # set when a refused tail left the stepper's state unusable
         self._model = _lib.NCFModel(ptr(self.user_w), ptr(self.item_w), ptr(self.m[0]), ptr(self.v[0]),
                                     ptr(self.m[1]), ptr(self.v[1]), ptr(self.mlp), ptr(self.m[2]), ptr(self.v[2]),
                                     self.U, self.I, E, self.M)
@@ -166,9 +167,12 @@ class NCFEngine:
             if self.world == 1 and self.neumf:
                 # NeuMF: the walk rides in the GMF tables' launch when that pass hides it (the
                 # stepper's test, rg_stepper.cpp, against the GMF rows instead of the MLP ones, at
-                # the ~4.5 TB/s the odd-width 16-lane rows stream at: 42 us for mf 50 on ML-20M)
+                # the ~4.5 TB/s the odd-width 16-lane rows stream at: 42 us for mf 50 on ML-20M
+                # with Adam); the pass streams p plus the optimizer's state arrays, read and
+                # written: SGD 2, RMSprop 4, Adam 6 arrays
                 walk_us = 0.47e-3 * 2 * n * B
-                gmf_us = 6.0 * (self.U + self.I) * 4.0 * self.M / 4.5e6
+                streams = {"sgd": 2.0, "rms": 4.0, "rmsprop": 4.0, "adam": 6.0}.get(self.opt_kind, 6.0)
+                gmf_us = streams * (self.U + self.I) * 4.0 * self.M / 4.5e6
                 cfg.gen_mode = 3 if walk_us <= gmf_us else 2
         self._stepper = lib.rg_mf_stepper_create(ctypes.byref(cfg))
         if not self._stepper:
@@ -292,6 +296,8 @@ class NCFEngine:
         (pos_u, pos_i) are this rank's columns of the global batch, ``global_pos`` its size
         (default R * n_pos), ``masks`` (if given) the GLOBAL batch's, and the exchange runs on
         ``comm`` or ``allreduce(flat)``."""
+        if self._broken:
+            raise RuntimeError("NCFEngine unusable: " + self._broken)
         n_pos = int(pos_u.numel())
         global_pos = n_pos * self.world if global_pos is None else int(global_pos)
         if self.world > 1 and self.comm is None and allreduce is None:
@@ -324,6 +330,12 @@ class NCFEngine:
             # one launch: the next step's prepare, the MLP update (with the loss) and the
             # embedding update (rg_ncf_tail; the same sums as the three separate calls)
             nb, nwk, need, gen = _lib.MFBatch(), _lib.MFWork(), 0, _lib.MTGen()
+            lossd = self._loss(global_pos, out)
+            # the tail's own checks first: the two stepper calls below commit the next unit and
+            # the MT ring slot, which only a launched tail may consume
+            check(self.lib.rg_ncf_tail_validate(ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
+                                                self.blocks, ctypes.byref(o), ptr(parts), ctypes.byref(lossd)),
+                  "rg_ncf_tail")
             if next_step is not None and not self._prefetch_side:
                 need = self.lib.rg_mf_stepper_prefetch_args(self._stepper, stream, ctypes.byref(self._next_in),
                                                             ctypes.byref(nb), ctypes.byref(nwk))
@@ -332,12 +344,15 @@ class NCFEngine:
             walk = self.lib.rg_mf_stepper_tail_gen(self._stepper, stream, ctypes.byref(gen))
             if walk < 0:
                 check(walk, "rg_mf_stepper_tail_gen")
-            check(self.lib.rg_ncf_tail(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
-                                       self.blocks, ctypes.byref(o), ptr(parts),
-                                       ctypes.byref(self._loss(global_pos, out)),
-                                       ctypes.byref(nb) if need else None, ctypes.byref(nwk) if need else None,
-                                       ctypes.byref(gen) if walk else None),
-                  "rg_ncf_tail")
+            rc = self.lib.rg_ncf_tail(stream, ctypes.byref(self._model), ctypes.byref(work), ctypes.byref(nw),
+                                      self.blocks, ctypes.byref(o), ptr(parts), ctypes.byref(lossd),
+                                      ctypes.byref(nb) if need else None, ctypes.byref(nwk) if need else None,
+                                      ctypes.byref(gen) if walk else None)
+            if rc != 0 and (need or walk):
+                # refused after the stepper committed a prepare / walk that never launched: later
+                # steps would read stale words and pairs, so this engine cannot continue
+                self._broken = "rg_ncf_tail refused after the stepper committed the next unit"
+            check(rc, "rg_ncf_tail")
         else:
             check(self.lib.rg_ncf_update(stream, ctypes.byref(self._model), ctypes.byref(nw), self.blocks,
                                          ctypes.byref(o), ptr(parts), ctypes.byref(self._loss(global_pos, out))),

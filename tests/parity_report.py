@@ -18,12 +18,35 @@ class ParityReport(UserWarning):
     pass
 
 
-def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None, alt32=None):
+def order_stats(got, ref32, order32, rtol=1e-5):
+    """The reference's own fp32 spread on the elements the GPU leaves outside rtol: ``order32`` is
+    a second fp32 restatement of the same steps summing the gradients in another order
+    (MFOracle(order_seed=...)).  Returns n_ref_out (elements where the two fp32 restatements
+    differ beyond rtol), n_gpu_out, n_both (GPU outside AND the second order outside too on the
+    same element) and max_ref_rel (max |order32 - ref32| / max |ref32|)."""
+    import torch
+    g = torch.as_tensor(got).double().reshape(-1).cpu()
+    r = torch.as_tensor(ref32).double().reshape(-1)
+    a = torch.as_tensor(order32).double().reshape(-1)
+    mx = float(r.abs().max()) if r.numel() else 0.0
+    tol = rtol * r.abs() + rtol * 1e-3 * mx
+    gout = (g - r).abs() > tol
+    aout = (a - r).abs() > tol
+    return {"n_ref_out": int(aout.sum()), "n_gpu_out": int(gout.sum()), "n_both": int((gout & aout).sum()),
+            "max_ref_rel": float((a - r).abs().max()) / max(mx, 1e-30) if r.numel() else 0.0}
+
+
+def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None, alt32=None, order32=None):
     ok_n, msg = omf.tensor_parity(got, ref32, ref64, rtol=rtol, band=band, before=before)
     ok_e, st = omf.elementwise_parity(got, ref32, ref64, rtol=rtol, band=band, before=before, noise=noise,
                                       alt32=alt32)
     line = (f"{tag}: max|d|/max|ref| {st['max_rel']:.2e}, outside 1e-5 {st['n_out']}/{st['n']} "
             f"({st['frac_out']:.2e}), ill-conditioned {st['n_ill']}, failing the fp64 band too {st['n_fail']}")
+    if order32 is not None:
+        st["order"] = order_stats(got, ref32, order32, rtol)
+        o = st["order"]
+        line += (f"; the reference in another fp32 summation order: outside 1e-5 on {o['n_ref_out']} elements, "
+                 f"{o['n_both']} of the GPU's {o['n_gpu_out']} among them")
     warnings.warn(line, ParityReport)
     try:
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
