@@ -1488,6 +1488,28 @@ __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs 
     apply_row<L, kApplyPull, NT, false, SPEC>(a, r, sub);
 }
 
+#ifdef RG_X_PIPE2
+// Timing prototype only (wrong results): step t+1's pair pass (blocks [0, pair_blocks), pair-pass
+// layout LP) in the same launch as the dense update of rows [row_begin, row_end) (layout LD): does a
+// latency-bound pair pass hide under an HBM-bound stream when they share a launch?
+template <class LP, class LD, int NMAX>
+__global__ __launch_bounds__(kBlock) void mf_pipe2_kernel(ApplyArgs a, PairsArgs pa, int64_t pair_blocks) {
+    int64_t blk = blockIdx.x;
+    if (blk < pair_blocks) {
+        pairs_body<LP, kFused, NMAX>(pa, blk);
+        return;
+    }
+    blk -= pair_blocks;
+    constexpr int LPU = LD::LPU, UPW = LD::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t wave = (blk * kBlock + threadIdx.x) >> 6;
+    const int64_t k = wave * UPW + (lane / LPU);
+    if (k >= a.row_end - a.row_begin) return;
+    apply_row<LD, kApplyPull, 0, false, true>(a, a.row_begin + k, sub);
+}
+#endif
+
 // The single-GPU dense pass as a software pipeline (the default split step): a grid of a few
 // workgroups per CU whose waves each walk a contiguous chunk of row groups (UPW rows per group),
 // the NEXT group's independent loads (p, m, v, biases, count, list entries, slot range) issued
@@ -1880,6 +1902,16 @@ struct ApplyLaunchF {
     int mode;
     template <class L>
     int operator()() {
+        // MF rows (not NCF's contribution rows) on the dense pass's layout: the item gradient and
+        // item update of the data-parallel steps, element-wise like the dense pass
+        using LB = typename BackLayout<L>::type;
+        if constexpr (!std::is_same<LB, L>::value) {
+            if (a->contrib == nullptr) return run<LB>();
+        }
+        return run<L>();
+    }
+    template <class L>
+    int run() {
         const int64_t rows = a->row_end - a->row_begin;
         if (rows <= 0 && a->loss_out == nullptr) return RG_OK;
         const int64_t waves = (rows + L::UPW - 1) / L::UPW;
@@ -2226,8 +2258,9 @@ struct BackLaunchF {
     int operator()() {
         using LB = typename BackLayout<L>::type;
         if constexpr (!std::is_same<LB, L>::value) {
-            // the single-GPU MF dense pass on its own row layout (RG_BACK_V64 / _V128)
-            if (!own && !upd && !lazy && a->contrib == nullptr) return run<LB, true>();
+            // the MF dense pass (single-GPU, or an owner rank's user rows) on its own row layout
+            // (RG_BACK_V64 / _V128)
+            if (!upd && !lazy && a->contrib == nullptr) return run<LB, true>();
         }
         return run<L, false>();
     }
@@ -2275,7 +2308,11 @@ struct BackLaunchF {
                 hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, s, *a, *prep, prep_out, nb, gen, bg, oa, ua);
         };
         if constexpr (V) {
-            go(mf_back_kernel<L, 0, true>);
+#ifndef RG_BACK_NT   // timing experiments: store policy of the V-layout dense pass (apply_row's NT)
+#define RG_BACK_NT 0
+#endif
+            if (own) go(mf_back_kernel<L, 0, true, true>);
+            else go(mf_back_kernel<L, RG_BACK_NT, true>);
             return check_launch("rg_mf_apply_prepare");
         } else {
         if (own) {
@@ -2428,6 +2465,43 @@ extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work
     return dispatch_dim(t->dim, f);
 #endif
 }
+
+#ifdef RG_X_PIPE2
+namespace {
+struct Pipe2LaunchF {
+    ApplyArgs *a;
+    PairsArgs *pa;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        using LB = typename BackLayout<L>::type;
+        const int64_t pb = pairs_blocks<L>(pa->cols);
+        const int64_t rows = a->row_end - a->row_begin;
+        const int64_t nb = ((rows + LB::UPW - 1) / LB::UPW + kBlock / kWave - 1) / (kBlock / kWave);
+        if (pa->n_neg <= 5)
+            hipLaunchKernelGGL((mf_pipe2_kernel<L, LB, 5>), dim3((unsigned)(pb + nb)), dim3(kBlock), 0, s, *a, *pa, pb);
+        else
+            hipLaunchKernelGGL((mf_pipe2_kernel<L, LB, kNMax>), dim3((unsigned)(pb + nb)), dim3(kBlock), 0, s, *a, *pa, pb);
+        return check_launch("rg_x_pipe2");
+    }
+};
+}  // namespace
+
+// timing prototype only: the pair pass of `pair_b` (on the tables' out set) and the dense update of
+// rows [row_begin, row_end) in ONE launch
+extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                          int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w) {
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, nullptr, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    rg_mf_tables_t pt = *t;
+    pt.user_w = t->user_w_out; pt.item_w = t->item_w_out; pt.user_b = t->user_b_out; pt.item_b = t->item_b_out;
+    PairsArgs pa;
+    if ((rc = pairs_args(&pt, pair_b, pair_w, 1, pa))) return rc;
+    Pipe2LaunchF f{&a, &pa, (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
+}
+#endif
 
 extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
                                    int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,

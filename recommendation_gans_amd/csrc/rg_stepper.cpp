@@ -54,6 +54,11 @@
 #define RG_PIPE_DEFAULT 0
 #endif
 
+#ifdef RG_X_PIPE2
+extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                          int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w);
+static int64_t g_x_paired = -1;   // timing prototype: the unit whose pair pass ran in the last launch
+#endif
 namespace {
 
 constexpr int kSlots = 3;        // word slots in the ring
@@ -582,9 +587,16 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         nbatch = make_batch(st, *next, unit + 1);
         nw = train_work(st, *next, unit + 1);
         if ((rc = rg_mf_pairs_prepare(s, tb, &batch, &w, &nbatch, &nw, nullptr, 0))) return rc;
-    } else if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
+    }
+#ifdef RG_X_PIPE2
+    else if (g_x_paired != unit && (rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
         return rc;
     }
+#elif !defined(RG_X_NOPAIR)   // timing experiments only (wrong results): the split step without its pair pass
+    else if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
+        return rc;
+    }
+#endif
     if ((rc = release(st, s))) return rc;
     if (next && !pip) {
         if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
@@ -615,11 +627,29 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
             return rc;
     }
     rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // timed by the dispatch itself
+#ifdef RG_X_PIPE2
+    // timing prototype (wrong results): launch A = the last H users + every item (+ next prepare,
+    // walk, loss); launch B = the NEXT step's pair pass beside the dense update of users [0, U - H)
+    static const int64_t xh = [] { const char *e = getenv("RG_X_H"); return e ? atoll(e) : 36000LL; }();
+    const int64_t hb = next && !st.cfg.item_grad ? (U > xh ? U - xh : 0) : 0;
+    rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, hb, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
+                                 next && !pip ? &nbatch : nullptr, next && !pip ? &nw : nullptr,
+                                 gen_slot >= 0 ? &gen : nullptr);
+    rg::launch_events() = rg::LaunchEvents{};
+    if (rc) return rc;
+    g_x_paired = -1;
+    if (hb > 0) {
+        rg_mf_batch_t nb2 = nbatch;
+        if ((rc = rg_x_pipe2(s, tb, &w, &o, 0, hb, &nb2, &nw))) return rc;
+        g_x_paired = unit + 1;
+    }
+#else
     rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
                                  next && !pip ? &nbatch : nullptr, next && !pip ? &nw : nullptr,
                                  gen_slot >= 0 ? &gen : nullptr);
     rg::launch_events() = rg::LaunchEvents{};
     if (rc) return rc;
+#endif
     if (gen_slot >= 0) end_production(st, s, gen_slot);
     if (st.cfg.item_grad) {
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
