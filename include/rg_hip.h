@@ -341,6 +341,31 @@ int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *wo
 int rg_mf_prepare_hot(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work, int32_t *hot_out,
                       int32_t *nhot_out);
 
+/* The single-GPU step as TWO launches per step t (the stepper's default for pointwise / bpr / hinge,
+ * rg_mf_stepper_train_ahead), replacing run_train_iteration (implicit.py:347-364) of
+ * step t+1 up to its backward and the optimizer step (implicit.py:363, spotlight/optimizers.py:10-16)
+ * of step t, with step t+1's latency-bound pair pass beside the HBM-bound update of the rows it does
+ * not read:
+ *   rg_mf_pipe2_hot:  step t's dense update (as rg_mf_apply) of every item row and of the users in
+ *                     hot_users[0 .. *nhot) (step t+1's hot list); step t's loss; *nhot_clear = 0
+ *                     (optional: the list the cold launch's prepare appends to); gen: a later unit's
+ *                     MT walk in one workgroup (optional).  hot_cap >= *nhot sizes the grid.
+ *   rg_mf_pipe2_cold: step t+1's pair pass (pair_batch / pair_work: prepared with claims in
+ *                     counts_next, which must be pair_work->row_count; it reads the tables' OUT set,
+ *                     rows the hot launch wrote), the prepare of step t+2 (optional: next null;
+ *                     claims in next_work->row_count, its hot list to hot_out / *nhot_out), gen, and
+ *                     step t's dense update of every user with counts_next[u] == 0.
+ * Per-row and per-column arithmetic is rg_mf_apply's / rg_mf_pairs', so the results are bit-identical
+ * to the split step.  pair_work's scratch (lists, overflow accumulators, partials, planned partials,
+ * counts) must not alias work's.  Loss: pointwise, bpr, hinge. */
+int rg_mf_pipe2_hot(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
+                    const rg_mf_loss_t *loss, const int32_t *hot_users, const int32_t *nhot, int64_t hot_cap,
+                    int32_t *nhot_clear, const rg_mt_gen_t *gen);
+int rg_mf_pipe2_cold(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, const rg_opt_t *opt,
+                     const rg_mf_batch_t *pair_batch, rg_mf_work_t *pair_work, const int32_t *counts_next,
+                     const rg_mf_batch_t *next, const rg_mf_work_t *next_work, int32_t *hot_out, int32_t *nhot_out,
+                     const rg_mt_gen_t *gen);
+
 /* Pull the DATA gradient (no weight decay) of the rows in range into the flat
  * buffer grad_dev = [n*dim row grads | n bias grads | loss], n = row_end - row_begin
  * (the loss slot is written when loss->out is non-null).  Resets the lists like

@@ -286,6 +286,13 @@ SIGNATURES = [
                                                ctypes.POINTER(MFWork), ctypes.POINTER(MTGen)]),
     ("rg_mf_prepare_hot", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
                                          ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_mf_pipe2_hot", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                       ctypes.POINTER(Opt), ctypes.POINTER(MFLoss), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(MTGen)]),
+    ("rg_mf_pipe2_cold", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                        ctypes.POINTER(Opt), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                        ctypes.c_void_p, ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MTGen)]),
     ("rg_mf_pipe_step", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
                                        ctypes.POINTER(Opt), ctypes.POINTER(MFLoss), ctypes.POINTER(MFBatch),
                                        ctypes.POINTER(MFWork), ctypes.POINTER(MFBatch), ctypes.POINTER(MFWork),

@@ -127,16 +127,18 @@ __device__ int g_diag_flags;   // timing only (results are wrong): bit 0 skip th
 // thread per entry, column-major so the record is written contiguously.
 // With stamps, every row a pair touches (valid or not: extra rows are harmless, a
 // missed one would not be) is stamped with the serial, and the first stamper owns it.
-__device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict__ out, int64_t idx) {
+// Returns the user this entry claimed a FIRST list slot of (the users the prepared step's pair pass
+// reads, for a hot list), else -1.
+__device__ __forceinline__ int prepare_body(const PairsArgs &a, int2 *__restrict__ out, int64_t idx) {
     const int NP = 1 + a.n_neg, E = NP + 1;              // entries written per column
     const int64_t total = (int64_t)E * a.cols;
-    if (idx >= total) return;
+    if (idx >= total) return -1;
     const int64_t s = idx / E;
     const int q = (int)(idx - s * E);
     int2 *rec = out + s * pair_stride(a.n_neg);
     if (q == NP) {                                       // the plan slot of the positive
         rec[q] = make_int2(a.pos_slot != nullptr && s < a.n_pos ? a.pos_slot[s] : -1, 0);
-        return;
+        return -1;
     }
     const int64_t col = a.perm ? (int64_t)a.perm[s] : s;
     int2 r;
@@ -148,6 +150,7 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         r = a.pool[choice_index(w.x, w.y, a.pool_len)];
     }
     if (a.umark != nullptr) a.umark[r.x] = a.umark_step;   // plain store: every writer stores the same value
+    int hot = -1;
     if (a.claimed) {
         // the list slots the pair pass would claim (pairs_body's validity): the positive if the
         // position has one, a negative if its column pairs with a positive or the loss is
@@ -156,7 +159,7 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         const bool v = q == 0 ? s < a.n_pos : (a.loss != RG_LOSS_POINTWISE_POS && (s < a.n_pos || !pairwise));
         if (v) {
             const int su = atomicAdd(a.row_count + r.x, 1);
-            if (su == 0 && a.hot_out != nullptr) a.hot_out[atomicAdd(a.nhot_out, 1)] = r.x;
+            if (su == 0) hot = r.x;
             const bool item_side = !(q == 0 && a.pos_slot != nullptr);
             const int si = item_side ? atomicAdd(a.row_count + a.num_users + r.y, 1) : 0;
             r.x |= (su < kCap ? su : kCap) << kSlotShift;
@@ -170,7 +173,29 @@ __device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict
         if (oi != a.serial) r.y |= kOwnerBit;
     }
     rec[q] = r;
+    return hot;
 }
+
+// append each lane's `user` (>= 0) to a.hot_out: one atomic per wave (a ballot and a prefix count),
+// not one per user -- tens of thousands of returning atomics on ONE counter serialise; every lane of
+// the wave calls it
+__device__ __forceinline__ void hot_append(const PairsArgs &a, int user) {
+    const unsigned long long m = __ballot(user >= 0);
+    if (m == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(a.nhot_out, __popcll(m));
+    base = __shfl(base, leader);
+    if (user >= 0) a.hot_out[base + __popcll(m & ((1ull << lane) - 1ull))] = user;
+}
+
+// one prepared entry (every thread of the workgroup calls it: the hot-list append is per wave)
+__device__ __forceinline__ void prepare_one(const PairsArgs &a, int2 *__restrict__ out, int64_t idx) {
+    const int hot = prepare_body(a, out, idx);
+    if (a.hot_out != nullptr) hot_append(a, hot);
+}
+
 
 __host__ __device__ inline int64_t prepare_threads(int64_t cols, int n_neg) { return (int64_t)(n_neg + 3) * cols; }
 
@@ -602,6 +627,9 @@ struct ApplyArgs {
     int32_t lazy_dbg;             // timing experiments only (RG_LAZY_DBG; wrong results): bit 0 no catch-up,
                                   // 1 every user row processed, 2 no constants window, 3 no odd-lag reload
     int32_t lazy_cap;             // > 0: a row that has missed this many steps is processed anyway
+    // apply_row<..., GUARD>: a row with guard[r] > 0 is left alone (another launch updates it); the
+    // guard is loaded beside the row's other loads, so it costs no round trip of its own
+    const int32_t *guard;
 };
 
 #ifndef RG_DENSE_WT
@@ -987,7 +1015,8 @@ __device__ __forceinline__ void apply_row_lean(const ApplyArgs &a, const int64_t
     lean_finish<L>(a, r, sub, true, x);
 }
 
-template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false>
+template <class L, int MODE, int NT, bool COLD, bool SPEC = false, bool LAZY = false, bool LSPEC = false,
+          bool GUARD = false>
 __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, const int sub,
                                           const LazyRow lzr = LazyRow{}) {
     constexpr int EPL = L::EPL;
@@ -1079,6 +1108,8 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     }
     L::zero(g);
     float gb = 0.0f;
+    bool guarded = false;
+    if constexpr (GUARD) guarded = a.guard[r] > 0;
 
     if (MODE == kApplyDense) {
         const float *gbase;
@@ -1125,7 +1156,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
                 hb0[kOneTrip ? u : 0] = a.has_bias ? a.part_bias[ss] : 0.0f;
             }
         }
-        if (c > 0) {
+        if (c > 0 && !guarded) {
             const int ne = c < kCap ? c : kCap;
             int2 ent[kCap];
 #pragma unroll
@@ -1214,7 +1245,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 #ifdef RG_X_NOPART  // timing experiments only (wrong results): no planned partials
         if (false) {
 #else
-        if (parts) {   // planned positive partials of this item
+        if (parts && !guarded) {   // planned positive partials of this item
 #endif
             if (!SPEC || lz) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
             for (int sl = s0; sl < s1; sl += 4) {
@@ -1254,7 +1285,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
 
     if (LAZY && !(a.lazy_dbg & 1))   // every lane of the wave (item / skipped rows: nothing to catch up)
         catch_up<L>(a, wconst, wmax, lag, a.lazy_t, sub, p, m, v, pb, mb, vb);
-    if (!proc) return;
+    if (!proc || guarded) return;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) p[q] = opt_update(a.opt, p[q], g[q], m[q], v[q]);
     if (NT == 3) {          // optimizer state streamed past the caches, the new row kept (next gathers)
@@ -1486,6 +1517,104 @@ __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs 
     }
     if (k >= nr) return;
     apply_row<L, kApplyPull, NT, false, SPEC>(a, r, sub);
+}
+
+// ---------------------------------------------------------------------------- two-launch pipelined step
+// The single-GPU step as two launches per step t, overlapping step t+1's latency-bound pair pass
+// with the HBM-bound update of the rows that pass does not read:
+//
+//   hot launch  (mf_pipe2_hot_kernel):  the dense update of step t for every item row and for the
+//               users step t+1's pair pass reads (its prepare's hot list); step t's loss
+//   cold launch (mf_pipe2_cold_kernel): [step t+1's pair pass] [the MT walk of a later unit]
+//               [step t+2's prepare, appending its hot list] [the dense update of step t for every
+//               other user (its claim count of step t+1 is zero)]
+//
+// The pair pass reads only rows the hot launch wrote (stream order: no gate, no spin), and the
+// cold rows it leaves to the same launch are rows it does not read.  Per-row and per-column
+// arithmetic is the split step's, so results are bit-identical to it.  A unit's scratch alternates
+// by parity (claims in three count arrays, lists / overflow accumulators / partials in two sets:
+// rg_stepper.cpp train_pipe2).
+struct Pipe2Args {
+    const int32_t *hot;           // hot launch: the users step t+1's pair pass reads
+    const int32_t *nhot;          // hot launch: their number (device)
+    int64_t hot_blocks, item_blocks;
+    int32_t *nhot_clear;          // hot launch: zeroed (the list the cold launch's prepare appends to)
+    const int32_t *counts_next;   // cold launch: step t+1's claims (a user with one is hot)
+    int64_t pair_blocks, prep_blocks, cold_blocks;
+};
+
+template <class LD>
+__global__ __launch_bounds__(kBlock) void mf_pipe2_hot_kernel(ApplyArgs a, Pipe2Args p, MtGenArgs gen) {
+    int64_t blk = blockIdx.x;
+    if (gen.nwords > 0) {
+        if (blk == 0) {
+            __shared__ uint32_t X[kRing + 2];
+            mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
+            return;
+        }
+        --blk;
+    }
+    constexpr int LPU = LD::LPU, UPW = LD::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    if (blk == 0) {
+        if (threadIdx.x == 0 && p.nhot_clear != nullptr) *p.nhot_clear = 0;
+        if (a.loss_out != nullptr && threadIdx.x >= kWave && threadIdx.x < 2 * kWave) {
+            const float lv = finalize_loss(a.partials, a.n_partials, a.inv_a, a.inv_b, lane);   // step t's loss
+            if (lane == 0) *a.loss_out = lv;
+        }
+    }
+    constexpr int64_t rpb = (kBlock / kWave) * UPW;
+    const int64_t in_block = (threadIdx.x >> 6) * UPW + lane / LPU;
+    int64_t r;
+    if (blk < p.item_blocks) {
+        const int64_t k = blk * rpb + in_block;
+        if (k >= a.num_items) return;
+        r = a.num_users + k;
+    } else {
+        const int64_t j = (blk - p.item_blocks) * rpb + in_block;
+        if (j >= (int64_t)*p.nhot) return;
+        r = p.hot[j];
+    }
+    apply_row<LD, kApplyPull, 0, false, true>(a, r, sub);
+}
+
+template <class LP, class LD, int NMAX>
+__global__ __launch_bounds__(kBlock) void mf_pipe2_cold_kernel(ApplyArgs a, PairsArgs pa, PairsArgs prep,
+                                                               int2 *prep_out, Pipe2Args p, MtGenArgs gen) {
+    static_assert(kPairBlock == kBlock, "the pair workgroups share the launch's block size");
+    int64_t blk = blockIdx.x;
+    if (blk < p.pair_blocks) {                  // first in the grid: the step's latency chain
+        pairs_body<LP, kFused, NMAX>(pa, blk);
+        return;
+    }
+    blk -= p.pair_blocks;
+    if (gen.nwords > 0) {
+        if (blk == 0) {
+            __shared__ uint32_t X[kRing + 2];
+            mt_generate_block(X, gen.state, gen.out, gen.nwords, gen.state_before);
+            return;
+        }
+        --blk;
+    }
+    if (blk < p.prep_blocks) {
+        prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
+        return;
+    }
+    blk -= p.prep_blocks;
+    constexpr int LPU = LD::LPU, UPW = LD::UPW;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int sub = lane & (LPU - 1);
+    const int64_t u = blk * ((kBlock / kWave) * UPW) + (threadIdx.x >> 6) * UPW + lane / LPU;
+    if (u >= a.num_users) return;
+#ifdef RG_PIPE2_CHECK_FIRST   // timing experiments: the hot test as a round trip of its own
+    if (p.counts_next[u] > 0) return;
+    apply_row<LD, kApplyPull, 0, false, true>(a, u, sub);
+#else
+    // a user with a claim of step t+1 was updated by the hot launch: its guard is loaded beside its
+    // other loads (wasted bytes for it, but no round trip in front of every row)
+    apply_row<LD, kApplyPull, 0, false, true, false, false, true>(a, u, sub);
+#endif
 }
 
 #ifdef RG_X_PIPE2
@@ -2311,6 +2440,23 @@ struct BackLaunchF {
 #ifndef RG_BACK_NT   // timing experiments: store policy of the V-layout dense pass (apply_row's NT)
 #define RG_BACK_NT 0
 #endif
+#ifdef RG_BACK_PIPE   // timing experiments: the persistent software-pipelined dense kernel (mf_dense_kernel)
+            if (!own) {
+                int64_t db = (int64_t)num_cus() * RG_BACK_PIPE;
+                const int64_t groups = (rows + L::UPW - 1) / L::UPW;
+                const int64_t need = (groups + kBlock / kWave - 1) / (kBlock / kWave);
+                if (db > need) db = need;
+                BackGrid dg{prep_blocks, 0, 0, 1, 0};
+                dg.apply_start = (head + 7) / 8 * 8;
+                const dim3 dgrid((unsigned)(dg.apply_start + db));
+                if (e0 || e1)
+                    hipExtLaunchKernelGGL(mf_dense_kernel<L>, dgrid, dim3(kBlock), 0, s, e0, e1, 0, *a, *prep, prep_out, db,
+                                          gen, dg);
+                else
+                    hipLaunchKernelGGL(mf_dense_kernel<L>, dgrid, dim3(kBlock), 0, s, *a, *prep, prep_out, db, gen, dg);
+                return check_launch("rg_mf_apply_prepare");
+            }
+#endif
             if (own) go(mf_back_kernel<L, 0, true, true>);
             else go(mf_back_kernel<L, RG_BACK_NT, true>);
             return check_launch("rg_mf_apply_prepare");
@@ -2464,6 +2610,136 @@ extern "C" int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *t, rg_mf_work
                   (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 #endif
+}
+
+namespace {
+struct Pipe2HotF {
+    ApplyArgs *a;
+    Pipe2Args p;
+    MtGenArgs gen;
+    int64_t hot_cap;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        using LD = typename BackLayout<L>::type;
+        constexpr int64_t rpb = (kBlock / kWave) * LD::UPW;
+        p.item_blocks = (a->num_items + rpb - 1) / rpb;
+        p.hot_blocks = (hot_cap + rpb - 1) / rpb;
+        int64_t total = p.item_blocks + p.hot_blocks + (gen.nwords > 0 ? 1 : 0);
+        if (total < 1) total = 1;
+        LaunchEvents &le = launch_events();
+        const hipEvent_t e0 = le.start, e1 = le.stop;
+        le = LaunchEvents{};
+        if (e0 || e1)
+            hipExtLaunchKernelGGL(mf_pipe2_hot_kernel<LD>, dim3((unsigned)total), dim3(kBlock), 0, s, e0, e1, 0, *a, p,
+                                  gen);
+        else
+            hipLaunchKernelGGL(mf_pipe2_hot_kernel<LD>, dim3((unsigned)total), dim3(kBlock), 0, s, *a, p, gen);
+        return check_launch("rg_mf_pipe2_hot");
+    }
+};
+
+struct Pipe2ColdF {
+    ApplyArgs *a;
+    PairsArgs *pa, *prep;
+    int2 *prep_out;
+    Pipe2Args p;
+    MtGenArgs gen;
+    hipStream_t s;
+    template <class L>
+    int operator()() {
+        if (pa->n_neg <= 5) return run<L, 5>();
+        return run<L, kNMax>();
+    }
+    template <class L, int NMAX>
+    int run() {
+        using LD = typename BackLayout<L>::type;
+        constexpr int64_t rpb = (kBlock / kWave) * LD::UPW;
+        p.pair_blocks = pairs_blocks<L>(pa->cols);
+        p.cold_blocks = (a->num_users + rpb - 1) / rpb;
+        const int64_t total = p.pair_blocks + (gen.nwords > 0 ? 1 : 0) + p.prep_blocks + p.cold_blocks;
+        LaunchEvents &le = launch_events();
+        const hipEvent_t e0 = le.start, e1 = le.stop;
+        le = LaunchEvents{};
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((mf_pipe2_cold_kernel<L, LD, NMAX>), dim3((unsigned)total), dim3(kBlock), 0, s, e0,
+                                  e1, 0, *a, *pa, *prep, prep_out, p, gen);
+        else
+            hipLaunchKernelGGL((mf_pipe2_cold_kernel<L, LD, NMAX>), dim3((unsigned)total), dim3(kBlock), 0, s, *a, *pa,
+                               *prep, prep_out, p, gen);
+        return check_launch("rg_mf_pipe2_cold");
+    }
+};
+}  // namespace
+
+static int gen_args(const rg_mt_gen_t *gen, MtGenArgs &g, const char *what) {
+    g = MtGenArgs{};
+    if (gen && gen->nwords > 0) {
+        if (!gen->state || !gen->out) return fail_arg(std::string(what) + ": null MT state / output");
+        g.state = gen->state; g.out = gen->out; g.state_before = gen->state_before; g.nwords = gen->nwords;
+    }
+    return RG_OK;
+}
+
+extern "C" int rg_mf_pipe2_hot(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                               const rg_mf_loss_t *loss, const int32_t *hot_users, const int32_t *nhot,
+                               int64_t hot_cap, int32_t *nhot_clear, const rg_mt_gen_t *gen) {
+    if (!hot_users || !nhot || hot_cap < 0) return fail_arg("rg_mf_pipe2_hot: null hot list");
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, 0, -1, loss, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    MtGenArgs g;
+    if ((rc = gen_args(gen, g, "rg_mf_pipe2_hot"))) return rc;
+    Pipe2Args p{};
+    p.hot = hot_users;
+    p.nhot = nhot;
+    p.nhot_clear = nhot_clear;
+    Pipe2HotF f{&a, p, g, hot_cap < t->num_users ? hot_cap : t->num_users, (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_pipe2_cold(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
+                                const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w, const int32_t *counts_next,
+                                const rg_mf_batch_t *next, const rg_mf_work_t *next_w, int32_t *hot_out,
+                                int32_t *nhot_out, const rg_mt_gen_t *gen) {
+    if (kPairBlock != kBlock) return fail_arg("rg_mf_pipe2_cold: built with a pair-pass workgroup != 256 threads");
+    if (!pair_b || !pair_w || !counts_next) return fail_arg("rg_mf_pipe2_cold: null pair batch / work / counts");
+    if (pair_b->loss != RG_LOSS_POINTWISE && pair_b->loss != RG_LOSS_BPR && pair_b->loss != RG_LOSS_HINGE)
+        return fail_arg("rg_mf_pipe2_cold: pointwise, bpr or hinge only (the adaptive hinge needs the max first)");
+    if (pair_w->claim_num_users <= 0 || pair_w->row_count != counts_next)
+        return fail_arg("rg_mf_pipe2_cold: the paired step must carry claimed slots in counts_next");
+    if (pair_w->row_list == w->row_list || pair_w->hot_grad == w->hot_grad || pair_w->loss_partials == w->loss_partials ||
+        (w->part_row && pair_w->part_row == w->part_row) || pair_w->row_count == w->row_count)
+        return fail_arg("rg_mf_pipe2_cold: the paired step's scratch must not alias this step's");
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, nullptr, opt, 0, t->num_users, nullptr, nullptr, kApplyPull, a);
+    if (rc) return rc;
+    // the pair pass of step t+1 reads the tables this step writes (their rows the hot launch wrote)
+    rg_mf_tables_t pt = *t;
+    pt.user_w = t->user_w_out; pt.item_w = t->item_w_out; pt.user_b = t->user_b_out; pt.item_b = t->item_b_out;
+    PairsArgs pa;
+    if ((rc = pairs_args(&pt, pair_b, pair_w, 1, pa))) return rc;
+    PairsArgs prep{};
+    int2 *prep_out = nullptr;
+    a.guard = counts_next;
+    Pipe2Args p{};
+    p.counts_next = counts_next;
+    if (next) {
+        if ((rc = prepare_args(next, next_w, nullptr, prep))) return rc;
+        if (!prep.claimed || !hot_out || !nhot_out)
+            return fail_arg("rg_mf_pipe2_cold: the prepared step needs claimed slots and a hot list");
+        if (next->pairs == pair_b->pairs) return fail_arg("rg_mf_pipe2_cold: prepared pairs alias the paired step's");
+        if (next_w->row_count == counts_next || next_w->row_count == w->row_count)
+            return fail_arg("rg_mf_pipe2_cold: the prepared step's claims alias a live count array");
+        prep.hot_out = hot_out;
+        prep.nhot_out = nhot_out;
+        prep_out = reinterpret_cast<int2 *>(next->pairs);
+        p.prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
+    }
+    MtGenArgs g;
+    if ((rc = gen_args(gen, g, "rg_mf_pipe2_cold"))) return rc;
+    Pipe2ColdF f{&a, &pa, &prep, prep_out, p, g, (hipStream_t)stream};
+    return dispatch_dim(t->dim, f);
 }
 
 #ifdef RG_X_PIPE2

@@ -59,6 +59,9 @@ extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w
                           int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w);
 static int64_t g_x_paired = -1;   // timing prototype: the unit whose pair pass ran in the last launch
 #endif
+#ifndef RG_PIPE2_DEFAULT
+#define RG_PIPE2_DEFAULT 0
+#endif
 namespace {
 
 constexpr int kSlots = 3;        // word slots in the ring
@@ -156,6 +159,9 @@ struct Stepper {
     int64_t hot_prepped = -1;              // unit prepared with claims and a hot list, pair pending
     rg_mf_step_in_t hot_in{};
     int64_t last_pipe = -1;                // unit of the last pipelined launch (its counter resets)
+    // two-launch pipelined step (train_pipe2, the single-GPU default): the same per-unit scratch
+    // parities as `pipe`, no gate
+    bool pipe2 = false;
 };
 
 int hip_fail(const char *what, hipError_t e) {
@@ -714,7 +720,7 @@ int pipe_clean_accum(Stepper &st, hipStream_t s, int k) {
 // drop every pipelined unit not trained yet (a pair pass and / or a prepare ahead): their
 // claims and overflow adds are cleared; their words stay (input independent)
 int pipe_abandon(Stepper &st, hipStream_t s) {
-    if (!st.pipe) return RG_OK;
+    if (!st.pipe && !st.pipe2) return RG_OK;
     int rc = RG_OK;
     for (int k = 0; k < 3 && rc == RG_OK; ++k) rc = pipe_clean_counts(st, s, k);
     for (int k = 0; k < 2 && rc == RG_OK; ++k) rc = pipe_clean_accum(st, s, k);
@@ -835,6 +841,113 @@ int train_pipe(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_
         st.hot_prepped = -1;
     }
     st.last_pipe = unit;
+    st.set = 1 - st.set;
+    return RG_OK;
+}
+
+// Two-launch pipelined step of unit t = taken (rg_mf_pipe2_hot / rg_mf_pipe2_cold):
+//   hot  (t): step t's dense update of every item row and of the users step t+1's pair pass reads
+//   cold (t): step t+1's pair pass | the MT walk | step t+2's prepare | step t's dense update of
+//             every other user
+// Preconditions carried from the previous call: step t's pair pass ran (its lists), step t+1 was
+// prepared with claims and its hot list.  A cold start (nothing pending, or pending for another
+// input) runs prepare t, pair pass t and prepare t+1 as launches of their own; without `next` the
+// step is the plain dense pass and the pipeline drains; without `next2` the cold launch prepares
+// nothing ahead (the next call prepares its t+1 on its own).
+int train_pipe2(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg_mf_step_in_t *next,
+                const rg_mf_step_in_t *next2, float *loss_out, void *ev0, void *ev1) {
+    const int64_t unit = st.taken;
+    int rc = st.inline_gen ? generate_upto(st, unit + (next2 ? 2 : next ? 1 : 0), 0) : keep_ahead(st, unit);
+    if (rc) return rc;
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    const rg_mf_tables_t &t0 = st.cfg.tables[0];
+    rg_mf_work_t w = pipe_work(st, cur, unit);
+    const rg_mf_batch_t batch = make_batch(st, cur, unit);
+    if (!(st.paired == unit && same_input(st.paired_in, cur))) {
+        // cold start: whatever ran ahead belongs to another input
+        if ((rc = pipe_abandon(st, s))) return rc;
+        if ((rc = wait_side(st, s, (int)(unit % 2))) || (rc = wait_words(st, s, unit))) return rc;
+        if ((rc = rg_mf_prepare(s, &batch, &w))) return rc;
+        st.pdirty[unit % 3] = true;
+        if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) return rc;
+        st.pair_dirty[unit % 2] = true;
+        st.paired = unit;
+        st.paired_in = cur;
+    }
+    st.cfg.step += 1;
+    const rg_opt_t o = opt_at(st, st.cfg.step);
+    const rg_mf_loss_t l = loss_of(st, cur.global_pos, loss_out);
+    const int64_t U = t0.num_users, R = U + t0.num_items;
+    if (!next) {                       // the last step of a sequence: dense pass only
+        if ((rc = release(st, s))) return rc;
+        rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};
+        rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, R, &l, nullptr, nullptr, nullptr);
+        rg::launch_events() = rg::LaunchEvents{};
+        if (rc) return rc;
+        st.pdirty[unit % 3] = false;
+        st.pair_dirty[unit % 2] = false;
+        st.paired = -1;
+        st.hot_prepped = -1;
+        st.set = 1 - st.set;
+        return RG_OK;
+    }
+    const int64_t u1 = unit + 1, u2 = unit + 2;
+    rg_mf_work_t w1 = pipe_work(st, *next, u1);
+    const rg_mf_batch_t b1 = make_batch(st, *next, u1);
+    int32_t *nhot = st.pint;
+    if (!(st.hot_prepped == u1 && same_input(st.hot_in, *next))) {
+        if ((rc = pipe_clean_counts(st, s, (int)(u1 % 3)))) return rc;
+        if ((rc = pipe_clean_accum(st, s, (int)(u1 % 2)))) return rc;
+        if ((rc = wait_side(st, s, (int)(u1 % 2))) || (rc = wait_words(st, s, u1))) return rc;
+        if ((rc = pipe_memset(nhot + u1 % 3, sizeof(int32_t), s, "stepper: hot list"))) return rc;
+        if ((rc = rg_mf_prepare_hot(s, &b1, &w1, st.hot[u1 % 3], nhot + u1 % 3))) return rc;
+        st.pdirty[u1 % 3] = true;
+        st.hot_prepped = u1;
+        st.hot_in = *next;
+    }
+    rg_mf_batch_t b2{};
+    rg_mf_work_t w2{};
+    if (next2) {
+        if ((rc = pipe_clean_counts(st, s, (int)(u2 % 3)))) return rc;
+        if ((rc = wait_side(st, s, (int)(u2 % 2))) || (rc = wait_words(st, s, u2))) return rc;
+        b2 = make_batch(st, *next2, u2);
+        w2 = pipe_work(st, *next2, u2);
+    }
+    if ((rc = pipe_clean_accum(st, s, (int)(u1 % 2)))) return rc;   // set u1 % 2 is the pair pass's
+    if ((rc = release(st, s))) return rc;
+    rg_mt_gen_t gen{};
+    int gen_slot = -1;
+    if (st.inline_gen && st.gen_slots == rel_slot(st, unit + 3)) {
+        gen_slot = (int)(st.gen_slots % kSlots);
+        if ((rc = begin_production(st, s, gen_slot))) return rc;
+        gen.state = st.cfg.mt_state;
+        gen.out = st.words[gen_slot];
+        gen.state_before = st.start_state[gen_slot];
+        gen.nwords = st.G * st.W;
+    }
+    const int64_t hot_cap = std::min<int64_t>(U, (int64_t)(1 + st.cfg.n_neg) * st.cfg.cols);
+    if ((rc = rg_mf_pipe2_hot(s, tb, &w, &o, &l, st.hot[u1 % 3], nhot + u1 % 3, hot_cap,
+                              next2 ? nhot + u2 % 3 : nullptr, nullptr)))
+        return rc;
+    rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // the cold launch
+    rc = rg_mf_pipe2_cold(s, tb, &w, &o, &b1, &w1, st.pcounts[u1 % 3], next2 ? &b2 : nullptr,
+                          next2 ? &w2 : nullptr, next2 ? st.hot[u2 % 3] : nullptr, next2 ? nhot + u2 % 3 : nullptr,
+                          gen_slot >= 0 ? &gen : nullptr);
+    rg::launch_events() = rg::LaunchEvents{};
+    if (rc) return rc;
+    if (gen_slot >= 0) end_production(st, s, gen_slot);
+    st.pdirty[unit % 3] = false;                 // the two launches consumed and reset its claims
+    st.pair_dirty[unit % 2] = false;             // and its overflow accumulators
+    st.pair_dirty[u1 % 2] = true;
+    st.paired = u1;
+    st.paired_in = *next;
+    if (next2) {
+        st.pdirty[u2 % 3] = true;
+        st.hot_prepped = u2;
+        st.hot_in = *next2;
+    } else {
+        st.hot_prepped = -1;
+    }
     st.set = 1 - st.set;
     return RG_OK;
 }
@@ -1417,7 +1530,13 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         st->pipe = upb > 0 && (cfg->cols + upb - 1) / upb <= 2 * (int64_t)rg::num_cus() &&
                    std::max(t0.num_users, t0.num_items) * (int64_t)t0.dim * 4 < ((int64_t)1 << 31);
     }
-    if (st->pipe) {
+    // two-launch pipelined step (rg_mf_pipe2_hot / _cold) for the single-rank losses with claimed
+    // slots: RG_PIPE2=1 selects it, RG_PIPE2_DEFAULT the build's default (0: the split step, which
+    // measures faster -- DESIGN §4.1)
+    st->pipe2 = !st->pipe && env_flag("RG_PIPE2", RG_PIPE2_DEFAULT != 0) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
+                (cfg->loss == RG_LOSS_POINTWISE || cfg->loss == RG_LOSS_BPR || cfg->loss == RG_LOSS_HINGE) &&
+                cfg->work.part_row && cfg->work.part_bias && cfg->work.loss_partials && cfg->n_partials > 0;
+    if (st->pipe || st->pipe2) {
         const int64_t rows = t0.num_users + t0.num_items;
         const int64_t hot_len = std::min<int64_t>(t0.num_users, (int64_t)(1 + cfg->n_neg) * cfg->cols);
         e = hipMalloc(&st->p_counts2, (size_t)rows * sizeof(int32_t));
@@ -1471,6 +1590,7 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
         return train_owner(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     }
     if (st->pipe) return train_pipe(*st, s, *cur, next, nullptr, loss_out, ev_apply_begin, ev_apply_end);
+    if (st->pipe2) return train_pipe2(*st, s, *cur, next, nullptr, loss_out, ev_apply_begin, ev_apply_end);
     if (st->fused && st->cfg.loss != RG_LOSS_ADAPTIVE_HINGE)
         return train_fused(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
     if (st->lazy) return train_lazy(*st, s, *cur, next, loss_out, ev_apply_begin, ev_apply_end);
@@ -1484,13 +1604,15 @@ extern "C" int rg_mf_stepper_train_ahead(void *h, void *stream, const rg_mf_step
     if (!st || !cur) return rg::fail_arg("rg_mf_stepper_train_ahead: null handle/input");
     if (!next && next2) return rg::fail_arg("rg_mf_stepper_train_ahead: next2 without next");
     if (st->pipe) return train_pipe(*st, (hipStream_t)stream, *cur, next, next2, loss_out, ev_apply_begin, ev_apply_end);
+    if (st->pipe2 && st->cfg.dp_mode == 0)
+        return train_pipe2(*st, (hipStream_t)stream, *cur, next, next2, loss_out, ev_apply_begin, ev_apply_end);
     return rg_mf_stepper_train(h, stream, cur, next, loss_out, ev_apply_begin, ev_apply_end);
 }
 
 extern "C" int rg_mf_stepper_pipelined(void *h) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st) return rg::fail_arg("rg_mf_stepper_pipelined: null handle");
-    return st->pipe ? 1 : 0;
+    return st->pipe ? 1 : st->pipe2 ? 2 : 0;
 }
 
 extern "C" int rg_mf_stepper_pipe_error(void *h, int32_t *err_out) {
@@ -1682,7 +1804,7 @@ extern "C" int rg_mf_stepper_state(void *h, int32_t *current_set, int64_t *step)
 extern "C" int rg_mf_stepper_advance(void *h, int32_t flip_sets, int64_t steps) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st) return rg::fail_arg("rg_mf_stepper_advance: null handle");
-    if (st->pipe && (st->paired >= 0 || st->hot_prepped >= 0))
+    if ((st->pipe || st->pipe2) && (st->paired >= 0 || st->hot_prepped >= 0))
         return rg::fail_arg("rg_mf_stepper_advance: a pipelined step is pending (acquire first)");
     if (st->lazy_pending) return rg::fail_arg("rg_mf_stepper_advance: lazy rows pending (rg_mf_stepper_flush first)");
     if (flip_sets) st->set = 1 - st->set;

@@ -503,8 +503,14 @@ class MFEngine:
 
     @property
     def pipelined(self):
-        """True if the native step is the pipelined one (rg_mf_pipe_step)."""
+        """True if the native step is the single-launch pipelined one (rg_mf_pipe_step, A/B build)."""
         return self.lib.rg_mf_stepper_pipelined(self._stepper) == 1
+
+    @property
+    def pipeline_kind(self):
+        """0: the split step; 1: the single-launch pipelined step (A/B build); 2: the two-launch
+        pipelined step (rg_mf_pipe2_hot / rg_mf_pipe2_cold, the single-GPU default)."""
+        return int(self.lib.rg_mf_stepper_pipelined(self._stepper))
 
     def pipe_error(self):
         """True if a pipelined launch's pair workgroups ran out of their bounded wait (then its

@@ -25,7 +25,7 @@ import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        if any(k in n for k in ("mf_pairs", "mf_back", "mf_prepare", "mt_generate")):
+        if any(k in n for k in ("mf_pairs", "mf_back", "mf_prepare", "mt_generate", "pipe2", "mf_dense")):
             print(sys.argv[2], n.split("(")[0].split("::")[-1][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 2), "us")
 PY
 done
