@@ -123,6 +123,10 @@ def parse():
     ap.add_argument("--events-every", type=int, default=10,
                     help="record the dominant kernel's timing events on every k-th timed step (each event "
                          "pair leaves a ~6 us bubble on the stream: 2 pairs in the driver's 20 steps)")
+    ap.add_argument("--host-ahead", type=float, default=0.0, metavar="MS",
+                    help="diagnostic: a MS-long spin kernel before the timed steps lets the host enqueue them "
+                         "all ahead; the step time is then taken by events after the spin (GPU-side time only, "
+                         "reported as gpu_ahead_us_per_step; not the driver's line)")
     return ap.parse_args()
 
 
@@ -744,9 +748,17 @@ def main():
     if multi:
         dist.barrier()
     torch.cuda.synchronize()
+    ahead = None
+    if args.host_ahead > 0:
+        # ~2.1 GHz shader clock: the spin outlasts the host's enqueue of every timed step
+        torch.cuda._sleep(int(args.host_ahead * 2.1e6))
+        ahead = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ahead[0].record()
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s, evs[s])
+    if ahead is not None:
+        ahead[1].record()
     # the lazy pass leaves cold user rows behind: catching them all up is part of the timed
     # work (after this every row equals the eager pass's; no-op when eager)
     eng.flush()
@@ -781,8 +793,14 @@ def main():
         lazy_rows = eng.lazy_rows(enable=False) / (n_extra - 1)
         eng.flush()
 
+    if ahead is not None:
+        torch.cuda.synchronize()
+        ahead = ahead[0].elapsed_time(ahead[1]) * 1e3 / args.steps
+        if t_enq * 1e3 > args.host_ahead:
+            print(f"warning: the host took {t_enq * 1e3:.2f} ms to enqueue, longer than the {args.host_ahead} ms spin",
+                  file=sys.stderr)
     if emu is not None:
-        return report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq)
+        return report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq, ahead)
     if rank == 0:
         value = args.steps * B * world / el
         # per rank: its user shard + every item go through the dense optimizer pass
@@ -813,6 +831,11 @@ def main():
                                 "achieved_GBs": step_bytes / (el / args.steps) / 1e9,
                                 "frac": step_bytes / (el / args.steps) / 1e9 / HBM_PEAK_GBS}
         out["host_enqueue_us_per_step"] = t_enq / args.steps * 1e6
+        if ahead is not None:   # --host-ahead diagnostic (the wall time includes the spin)
+            out["gpu_ahead_us_per_step"] = ahead
+            out["ms_per_step"] = ahead * 1e-3
+            out["value"] = B * world / (ahead * 1e-6)
+            out["timing"] = "GPU events after a host-ahead spin (diagnostic)"
         if lazy_rows is not None:
             out["lazy_dense_pass"] = {
                 "user_rows_per_step": lazy_rows, "user_rows": U_local,
@@ -889,7 +912,7 @@ def main():
         dist.destroy_process_group()
 
 
-def report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq):
+def report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq, ahead=None):
     """--emulate-rank: one JSON line for rank R's step at W-rank geometry (NOT the driver's
     metric line): its time per step, the user-update kernel's events, and what W ranks each
     taking this step time would process (exchange time over xGMI NOT included: the
@@ -914,6 +937,13 @@ def report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq):
            # time means the GPU waits for the host
            "host_enqueue_us_per_step": t_enq / args.steps * 1e6,
            "final_loss": float(eng.loss_out[0])}
+    if ahead is not None:
+        # --host-ahead: every step enqueued before the GPU reached it (the wall time above
+        # includes the spin): the GPU-side step time alone
+        out["gpu_ahead_us_per_step"] = ahead
+        out["ms_per_step"] = ahead * 1e-3
+        out["value"] = B * w_ / (ahead * 1e-6)
+        out["timing"] = "GPU events after a host-ahead spin (diagnostic)"
     print(json.dumps(out), flush=True)
     eng.comm.close()
 

@@ -392,6 +392,18 @@ int rg_mf_grads_sharded(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t
 int rg_mf_apply_shard(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
                       int64_t shard_users, int64_t shard_items, int32_t world, int32_t rank, float *loss_out_dev);
 
+/* The owner-sharded step's item update split the same way (dp_mode 2 with shard_items = Is > 0):
+ * rg_mf_grads_item_shard writes the item rows' data gradient rank-major, chunk s =
+ * [item rows s*Is .. (s+1)*Is (dim floats each) | their Is biases | the loss share], each chunk
+ * rg_mf_item_grad_chunk(Is, dim) floats; after a reduce-scatter rg_mf_apply_item_shard updates
+ * items [rank*Is, min((rank+1)*Is, num_items)) into item_w_out / item_b_out, and an all-gather of
+ * those two tables (counts Is*dim, Is; allocated with world*Is rows) completes the item update. */
+int64_t rg_mf_item_grad_chunk(int64_t shard_items, int32_t dim);
+int rg_mf_grads_item_shard(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *work, float *grad_dev,
+                           int64_t shard_items, int32_t world, const rg_mf_loss_t *loss);
+int rg_mf_apply_item_shard(void *stream, const rg_mf_tables_t *tables, const float *grad_dev, const rg_opt_t *opt,
+                           int64_t shard_items, int32_t world, int32_t rank, float *loss_out_dev);
+
 /* ------------------------------------------------------------------------------
  * Owner-sharded data-parallel step (dp_mode 2; rg_owner.hip), reference-exact: R ranks
  * at batch B compute the reference's step at batch R*B (one global CPython stream of
@@ -567,7 +579,9 @@ typedef struct rg_mf_stepper_config {
     int32_t n_neg, loss;
     int64_t cols, col_offset, global_cols;   /* draw layout: j = (q-1)*global_cols + col_offset + col */
     int64_t neg_cols;               /* negatives per draw row over every rank (loss denominator) */
-    float *item_grad;               /* [num_items*(dim+1) + 1]: user-sharded DP step when non-null */
+    float *item_grad;               /* [num_items*(dim+1) + 1] (shard_items > 0 in dp_mode 2:
+                                       [world * rg_mf_item_grad_chunk(shard_items, dim)]): the
+                                       user-sharded DP step when non-null */
     void *comm;                     /* rg_comm_create handle (NULL: single rank, no exchange) */
     rg_opt_t opt;                   /* kind + fp32 hyper-parameters */
     double lr_d, beta1_d, beta2_d;  /* the same as Python floats (Adam bias corrections) */

@@ -315,6 +315,12 @@ SIGNATURES = [
     ("rg_mf_apply_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,
                                          ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_void_p]),
+    ("rg_mf_item_grad_chunk", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    ("rg_mf_grads_item_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.POINTER(MFWork),
+                                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(MFLoss)]),
+    ("rg_mf_apply_item_shard", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MFTables), ctypes.c_void_p,
+                                              ctypes.POINTER(Opt), ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.c_void_p]),
     ("rg_mf_stepper_dp_begin", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),
                                               ctypes.POINTER(MFStepIn), ctypes.c_void_p]),
     ("rg_mf_stepper_dp_end", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

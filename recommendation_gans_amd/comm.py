@@ -95,7 +95,8 @@ class HostComm(RcclComm):
     D2H -> a stream-ordered host callback summing over the group with torch.distributed -> H2D
     (rg_comm_create_host), so the step's own placement -- the score exchange fenced on the main
     stream, the item gradient's exchange on the side stream beside the user update -- runs as in
-    production.  Reduce-scatter / all-gather are not provided.
+    production.  A reduce-scatter is staged as an all-reduce of every chunk (each rank then reads
+    its own), an all-gather as an all-reduce with every other rank's chunk zeroed first.
 
     The callback takes the GIL on the runtime's callback thread: while the step's work is in
     flight, wait with ``sync()`` (a ctypes call, which releases the GIL), not with a torch call

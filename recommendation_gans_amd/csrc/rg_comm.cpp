@@ -222,8 +222,9 @@ int comm_end(void *h, hipStream_t stream) {
 int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || !buf || chunk < 0) return fail_arg("rg_comm_reduce_scatter_f32: bad argument");
-    if (c->local) return local_roundtrip(c, stream, buf + (int64_t)c->rank * chunk, chunk * c->world);
-    if (c->host_fn) return fail_arg("rg_comm (host): reduce-scatter not supported (all-reduce only)");
+    if (c->local) return local_roundtrip(c, stream, buf, chunk * c->world);   // the exchange's bytes
+    // host-staged: an all-reduce of every chunk (this rank then reads its own, summed)
+    if (c->host_fn) return host_allreduce(c, stream, buf, chunk * c->world);
     return nccl_after(c, stream, ncclReduceScatter(buf, buf + (int64_t)c->rank * chunk, (size_t)chunk, ncclFloat32,
                                                    ncclSum, c->comm, stream), "ncclReduceScatter");
 }
@@ -231,7 +232,20 @@ int comm_reduce_scatter(void *h, hipStream_t stream, float *buf, int64_t chunk) 
 int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const int64_t *counts) {
     Comm *c = static_cast<Comm *>(h);
     if (!c || n < 0 || (n > 0 && (!bufs || !counts))) return fail_arg("rg_comm_allgather_f32: bad argument");
-    if (c->host_fn) return fail_arg("rg_comm (host): all-gather not supported (all-reduce only)");
+    if (c->host_fn) {
+        // host-staged: every other rank's chunk zeroed, then an all-reduce (the sum is the gather)
+        for (int k = 0; k < n; ++k) {
+            const int64_t cnt = counts[k], r = c->rank;
+            hipError_t e = hipSuccess;
+            if (r > 0) e = hipMemsetAsync(bufs[k], 0, (size_t)(r * cnt) * sizeof(float), stream);
+            if (e == hipSuccess && r + 1 < c->world)
+                e = hipMemsetAsync(bufs[k] + (r + 1) * cnt, 0, (size_t)((c->world - r - 1) * cnt) * sizeof(float), stream);
+            if (e != hipSuccess) return hip_fail("rg_comm (host): all-gather", e);
+            const int rc = host_allreduce(c, stream, bufs[k], cnt * c->world);
+            if (rc) return rc;
+        }
+        return RG_OK;
+    }
     if (c->local) {
         for (int k = 0; k < n; ++k) {
             const int rc = local_roundtrip(c, stream, bufs[k], counts[k] * c->world);

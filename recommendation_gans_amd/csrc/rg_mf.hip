@@ -614,6 +614,10 @@ struct ApplyArgs {
     // biases (Us + Is) | loss], D floats per row
     int64_t shard_users, shard_items, chunk;
     int32_t world, rank;
+    // owner-sharded step's item exchange (rg_mf_grads_item_shard / rg_mf_apply_item_shard): the
+    // rank-major chunks hold item rows only (shard_users = 0): chunk s = [item rows s*Is .. | their
+    // biases | loss]
+    int32_t item_shard;
     // lazy dense pass: a USER row with a zero data gradient that the next step
     // does not read is skipped; its cold updates (weight decay + optimizer state only) are
     // applied, in order and with each step's constants, when the row is next processed
@@ -673,7 +677,7 @@ __device__ __forceinline__ void sort_entries(int2 (&ent)[8], int ne) {
 // location of unified row r's gradient in the flat buffer: *row_base + k*D, bias at *bias
 __device__ __forceinline__ void grad_loc(const ApplyArgs &a, int t, int64_t lr_, int64_t gk, int64_t nr,
                                          const float *&row_base, int64_t &k, int64_t &bias) {
-    if (a.shard_users > 0) {
+    if (a.shard_users > 0 || a.item_shard) {
         const int64_t s = t ? lr_ / a.shard_items : lr_ / a.shard_users;
         k = t ? a.shard_users + lr_ % a.shard_items : lr_ % a.shard_users;
         row_base = a.grad + s * a.chunk;
@@ -1391,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
         const float lv = finalize_loss_wg<kBlock>(a.partials, a.n_partials, a.inv_a, a.inv_b);
         if (threadIdx.x < kWave) {
             if (lane == 0) *a.loss_out = lv;
-            if (MODE == kGradOnly && a.shard_users > 0) {
+            if (MODE == kGradOnly && (a.shard_users > 0 || a.item_shard)) {
                 for (int s = lane; s < a.world; s += kWave) a.grad[s * a.chunk + slot_off] = lv;   // summed by the RS
             } else if (MODE == kGradOnly && lane == 0) {
                 a.grad[nr * (int64_t)(D + 1)] = lv;
@@ -1399,11 +1403,14 @@ __global__ __launch_bounds__(kBlock) void mf_apply_kernel(ApplyArgs a) {
         }
     }
     if (MODE == kApplyDense && a.loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-        *a.loss_out = a.shard_users > 0 ? a.grad[a.rank * a.chunk + slot_off] : a.grad[nr * (int64_t)(D + 1)];
+        *a.loss_out = (a.shard_users > 0 || a.item_shard) ? a.grad[a.rank * a.chunk + slot_off]
+                                                         : a.grad[nr * (int64_t)(D + 1)];
 
     if (k >= nr) return;
     int64_t r;
-    if (MODE == kApplyDense && a.shard_users > 0) {
+    if (MODE == kApplyDense && a.item_shard) {
+        r = a.num_users + a.rank * a.shard_items + k;         // this rank's item shard only
+    } else if (MODE == kApplyDense && a.shard_users > 0) {
         // this rank's shard: [rb, rb + nu) users, then items from U + rank * Is
         const int64_t u0 = a.rank * a.shard_users, i0 = a.rank * a.shard_items;
         const int64_t u1 = u0 + a.shard_users < a.num_users ? u0 + a.shard_users : a.num_users;
@@ -3317,6 +3324,48 @@ extern "C" int rg_mf_apply_shard(void *stream, const rg_mf_tables_t *t, const fl
     const int64_t ni = i0 < t->num_items ? std::min(shard_items, t->num_items - i0) : 0;
     a.row_begin = 0;
     a.row_end = nu + ni;            // rows of the shard, mapped in mf_apply_kernel
+    ApplyLaunchF f{&a, (hipStream_t)stream, kApplyDense};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int64_t rg_mf_item_grad_chunk(int64_t shard_items, int32_t dim) {
+    if (shard_items < 1 || dim < 1) return -1;
+    return (shard_items * (int64_t)(dim + 1) + 1 + 3) / 4 * 4;
+}
+
+static int item_shard_args(const rg_mf_tables_t *t, int64_t si, int32_t world, int32_t rank, ApplyArgs &a) {
+    if (world < 1 || rank < 0 || rank >= world) return fail_arg("rg_mf item shard: bad rank / world");
+    if (si < 1 || si * world < t->num_items) return fail_arg("rg_mf item shard: shards do not cover the items");
+    a.shard_users = 0;
+    a.shard_items = si;
+    a.item_shard = 1;
+    a.chunk = rg_mf_item_grad_chunk(si, t->dim);
+    a.world = world;
+    a.rank = rank;
+    return RG_OK;
+}
+
+extern "C" int rg_mf_grads_item_shard(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, float *grad_dev,
+                                      int64_t shard_items, int32_t world, const rg_mf_loss_t *loss) {
+    if (!grad_dev) return fail_arg("rg_mf_grads_item_shard: null grad");
+    ApplyArgs a;
+    int rc = apply_args(t, w, nullptr, grad_dev, nullptr, t->num_users, t->num_users + t->num_items, loss, nullptr,
+                        kGradOnly, a);
+    if (rc || (rc = item_shard_args(t, shard_items, world, 0, a))) return rc;
+    ApplyLaunchF f{&a, (hipStream_t)stream, kGradOnly};
+    return dispatch_dim(t->dim, f);
+}
+
+extern "C" int rg_mf_apply_item_shard(void *stream, const rg_mf_tables_t *t, const float *grad_dev,
+                                      const rg_opt_t *opt, int64_t shard_items, int32_t world, int32_t rank,
+                                      float *loss_out_dev) {
+    if (!grad_dev) return fail_arg("rg_mf_apply_item_shard: null grad");
+    ApplyArgs a;
+    int rc = apply_args(t, nullptr, grad_dev, nullptr, opt, 0, -1, nullptr, loss_out_dev, kApplyDense, a);
+    if (rc || (rc = item_shard_args(t, shard_items, world, rank, a))) return rc;
+    const int64_t i0 = rank * shard_items;
+    a.row_begin = 0;
+    a.row_end = i0 < t->num_items ? std::min(shard_items, t->num_items - i0) : 0;   // mapped in mf_apply_kernel
     ApplyLaunchF f{&a, (hipStream_t)stream, kApplyDense};
     return dispatch_dim(t->dim, f);
 }

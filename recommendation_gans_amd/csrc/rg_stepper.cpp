@@ -1170,22 +1170,38 @@ int owner_begin(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur) {
     return RG_OK;
 }
 
-// part 2 (after the score exchange): dL/dz, contribution lists, the item rows' data gradient
-// (grad_stream: where the item gradient runs, ordered after the backward on s)
-int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr,
-              hipEvent_t after_back = nullptr) {
+// the owner step with a sharded item update (dp_mode 2, shard_items > 0, a communicator of more than
+// one rank): the item gradient in rank-major chunks -> reduce-scatter -> this rank's 1/R of the
+// items' optimizer update -> all-gather of the updated item rows and biases (the same wire bytes as
+// the all-reduce, 1/R of the update work)
+bool item_sharded(const Stepper &st) {
+    return st.cfg.dp_mode == 2 && st.cfg.shard_items > 0 && st.cfg.comm != nullptr && st.cfg.world > 1;
+}
+
+// part 2a (after the score exchange): dL/dz and the contribution lists (after_back: recorded
+// after them -- the user rows' lists are complete, their update need not wait for the items')
+int owner_backward(Stepper &st, hipStream_t s, hipEvent_t after_back = nullptr) {
     if (st.own_stage != 1) return rg::fail_arg("rg_mf_stepper_owner_mid: owner_begin must come first");
     const rg_mf_owner_batch_t b = owner_batch(st, st.own_in, st.own_unit);
     rg_mf_work_t w = owner_work(st, st.own_in, st.own_unit);
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     int rc = RG_OK;
     if (st.cfg.loss == RG_LOSS_ADAPTIVE_HINGE && (rc = rg_mf_owner_adapt(s, &b))) return rc;   // global max, count
-    rc = rg_mf_owner_back(s, tb, &b, &w);
-    if (rc) return rc;
-    if (after_back) {   // the user rows' lists are complete: their update need not wait for the items'
+    if ((rc = rg_mf_owner_back(s, tb, &b, &w))) return rc;
+    if (after_back) {
         const hipError_t e = hipEventRecord(after_back, s);
         if (e != hipSuccess) return hip_fail("stepper: record the backward", e);
     }
+    st.own_stage = 3;
+    return RG_OK;
+}
+
+// part 2b: the item rows' data gradient (grad_stream: where it runs, ordered after the backward on s)
+int owner_item_grad(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr) {
+    if (st.own_stage != 3) return rg::fail_arg("rg_mf_stepper_owner_mid: the backward must come first");
+    rg_mf_work_t w = owner_work(st, st.own_in, st.own_unit);
+    const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
+    int rc = RG_OK;
     if (grad_stream && grad_stream != s) {
         hipError_t e = hipSuccess;
         if (!st.own_back) e = hipEventCreateWithFlags(&st.own_back, hipEventDisableTiming | hipEventDisableSystemFence);
@@ -1198,9 +1214,17 @@ int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stre
     l.n_partials = rg_mf_owner_partials_used(st.cfg.global_cols, st.cfg.n_neg, tb->dim, st.cfg.world,
                                              st.own_in.n_planned) / 2;
     const int64_t U = tb->num_users, R = U + tb->num_items;
-    if ((rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l))) return rc;
+    if (item_sharded(st)) rc = rg_mf_grads_item_shard(s, tb, &w, st.cfg.item_grad, st.cfg.shard_items, st.cfg.world, &l);
+    else rc = rg_mf_grads(s, tb, &w, st.cfg.item_grad, U, R, &l);
+    if (rc) return rc;
     st.own_stage = 2;
     return RG_OK;
+}
+
+// part 2 (the caller-run exchange API): 2a then 2b
+int owner_mid(Stepper &st, hipStream_t s, float *loss_out, hipStream_t grad_stream = nullptr) {
+    const int rc = owner_backward(st, s);
+    return rc ? rc : owner_item_grad(st, s, loss_out, grad_stream);
 }
 
 // part 3 (after the item-gradient exchange, or beside it on the communicator stream): the
@@ -1233,7 +1257,17 @@ int owner_user_update(Stepper &st, hipStream_t s, const rg_mf_step_in_t *next, c
 int owner_item_update(Stepper &st, hipStream_t s, const rg_opt_t &o, float *loss_out) {
     const rg_mf_tables_t *tb = &st.cfg.tables[st.set];
     const int64_t U = tb->num_users, R = U + tb->num_items;
-    int rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out);
+    int rc;
+    if (item_sharded(st)) {
+        const int64_t si = st.cfg.shard_items;
+        rc = rg_mf_apply_item_shard(s, tb, st.cfg.item_grad, &o, si, st.cfg.world, st.cfg.rank, loss_out);
+        if (rc) return rc;
+        float *bufs[2] = {tb->item_w_out, tb->item_b_out};
+        const int64_t counts[2] = {si * (int64_t)tb->dim, si};
+        rc = rg::comm_allgather(st.cfg.comm, s, 2, bufs, counts);
+    } else {
+        rc = rg_mf_apply_dense(s, tb, st.cfg.item_grad, &o, U, R, loss_out);
+    }
     if (rc) return rc;
     st.set = 1 - st.set;
     st.own_stage = 0;
@@ -1260,23 +1294,38 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     hipStream_t u = side ? rg::comm_stream(st.cfg.comm) : s;
     hipError_t e = hipSuccess;
     if (side) {
-        if (!st.own_grads) e = hipEventCreateWithFlags(&st.own_grads, hipEventDisableTiming);
-        if (e == hipSuccess && !st.own_users) e = hipEventCreateWithFlags(&st.own_users, hipEventDisableTiming);
+        // same-device ordering only: no system-scope fence (a cache write-back at every marker)
+        const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
+        if (!st.own_grads) e = hipEventCreateWithFlags(&st.own_grads, evf);
+        if (e == hipSuccess && !st.own_users) e = hipEventCreateWithFlags(&st.own_users, evf);
         if (e != hipSuccess) return hip_fail("stepper: owner events", e);
     }
     // the user update starts after the backward (its lists), beside the item-gradient pull, the
-    // item exchange and the item update (they touch item rows; it touches user rows)
-    if ((rc = owner_mid(st, s, loss_out, nullptr, side ? st.own_grads : nullptr))) return rc;
+    // item exchange and the item update (they touch item rows; it touches user rows).  It is
+    // ENQUEUED first too: the host's launches of the pull and the exchange (a few us each) would
+    // otherwise hold it back
+    if ((rc = owner_backward(st, s, side ? st.own_grads : nullptr))) return rc;
     if (side && (e = hipStreamWaitEvent(u, st.own_grads, 0)) != hipSuccess)
         return hip_fail("stepper: order the user update", e);
-    if ((rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1)))
-        return rc;
+    const rg_opt_t o = opt_at(st, st.cfg.step + 1);
+    if (side) {
+        if ((rc = record(ev0, u))) return rc;
+        if ((rc = owner_user_update(st, u, next, o))) return rc;
+        if ((rc = record(ev1, u))) return rc;
+        if ((e = hipEventRecord(st.own_users, u)) != hipSuccess) return hip_fail("stepper: record the user update", e);
+    }
+    if ((rc = owner_item_grad(st, s, loss_out))) return rc;
+    if (item_sharded(st))
+        rc = rg::comm_reduce_scatter(st.cfg.comm, s, st.cfg.item_grad, rg_mf_item_grad_chunk(st.cfg.shard_items, tb->dim));
+    else
+        rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1);
+    if (rc) return rc;
     st.cfg.step += 1;
-    const rg_opt_t o = opt_at(st, st.cfg.step);
-    if ((rc = record(ev0, u))) return rc;
-    if ((rc = owner_user_update(st, u, next, o))) return rc;
-    if ((rc = record(ev1, u))) return rc;
-    if (side && (e = hipEventRecord(st.own_users, u)) != hipSuccess) return hip_fail("stepper: record the user update", e);
+    if (!side) {
+        if ((rc = record(ev0, u))) return rc;
+        if ((rc = owner_user_update(st, u, next, o))) return rc;
+        if ((rc = record(ev1, u))) return rc;
+    }
     if ((rc = owner_item_update(st, s, o, loss_out))) return rc;
     if (side && (e = hipStreamWaitEvent(s, st.own_users, 0)) != hipSuccess)
         return hip_fail("stepper: wait the user update", e);
@@ -1400,7 +1449,8 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
         const int64_t segs = rg_mf_owner_segments(cfg->global_cols, cfg->n_neg);
         if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world || !cfg->item_grad ||
             cfg->cols != cfg->global_cols || cfg->col_offset != 0 || segs <= 0 || !cfg->owner_rec[0] || !cfg->owner_rec[1] ||
-            !cfg->owner_seg[0] || !cfg->owner_seg[1] || !cfg->owner_scores[0] || !cfg->owner_scores[1]) {
+            !cfg->owner_seg[0] || !cfg->owner_seg[1] || !cfg->owner_scores[0] || !cfg->owner_scores[1] ||
+            cfg->shard_items < 0 || (cfg->shard_items > 0 && cfg->shard_items * cfg->world < cfg->tables[0].num_items)) {
             rg::set_error("rg_mf_stepper_create: inconsistent owner-sharded data-parallel configuration");
             return nullptr;
         }

@@ -288,14 +288,15 @@ def _worker_own_rccl(rank, world, port, loss, out):
         dist.destroy_process_group()
 
 
-def _worker_own_host(rank, world, port, loss, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker_own_host(rank, world, port, loss, out, item_shard="0"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RG_OWNER_ITEM_SHARD=item_shard)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from recommendation_gans_amd.comm import HostComm
         comm = HostComm("cuda:0")
         e, inputs = _own_engine(rank, world, loss, comm=comm)
+        assert e.shard_items == (-(-e.I // world) if item_shard == "1" else 0)
 
         def step(cur, nxt):
             lv = e.train_step_in(cur, nxt)
@@ -363,16 +364,19 @@ def test_owner_native_rccl_world1():
     _own_check(out, 1, "bpr")
 
 
-@pytest.mark.parametrize("loss", ["bpr", "adaptive_hinge"])
-def test_owner_native_concurrent_step_world2(loss):
+@pytest.mark.parametrize("loss,item_shard", [("bpr", "0"), ("adaptive_hinge", "0"), ("bpr", "1"),
+                                              ("adaptive_hinge", "1")])
+def test_owner_native_concurrent_step_world2(loss, item_shard):
     """The whole native owner step (rg_mf_stepper_train, train_owner's stream placement: the score
     all-reduce and the item-gradient all-reduce on the main stream, where RCCL takes them; the
     user update and the next owner prepare on the communicator stream beside the item exchange
     and update) at world 2 -- two processes on cuda:0, each all-reduce host-staged through gloo
     on the main stream in stream order (comm.HostComm: D2H, host callback, H2D on the caller's
     stream, as RCCL would be enqueued; RCCL refuses two ranks on one GPU) -- == one process at
-    batch 2B."""
+    batch 2B.  item_shard "1" (RG_OWNER_ITEM_SHARD): the item update sharded -- reduce-scatter of the
+    rank-major item gradient, each rank's half of the items' Adam, all-gather of the item rows and
+    biases (host-staged as all-reduces of the chunks) -- with the same result."""
     out = mp.Manager().dict()
-    mp.spawn(_worker_own_host, args=(2, _free_port(), loss, out), nprocs=2, join=True)
+    mp.spawn(_worker_own_host, args=(2, _free_port(), loss, out, item_shard), nprocs=2, join=True)
     _own_check(out, 2, loss)
 
