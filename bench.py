@@ -264,6 +264,11 @@ def bench_ncf(args):
     torch.cuda.synchronize()
     every = max(1, args.events_every)
     evs = []
+    ahead = None
+    if args.host_ahead > 0:      # diagnostic (see --host-ahead): GPU-side step time alone
+        torch.cuda._sleep(int(args.host_ahead * 2.1e6))
+        ahead = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ahead[0].record()
     t0 = time.perf_counter()
     for s in range(args.steps):
         g = (args.warmup + s) % nplan
@@ -276,6 +281,9 @@ def bench_ncf(args):
             eng.kernel_events = None
         g2 = (args.warmup + s + 1) % nplan
         eng.train_step(u, i, plan=plans[g], next_step=(*cols(g2), plans[g2]))
+    if ahead is not None:
+        ahead[1].record()
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -308,7 +316,12 @@ def bench_ncf(args):
                                                                     else "ncf_pairs_kernel") + ")", "achieved": ach,
                         "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / HIDDEN_FP32_MFMA_TFLOPS,
                         "traffic": None, "algorithmic_flops_per_launch": flops, "avg_launch_us": ms * 1e3},
-           "final_loss": float(eng.loss_out[0])}
+           "final_loss": float(eng.loss_out[0]), "host_enqueue_us_per_step": t_enq / args.steps * 1e6}
+    if ahead is not None:
+        out["gpu_ahead_us_per_step"] = ahead[0].elapsed_time(ahead[1]) * 1e3 / args.steps
+        out["ms_per_step"] = out["gpu_ahead_us_per_step"] * 1e-3
+        out["value"] = B * world / (out["gpu_ahead_us_per_step"] * 1e-6)
+        out["timing"] = "GPU events after a host-ahead spin (diagnostic)"
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = ncf_cpu_baseline([p.clone() for p in params], names, data, B, n, neumf,
                                                args.cpu_baseline_seconds)
@@ -936,6 +949,7 @@ def report_emulated(args, emu, eng, evs, el, U, I, d, B, n, t_enq, ahead=None):
            # host time to enqueue a step (Python + the stepper's HIP calls): close to the step
            # time means the GPU waits for the host
            "host_enqueue_us_per_step": t_enq / args.steps * 1e6,
+           "mt_mode": eng.mt_mode,
            "final_loss": float(eng.loss_out[0])}
     if ahead is not None:
         # --host-ahead: every step enqueued before the GPU reached it (the wall time above

@@ -540,6 +540,12 @@ void *rg_comm_create_local(int32_t world, int32_t rank, int32_t device);
 typedef int (*rg_host_allreduce_fn)(void *ctx, float *host_buf, int64_t n);
 void *rg_comm_create_host(int32_t world, int32_t rank, int32_t device, int64_t max_floats,
                           rg_host_allreduce_fn fn, void *ctx);
+/* Host-staged stand-in only: the owner step's MT word all-gather (a rank's slice of each step's
+ * words to every rank, bit for bit), called synchronously on the stepper's host thread:
+ * fn(ctx, send, n, recv) must gather n words from every rank into recv[world * n] in rank order
+ * and return 0 (tests: a gloo all_gather on a group of its own). */
+typedef int (*rg_host_gather_fn)(void *ctx, const uint32_t *send, int64_t n, uint32_t *recv);
+int rg_comm_set_host_gather(void *comm, rg_host_gather_fn fn, void *ctx);
 int rg_comm_destroy(void *comm);
 /* What the native communicator reports: ncclCommCount / ncclCommUserRank of an RCCL
  * communicator (is_rccl = 1), or the configured world / rank of a local / host-staged stand-in
@@ -621,6 +627,10 @@ typedef struct rg_mf_step_in {
 } rg_mf_step_in_t;
 
 void *rg_mf_stepper_create(const rg_mf_stepper_config_t *config);
+/* How the stepper produces its MT words: 0 one walk of every word, 1 jump-ahead head + parallel
+ * tail segments of the whole global draw (data-parallel steps), 2 this rank's slice of every
+ * step's draw + a jump, the slices all-gathered (the owner step over a communicator). */
+int32_t rg_mf_stepper_mt_mode(void *stepper);
 int rg_mf_stepper_destroy(void *stepper);
 /* One fused training step on `stream`; `next` (optional) = the following step's
  * inputs, whose words and pairs are produced ahead on the side stream.  Optional

@@ -30,6 +30,8 @@ c_u32p = ctypes.POINTER(ctypes.c_uint32)
 c_u64p = ctypes.POINTER(ctypes.c_uint64)
 # rg_host_allreduce_fn (include/rg_hip.h): int (*)(void *ctx, float *host_buf, int64_t n)
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+# rg_host_gather_fn: int (*)(void *ctx, const uint32_t *send, int64_t n, uint32_t *recv)
+HOST_GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 
 
 class MFTables(ctypes.Structure):
@@ -255,6 +257,7 @@ SIGNATURES = [
     ("rg_comm_create_local", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("rg_comm_create_host", ctypes.c_void_p, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                               ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_comm_set_host_gather", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("rg_comm_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                     ctypes.POINTER(ctypes.c_int32)]),
@@ -354,6 +357,7 @@ SIGNATURES = [
     ("rg_mf_scores", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_int64, ctypes.c_void_p]),
+    ("rg_mf_stepper_mt_mode", ctypes.c_int32, [ctypes.c_void_p]),
     ("rg_mf_stepper_create", ctypes.c_void_p, [ctypes.POINTER(MFStepperConfig)]),
     ("rg_mf_stepper_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("rg_mf_stepper_train", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MFStepIn),

@@ -96,7 +96,8 @@ class HostComm(RcclComm):
     (rg_comm_create_host), so the step's own placement -- the score exchange fenced on the main
     stream, the item gradient's exchange on the side stream beside the user update -- runs as in
     production.  A reduce-scatter is staged as an all-reduce of every chunk (each rank then reads
-    its own), an all-gather as an all-reduce with every other rank's chunk zeroed first.
+    its own), an all-gather as an all-reduce with every other rank's chunk zeroed first; the owner
+    step's MT word all-gather goes through a gather callback on a gloo group of its own.
 
     The callback takes the GIL on the runtime's callback thread: while the step's work is in
     flight, wait with ``sync()`` (a ctypes call, which releases the GIL), not with a torch call
@@ -123,6 +124,24 @@ class HostComm(RcclComm):
                                                    ctypes.cast(self._cb, ctypes.c_void_p), None)
         if not self.handle:
             raise RuntimeError("rg_comm_create_host: " + self.lib.rg_last_error().decode())
+        # the owner step's MT word all-gather (rank slices of the global draw's words, bit for bit):
+        # a gloo group of its own, called synchronously from the stepper's host thread, so it
+        # never interleaves with the step's all-reduces on the callback thread
+        ranks = list(range(self.world))
+        self.words_group = dist.new_group(ranks, backend="gloo")
+
+        def _gather(ctx, send, n, recv):
+            try:
+                src = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_int32 * n).from_address(send)))
+                dst = np.ctypeslib.as_array((ctypes.c_int32 * (n * self.world)).from_address(recv))
+                outs = [torch.from_numpy(dst[r * n:(r + 1) * n]) for r in range(self.world)]
+                dist.all_gather(outs, src, group=self.words_group)
+                return 0
+            except Exception:
+                return 1
+        self._gcb = _lib.HOST_GATHER_FN(_gather)
+        check(self.lib.rg_comm_set_host_gather(self.handle, ctypes.cast(self._gcb, ctypes.c_void_p), None),
+              "rg_comm_set_host_gather")
         self._hip = ctypes.CDLL("libamdhip64.so.7")
 
     def sync(self):

@@ -24,6 +24,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "rg_common.h"
 
@@ -49,6 +50,13 @@ struct Comm {
         int64_t n;
     };
     std::atomic<int> host_error{0};
+    // the owner step's MT word all-gather (comm_words_allgather): its own RCCL communicator (split
+    // from `comm`), or the host gather callback; the local stand-in's hash seed counter
+    ncclComm_t comm_words = nullptr;
+    rg_host_gather_fn gather_fn = nullptr;
+    void *gather_ctx = nullptr;
+    std::vector<uint32_t> gsend, grecv;
+    uint32_t words_calls = 0;
     // RCCL deadline (bounded failure of a multi-process run): a watchdog thread checks the
     // communicator's asynchronous error and the completion of the last tracked collective; past
     // the deadline it aborts the communicator (which releases the GPU's waiting kernels) and
@@ -96,6 +104,9 @@ static void watchdog_loop(Comm *c) {
         ncclResult_t ae = ncclSuccess;
         if (c->comm && ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
             comm_die(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+        if (c->comm_words && ncclCommGetAsyncError(c->comm_words, &ae) == ncclSuccess && ae != ncclSuccess &&
+            ae != ncclInProgress)
+            comm_die(c, std::string("RCCL asynchronous error (word all-gather): ") + ncclGetErrorString(ae));
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->tracking) continue;
         if (hipEventQuery(c->ev_track) == hipSuccess) { c->tracking = false; continue; }
@@ -262,7 +273,81 @@ int comm_allgather(void *h, hipStream_t stream, int n, float *const *bufs, const
     return nccl_after(c, stream, r2, "ncclAllGather (group)");
 }
 
+int comm_kind(void *h) {
+    const Comm *c = static_cast<const Comm *>(h);
+    return !c ? -1 : c->local ? 2 : c->host_fn ? 1 : 0;
+}
+
+// wait out ncclInProgress of a call on communicator `cm` within the deadline
+static ncclResult_t nccl_settle(Comm *c, ncclComm_t cm, ncclResult_t r, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        if (ncclCommGetAsyncError(cm, &r) != ncclSuccess) break;
+        if (r != ncclInProgress) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+            comm_die(c, std::string(what) + " still in progress after the deadline");
+        std::this_thread::yield();
+    }
+    return r;
+}
+
+int comm_words_prepare(void *h) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c) return fail_arg("comm_words_prepare: null communicator");
+    if (c->local || c->host_fn || c->comm_words) return RG_OK;
+    // every rank splits at stepper creation (the same point of each rank's call sequence)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommSplit(c->comm, 0, c->rank, &c->comm_words, &cfg);
+    if (r == ncclInProgress && c->comm_words) r = nccl_settle(c, c->comm_words, r, "ncclCommSplit");
+    if (r != ncclSuccess) {
+        c->comm_words = nullptr;
+        return nccl_fail("ncclCommSplit (word all-gather communicator)", r);
+    }
+    return RG_OK;
+}
+
+int comm_words_allgather(void *h, hipStream_t stream, uint32_t *words, int64_t units, int64_t W, int64_t L) {
+    Comm *c = static_cast<Comm *>(h);
+    if (!c || !words || units < 0 || L <= 0 || W != L * c->world) return fail_arg("comm_words_allgather: bad argument");
+    if (c->local) return mt_fill_other_slices(stream, words, units, W, L, c->rank, c->world, 0x5bd1e995u * ++c->words_calls);
+    if (c->host_fn) {
+        if (!c->gather_fn) return fail_arg("comm_words_allgather: the host communicator has no gather callback");
+        c->gsend.resize((size_t)L);
+        c->grecv.resize((size_t)W);
+        for (int64_t k = 0; k < units; ++k) {
+            uint32_t *u = words + k * W;
+            hipError_t e = hipMemcpyAsync(c->gsend.data(), u + c->rank * L, (size_t)L * 4, hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return hip_fail("comm_words_allgather (host)", e);
+            if (c->gather_fn(c->gather_ctx, c->gsend.data(), L, c->grecv.data()) != 0)
+                return fail_arg("comm_words_allgather: the host gather callback failed");
+            e = hipMemcpyAsync(u, c->grecv.data(), (size_t)W * 4, hipMemcpyHostToDevice, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return hip_fail("comm_words_allgather (host)", e);
+        }
+        return RG_OK;
+    }
+    int rc = comm_words_prepare(h);
+    if (rc) return rc;
+    ncclResult_t r = ncclGroupStart();
+    for (int64_t k = 0; k < units && r == ncclSuccess; ++k)
+        r = ncclAllGather(words + k * W + c->rank * L, words + k * W, (size_t)L, ncclUint32, c->comm_words, stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess && r != ncclInProgress) return nccl_fail("ncclAllGather (words)", r);
+    r = nccl_settle(c, c->comm_words, r2, "ncclAllGather (words)");
+    return r == ncclSuccess ? RG_OK : nccl_fail("ncclAllGather (words, group)", r);
+}
+
 }  // namespace rg
+
+extern "C" int rg_comm_set_host_gather(void *comm, rg_host_gather_fn fn, void *ctx) {
+    rg::Comm *c = static_cast<rg::Comm *>(comm);
+    if (!c || !c->host_fn) return rg::fail_arg("rg_comm_set_host_gather: not a host-staged communicator");
+    c->gather_fn = fn;
+    c->gather_ctx = ctx;
+    return RG_OK;
+}
 
 extern "C" int rg_comm_reduce_scatter_f32(void *comm, void *stream, float *buf, int64_t chunk) {
     return rg::comm_reduce_scatter(comm, (hipStream_t)stream, buf, chunk);
@@ -397,6 +482,7 @@ extern "C" int rg_comm_destroy(void *h) {
     if (c->ev_track) hipEventDestroy(c->ev_track);
     if (c->scratch) hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->comm_words) ncclCommDestroy(c->comm_words);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     if (c->ev_out) hipEventDestroy(c->ev_out);

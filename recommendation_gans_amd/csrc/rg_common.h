@@ -38,6 +38,15 @@ int comm_allgather(void *comm, hipStream_t stream, int n, float *const *bufs, co
 hipStream_t comm_stream(void *comm);   // the communicator's own stream
 // the all-reduce enqueued on `stream` itself (no cross-stream events; host mode: begin + end)
 int comm_allreduce_on(void *comm, hipStream_t stream, float *buf, int64_t n);
+// the owner step's MT word exchange: `units` units of W = world * L words each, rank r having
+// written words [k W + r L, k W + (r + 1) L) of unit k; afterwards every rank holds every unit's
+// W words.  On `stream` (the generator stream), over a communicator of its own (RCCL: split off
+// the step's, so it never orders against the step's collectives); host mode: synchronous, through
+// the gather callback; local mode: the other slices hashed (a stand-in of the same shape)
+int comm_words_prepare(void *comm);
+int comm_words_allgather(void *comm, hipStream_t stream, uint32_t *words, int64_t units, int64_t W, int64_t L);
+// 0: RCCL, 1: host-staged, 2: local copies
+int comm_kind(void *comm);
 
 // ---------------------------------------------------------------- MT jump-ahead
 // One step's words as a sequential head + parallel tail segments (rg_mtjump.cpp,
@@ -56,11 +65,19 @@ struct MtJumpPlan {
     uint32_t *raw = nullptr;       // [(segs.n + 1) * 624] XOR accumulators
 };
 // nullptr if `words` is too short for the jump path (then use rg_mt_generate)
-MtJumpPlan *mt_jump_plan_create(int64_t words);
+// tail < 0: segments of ~20k words; tail = 0: no segments, only the state `words` ahead (a jump)
+MtJumpPlan *mt_jump_plan_create(int64_t words, int tail = -1);
 void mt_jump_plan_destroy(MtJumpPlan *plan);
-// head -> jump -> tail on `stream`: out[0 .. words) and the next window-form state
+// head -> jump -> tail on `stream`: out[0 .. words) and the next window-form state.  walk > 0
+// (a plan without tail segments): the head walks exactly `walk` >= plan.head words into out
+// (bounded: nothing past out[walk - 1]) -- one rank's slice of a step's stream, the state then
+// jumping `plan.words` ahead of the slice's start
 int mt_produce_jump(hipStream_t stream, const MtJumpPlan &plan, uint32_t *state, uint32_t *out,
-                    uint32_t *state_before);
+                    uint32_t *state_before, int64_t walk = 0);
+// the local (one-process) stand-in of the owner step's word all-gather: the slices of the other
+// ranks, of each of `units` units of `W` words ([R][L] per unit), filled with hashed words
+int mt_fill_other_slices(hipStream_t stream, uint32_t *words, int64_t units, int64_t W, int64_t L, int rank,
+                         int world, uint32_t seed);
 
 // ---------------------------------------------------------------- prepared pairs
 // rg_mf_prepare's output: one record per batch column s (processing order) of
@@ -412,6 +429,31 @@ struct BackLayout<RowLayout<16, 4, true>> {
 template <>
 struct BackLayout<RowLayout<32, 4, true>> {
     using type = RowLayoutV<RG_BACK_V128, 128 / (4 * RG_BACK_V128)>;
+};
+#endif
+
+// The split step's pair pass on its own row layout (RG_PAIR_V64 / RG_PAIR_V128 lanes per row, 0:
+// the dispatch layout): timing experiments of fewer lanes per row in the latency-bound gather
+#ifndef RG_PAIR_V64
+#define RG_PAIR_V64 0
+#endif
+#ifndef RG_PAIR_V128
+#define RG_PAIR_V128 0
+#endif
+template <class L>
+struct PairLayout {
+    using type = L;
+};
+#if RG_PAIR_V64
+template <>
+struct PairLayout<RowLayout<16, 4, true>> {
+    using type = RowLayoutV<RG_PAIR_V64, 64 / (4 * RG_PAIR_V64)>;
+};
+#endif
+#if RG_PAIR_V128
+template <>
+struct PairLayout<RowLayout<32, 4, true>> {
+    using type = RowLayoutV<RG_PAIR_V128, 128 / (4 * RG_PAIR_V128)>;
 };
 #endif
 

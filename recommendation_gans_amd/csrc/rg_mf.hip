@@ -246,7 +246,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
     constexpr bool kBackward = (PHASE == kFused) || (PHASE == kAdaptBwd);
     constexpr bool kScoresFromBuf = (PHASE == kAdaptBwd) || (PHASE == kAdaptLoss);
     __shared__ float red[2][kPairBlock / kWave];
-    __shared__ float lrow[kLdsFloats];
+    __shared__ float lrow[UPB * (LPU * EPL + 1)];   // a planned partial row (D <= LPU * EPL) per unit
     __shared__ int lslot[UPB];
     __shared__ float ldz[kBackward ? UPB * NP : 1];
     const int lane = threadIdx.x & (kWave - 1);
@@ -328,7 +328,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
         float ur[NP][EPL], ir[NP][EPL], ub[NP], ib[NP];
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-            if (SC1) {   // rows written by this launch's hot workgroups (mf_pipe_kernel)
+            if constexpr (SC1) {   // rows written by this launch's hot workgroups (mf_pipe_kernel)
                 L::load_sc1(ur[q], a.user_w, uid[q], D, sub);
                 L::load_sc1(ir[q], a.item_w, iid[q], D, sub);
                 ub[q] = L::load1_sc1(a.user_b + uid[q]);
@@ -460,12 +460,12 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                     float o[EPL];
                     if (t & 1) {
                         const int64_t row = a.num_users + iid[q];
-                        if (SC1) L::load_sc1(o, a.user_w, uid[q], D, sub);
+                        if constexpr (SC1) L::load_sc1(o, a.user_w, uid[q], D, sub);
                         else L::load(o, a.user_w, uid[q], D, sub);
                         overflow_add<L>(a.hot_grad, row, D, sub, dz[q], o);
                         if (sub == 0) fix_add(a.hot_bias_grad + row, dz[q]);
                     } else {
-                        if (SC1) L::load_sc1(o, a.item_w, iid[q], D, sub);
+                        if constexpr (SC1) L::load_sc1(o, a.item_w, iid[q], D, sub);
                         else L::load(o, a.item_w, iid[q], D, sub);
                         overflow_add<L>(a.hot_grad, uid[q], D, sub, dz[q], o);
                         if (sub == 0) fix_add(a.hot_bias_grad + uid[q], dz[q]);
@@ -1990,21 +1990,22 @@ struct PartialsLenF {
     int64_t cols;
     int64_t *nb;
     template <class L>
-    int operator()() { *nb = pairs_blocks<L>(cols); return 0; }
+    int operator()() { *nb = pairs_blocks<typename PairLayout<L>::type>(cols); return 0; }
 };
 
 struct UnitsPerBlockF {
     int64_t *upb;
     template <class L>
-    int operator()() { *upb = kPairBlock / L::LPU; return 0; }
+    int operator()() { *upb = kPairBlock / PairLayout<L>::type::LPU; return 0; }
 };
 
 struct PairsLaunchF {
     PairsArgs *a;
     hipStream_t s;
     bool adaptive, backward;
-    template <class L>
+    template <class L0>
     int operator()() {
+        using L = typename PairLayout<L0>::type;
         if (a->n_neg <= 5) return run<L, 5>();
         return run<L, kNMax>();
     }

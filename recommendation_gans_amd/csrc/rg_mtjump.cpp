@@ -167,10 +167,11 @@ void window_from_stream(const uint32_t *x, int64_t D, uint32_t *mt) {
 
 }  // namespace mtj
 
-MtJumpPlan *mt_jump_plan_create(int64_t words) {
+MtJumpPlan *mt_jump_plan_create(int64_t words, int tail) {
     using namespace mtj;
     const int64_t head = kDeg + kN - 1;          // windows S_i, i < 19937, need x[0 .. 20560)
-    if (words < 2 * head || mtj::charpoly().empty()) return nullptr;
+    // a jump alone (tail 0) needs only its window stream; tail segments at least one head apart
+    if (words < (tail == 0 ? (int64_t)kN + 1 : 2 * head) || mtj::charpoly().empty()) return nullptr;
     // tail segments of ~20k words: each walks about as long as the head does
 #if RG_AB
     const char *env = getenv("RG_MT_TAIL");
@@ -179,11 +180,12 @@ MtJumpPlan *mt_jump_plan_create(int64_t words) {
 #endif
     int n = env ? atoi(env) : (int)((words - head + 19999) / 20000);
     n = n < 1 ? 1 : (n > kMtMaxTail ? kMtMaxTail : n);
+    if (tail >= 0) n = tail > kMtMaxTail ? kMtMaxTail : tail;   // 0: the jump alone
     MtJumpPlan *p = new MtJumpPlan();
     p->words = words;
     p->head = head;
     p->segs.n = n;
-    const int64_t tail = words - head, len = (tail + n - 1) / n;
+    const int64_t rest = words - head, len = n > 0 ? (rest + n - 1) / n : 0;
     std::vector<int32_t> terms, off{0};
     for (int j = 0; j <= n; ++j) {
         int64_t start = words;

@@ -37,6 +37,7 @@ __global__ __launch_bounds__(kGenThreads) void mt_generate_kernel(uint32_t *__re
 // segments (and the next step) start; the tail segments are walked concurrently.
 
 // head: state_before copy, zero the jump accumulators, walk H words
+template <bool BOUNDED>
 __global__ __launch_bounds__(kGenThreads) void mt_head_kernel(const uint32_t *__restrict__ state,
                                                               uint32_t *__restrict__ out, int64_t H,
                                                               uint32_t *__restrict__ state_before,
@@ -49,7 +50,27 @@ __global__ __launch_bounds__(kGenThreads) void mt_head_kernel(const uint32_t *__
         for (int i = p; i <= kMtN; i += kGenThreads) state_before[i] = state[i];
     for (int i = p; i < nraw; i += kGenThreads) raw[i] = 0U;
     __syncthreads();
-    mt_walk<false>(X, p, pos0, H, out);
+    mt_walk<BOUNDED>(X, p, pos0, H, out);
+}
+
+// the other ranks' slices of `units` units ([R][L] words each), hashed (local stand-in of the
+// owner step's word all-gather: the words are random, the draws they make are not the stream's)
+__global__ __launch_bounds__(256) void mt_fill_slices_kernel(uint32_t *__restrict__ words, int64_t units, int64_t W,
+                                                             int64_t L, int rank, uint32_t seed) {
+    const int64_t n = units * W;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        if ((i % W) / L == rank) continue;
+        uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
+        h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+        words[i] = h;
+    }
+}
+
+int mt_fill_other_slices(hipStream_t stream, uint32_t *words, int64_t units, int64_t W, int64_t L, int rank,
+                         int world, uint32_t seed) {
+    if (!words || units < 0 || L <= 0 || W != L * world) return fail_arg("mt_fill_other_slices: bad geometry");
+    hipLaunchKernelGGL(mt_fill_slices_kernel, dim3(1024), dim3(256), 0, stream, words, units, W, L, rank, seed);
+    return check_launch("mt_fill_other_slices");
 }
 
 // raw[j][k] ^= XOR over this block's share of jump j's terms i of x[i + k].
@@ -123,10 +144,16 @@ __global__ __launch_bounds__(kGenThreads) void mt_tail_kernel(const uint32_t *__
 }
 
 int mt_produce_jump(hipStream_t stream, const MtJumpPlan &plan, uint32_t *state, uint32_t *out,
-                    uint32_t *state_before) {
+                    uint32_t *state_before, int64_t walk) {
     const int nslots = plan.segs.n + 1;
-    hipLaunchKernelGGL(mt_head_kernel, dim3(1), dim3(kGenThreads), 0, stream, state, out, plan.head,
-                       state_before, plan.raw, nslots * kMtN);
+    if (walk > 0) {
+        if (plan.segs.n != 0 || walk < plan.head) return fail_arg("mt_produce_jump: a slice walk needs a jump-only plan");
+        hipLaunchKernelGGL(mt_head_kernel<true>, dim3(1), dim3(kGenThreads), 0, stream, state, out, walk, state_before,
+                           plan.raw, nslots * kMtN);
+    } else {
+        hipLaunchKernelGGL(mt_head_kernel<false>, dim3(1), dim3(kGenThreads), 0, stream, state, out, plan.head,
+                           state_before, plan.raw, nslots * kMtN);
+    }
     const int nx = (int)plan.head;
     const size_t lds = (size_t)nx * sizeof(uint32_t);
     static const bool attr = [&] {

@@ -113,6 +113,17 @@ struct Stepper {
     int32_t cp_pos = 624;
     bool win_at[kSlots] = {false, false, false};   // form / position at each slot's start
     int32_t pos_at[kSlots] = {624, 624, 624};
+    // owner step over a communicator (dp_mode 2, world > 1; RG_OWNER_MT_SLICE=0: off): each rank
+    // walks only ITS slice of every unit's words (L = W / world words at offset rank * L; the device
+    // state then jumps W ahead of the slice's start), the slices are all-gathered on the generator
+    // stream (rg::comm_words_allgather), and gstate -- the global stream's state at the start of the
+    // next slot to produce, what the CPython state exports read -- is advanced by a jump of G * W
+    // per slot.  One rank's MT work per unit: an L-word walk and two one-window jumps, instead of
+    // the whole global draw's W words
+    bool slice = false;
+    int64_t L = 0;
+    rg::MtJumpPlan *slice_plan = nullptr, *gjump = nullptr, *rjump = nullptr;
+    uint32_t *gstate = nullptr, *jscratch = nullptr;
     // owner-sharded step (dp_mode 2) between its parts
     rg_mf_step_in_t own_in{};
     int64_t own_unit = -1;
@@ -285,12 +296,31 @@ void end_production(Stepper &st, hipStream_t p, int slot) {
     ++st.gen_slots;
 }
 
+// slice mode: this rank's device state at its slice of the unit gstate starts (a jump of rank * L)
+int slice_reset(Stepper &st) {
+    hipError_t e = hipMemcpyAsync(st.cfg.mt_state, st.gstate, 625 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st.gen);
+    if (e != hipSuccess) return hip_fail("stepper: slice state", e);
+    if (st.rjump) return rg::mt_produce_jump(st.gen, *st.rjump, st.cfg.mt_state, st.jscratch, nullptr, 0);
+    return RG_OK;
+}
+
 // generate the next ring slot (G units) on the gen stream
 int generate_one(Stepper &st) {
     const int slot = (int)(st.gen_slots % kSlots);
     int rc = begin_production(st, st.gen, slot);
     if (rc) return rc;
-    if (st.jump) {
+    if (st.slice) {
+        hipError_t e = hipMemcpyAsync(st.start_state[slot], st.gstate, 625 * sizeof(uint32_t),
+                                      hipMemcpyDeviceToDevice, st.gen);
+        if (e != hipSuccess) return hip_fail("stepper: slot start state", e);
+        const int64_t off = (int64_t)st.cfg.rank * st.L;
+        for (int64_t k = 0; k < st.G && rc == RG_OK; ++k)
+            rc = rg::mt_produce_jump(st.gen, *st.slice_plan, st.cfg.mt_state, st.words[slot] + k * st.W + off, nullptr,
+                                     st.L);
+        if (rc == RG_OK) rc = rg::comm_words_allgather(st.cfg.comm, st.gen, st.words[slot], st.G, st.W, st.L);
+        if (rc == RG_OK) rc = rg::mt_produce_jump(st.gen, *st.gjump, st.gstate, st.jscratch, nullptr, 0);
+        st.window_form = true;
+    } else if (st.jump) {
         rc = rg::mt_produce_jump(st.gen, *st.jump, st.cfg.mt_state, st.words[slot], st.start_state[slot]);
         st.window_form = true;
     } else {
@@ -1434,6 +1464,11 @@ void destroy(Stepper *st) {
     if (st->gen) hipStreamDestroy(st->gen);
     if (st->prep) hipStreamDestroy(st->prep);
     rg::mt_jump_plan_destroy(st->jump);
+    rg::mt_jump_plan_destroy(st->slice_plan);
+    rg::mt_jump_plan_destroy(st->gjump);
+    rg::mt_jump_plan_destroy(st->rjump);
+    if (st->gstate) hipFree(st->gstate);
+    if (st->jscratch) hipFree(st->jscratch);
     delete st;
 }
 
@@ -1614,8 +1649,44 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     }
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
-    if (env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1)) st->jump = rg::mt_jump_plan_create(st->G * st->W);
+    if (cfg->dp_mode == 2 && cfg->comm && cfg->world > 1 && st->W % cfg->world == 0 && !st->inline_gen &&
+        env_flag("RG_OWNER_MT_SLICE", true)) {
+        // each rank walks its slice of the global draw (see Stepper::slice); falls back to the
+        // jump-ahead walk of the whole draw when a slice is shorter than a jump's stream window
+        st->L = st->W / cfg->world;
+        st->slice_plan = rg::mt_jump_plan_create(st->W, 0);
+        st->gjump = rg::mt_jump_plan_create(st->G * st->W, 0);
+        if (cfg->rank > 0) st->rjump = rg::mt_jump_plan_create((int64_t)cfg->rank * st->L, 0);
+        st->slice = st->slice_plan && st->gjump && (cfg->rank == 0 || st->rjump) && st->L >= st->slice_plan->head;
+        if (st->slice) {
+            const size_t scratch = (size_t)(st->slice_plan->head + 2 * 227 + RG_MT_PAD);
+            e = hipMalloc(&st->gstate, 625 * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMalloc(&st->jscratch, scratch * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemcpy(st->gstate, cfg->mt_state, 625 * sizeof(uint32_t), hipMemcpyDeviceToDevice);
+            int rc = e == hipSuccess ? rg::comm_words_prepare(cfg->comm) : RG_E_LAUNCH;
+            if (e != hipSuccess) hip_fail("rg_mf_stepper_create: slice state", e);
+            if (rc == RG_OK) rc = slice_reset(*st);
+            if (rc == RG_OK && (e = hipStreamSynchronize(st->gen)) != hipSuccess) rc = hip_fail("rg_mf_stepper_create", e);
+            if (rc != RG_OK) {
+                destroy(st);
+                return nullptr;
+            }
+        } else {
+            rg::mt_jump_plan_destroy(st->slice_plan);
+            rg::mt_jump_plan_destroy(st->gjump);
+            rg::mt_jump_plan_destroy(st->rjump);
+            st->slice_plan = st->gjump = st->rjump = nullptr;
+        }
+    }
+    if (!st->slice && env_flag("RG_MT_JUMP", cfg->dp_mode != 0 && cfg->world > 1))
+        st->jump = rg::mt_jump_plan_create(st->G * st->W);
     return st;
+}
+
+extern "C" int32_t rg_mf_stepper_mt_mode(void *h) {
+    const Stepper *st = static_cast<const Stepper *>(h);
+    if (!st) return -1;
+    return st->slice ? 2 : st->jump ? 1 : 0;
 }
 
 extern "C" int rg_mf_stepper_destroy(void *h) {
@@ -1872,7 +1943,7 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
         const int64_t slot_rel = rel / st->G, inside = rel % st->G;
         const bool ahead = st->gen_slots > slot_rel;
         const int slot = (int)(slot_rel % kSlots);
-        const uint32_t *src = ahead ? st->start_state[slot] : st->cfg.mt_state;
+        const uint32_t *src = ahead ? st->start_state[slot] : st->slice ? st->gstate : st->cfg.mt_state;
         const bool window = ahead ? st->win_at[slot] : st->window_form;
         const int32_t pos = ahead ? st->pos_at[slot] : st->cp_pos;
         uint32_t dev[625];
@@ -1900,8 +1971,13 @@ extern "C" int rg_mf_stepper_sync_mt(void *h, uint32_t *host_state, int32_t dire
     st->prepared = false;
     st->window_form = false;
     st->cp_pos = (int32_t)host_state[624];
-    e = hipMemcpy(st->cfg.mt_state, host_state, 625 * sizeof(uint32_t), hipMemcpyHostToDevice);
+    e = hipMemcpy(st->slice ? st->gstate : st->cfg.mt_state, host_state, 625 * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail("stepper: copy MT state", e);
+    if (st->slice) {
+        const int rc = slice_reset(*st);
+        if (rc) return rc;
+        if ((e = hipStreamSynchronize(st->gen)) != hipSuccess) return hip_fail("stepper: slice state", e);
+    }
     return RG_OK;
 }
 

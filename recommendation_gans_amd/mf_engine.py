@@ -522,9 +522,15 @@ class MFEngine:
         return self.lib.rg_mf_stepper_pipelined(self._stepper) == 1
 
     @property
+    def mt_mode(self):
+        """0: one MT walk of every word; 1: jump-ahead segments of the global draw; 2: this rank's
+        slice of each step's draw, all-gathered (the owner step over a communicator)."""
+        return int(self.lib.rg_mf_stepper_mt_mode(self._stepper))
+
+    @property
     def pipeline_kind(self):
         """0: the split step; 1: the single-launch pipelined step (A/B build); 2: the two-launch
-        pipelined step (rg_mf_pipe2_hot / rg_mf_pipe2_cold, the single-GPU default)."""
+        pipelined step (rg_mf_pipe2_hot / rg_mf_pipe2_cold, opt-in: RG_PIPE2=1)."""
         return int(self.lib.rg_mf_stepper_pipelined(self._stepper))
 
     def pipe_error(self):

@@ -380,3 +380,67 @@ def test_owner_native_concurrent_step_world2(loss, item_shard):
     mp.spawn(_worker_own_host, args=(2, _free_port(), loss, out, item_shard), nprocs=2, join=True)
     _own_check(out, 2, loss)
 
+
+
+# ------------------------------------------------------------------ owner step: MT word slices
+def _worker_own_slices(rank, world, port, loss, slice_flag, out):
+    """Rank `rank` of the owner step with a host-staged communicator at a batch where one rank's
+    slice of a step's words (2 n B) is longer than a jump's stream window, RG_OWNER_MT_SLICE as
+    given; per step the loss and the exported CPython MT state, at the end the tables."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RG_OWNER_MT_SLICE=slice_flag,
+                      RG_MT_UNITS="2")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import rng as orng
+        from recommendation_gans_amd.comm import HostComm
+        from recommendation_gans_amd.mf_engine import MFEngine
+        comm = HostComm("cuda:0")
+        U, I, d, B, n, steps = 5000, 700, 32, 4096, 5, 5
+        rs = np.random.RandomState(3)
+        torch.manual_seed(3)
+        Uw, Iw = torch.empty(U, d).normal_(0, 1.0 / d), torch.empty(I, d).normal_(0, 1.0 / d)
+        pool_u, pool_i = rs.randint(0, U, 60000), rs.randint(0, I, 60000)
+        e = MFEngine(Uw, Iw, torch.zeros(U), torch.zeros(I), pool_u, pool_i, orng.py_seed_state(3), loss=loss,
+                     optimizer="adam", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B, device="cuda:0",
+                     rank=rank, world_size=world, dp="owner", comm=comm)
+        gb = B * world
+        tu = torch.from_numpy(rs.randint(0, U, (steps + 1) * gb).astype(np.int64)).cuda()
+        ti = torch.from_numpy(np.minimum(rs.zipf(1.3, (steps + 1) * gb) - 1, I - 1).astype(np.int64)).cuda()
+        plans = e.make_plans(ti, users=tu)
+        ins = [e.step_input(tu[g * gb:(g + 1) * gb], ti[g * gb:(g + 1) * gb], gb, plans[g]) for g in range(steps + 1)]
+        losses, states = [], []
+        for s in range(steps):
+            lv = e.train_step_in(ins[s], ins[s + 1])
+            comm.sync()
+            losses.append(float(lv[0]))
+            states.append(e.mt_state())
+        comm.sync()
+        out[rank] = ([p.cpu().clone() for p in e.params()], losses, states, e.mt_mode == 2)
+        del e
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("loss", ["bpr", "pointwise"])
+def test_owner_mt_slices_match_the_full_walk(loss):
+    """The owner step's MT words by rank slices (each rank walks 2 n B of every step's 2 n R B words
+    and jumps the rest; the slices all-gathered; the exported state advanced by a jump per slot)
+    against every rank walking the whole global draw (RG_OWNER_MT_SLICE=0): per-step losses, the
+    exported CPython MT state after every step, and the tables, bit for bit, at world 2 over a
+    host-staged communicator, across several word slots (RG_MT_UNITS=2)."""
+    res = {}
+    for flag in ("1", "0"):
+        out = mp.Manager().dict()
+        mp.spawn(_worker_own_slices, args=(2, _free_port(), loss, flag, out), nprocs=2, join=True)
+        res[flag] = dict(out)
+    for r in range(2):
+        ps, ls, ss, sl = res["1"][r]
+        pf, lf, sf, fl = res["0"][r]
+        assert sl and not fl, (r, "slice mode on / off as asked")
+        assert ls == lf, (r, ls, lf)
+        for s in range(len(ss)):
+            assert (ss[s] == sf[s]).all(), (r, s, "MT state")
+        for k in range(4):
+            assert torch.equal(ps[k], pf[k]), (r, k)
