@@ -67,6 +67,9 @@ struct MtJumpPlan {
 // nullptr if `words` is too short for the jump path (then use rg_mt_generate)
 // tail < 0: segments of ~20k words; tail = 0: no segments, only the state `words` ahead (a jump)
 MtJumpPlan *mt_jump_plan_create(int64_t words, int tail = -1);
+// one rank's slices of `units` consecutive units of W words (L words at the start of each, the
+// output's unit stride W): the head + parallel segments, the state then units * W ahead
+MtJumpPlan *mt_slice_plan_create(int64_t W, int64_t L, int64_t units);
 void mt_jump_plan_destroy(MtJumpPlan *plan);
 // head -> jump -> tail on `stream`: out[0 .. words) and the next window-form state.  walk > 0
 // (a plan without tail segments): the head walks exactly `walk` >= plan.head words into out

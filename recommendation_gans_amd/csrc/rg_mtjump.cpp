@@ -167,32 +167,20 @@ void window_from_stream(const uint32_t *x, int64_t D, uint32_t *mt) {
 
 }  // namespace mtj
 
-MtJumpPlan *mt_jump_plan_create(int64_t words, int tail) {
+// a plan from explicit tail segments (start, length) past the head, and the state `words` ahead
+static MtJumpPlan *plan_from(int64_t words, const std::vector<std::pair<int64_t, int64_t>> &segs) {
     using namespace mtj;
-    const int64_t head = kDeg + kN - 1;          // windows S_i, i < 19937, need x[0 .. 20560)
-    // a jump alone (tail 0) needs only its window stream; tail segments at least one head apart
-    if (words < (tail == 0 ? (int64_t)kN + 1 : 2 * head) || mtj::charpoly().empty()) return nullptr;
-    // tail segments of ~20k words: each walks about as long as the head does
-#if RG_AB
-    const char *env = getenv("RG_MT_TAIL");
-#else
-    const char *env = nullptr;
-#endif
-    int n = env ? atoi(env) : (int)((words - head + 19999) / 20000);
-    n = n < 1 ? 1 : (n > kMtMaxTail ? kMtMaxTail : n);
-    if (tail >= 0) n = tail > kMtMaxTail ? kMtMaxTail : tail;   // 0: the jump alone
+    if ((int)segs.size() > kMtMaxTail || mtj::charpoly().empty()) return nullptr;
     MtJumpPlan *p = new MtJumpPlan();
     p->words = words;
-    p->head = head;
-    p->segs.n = n;
-    const int64_t rest = words - head, len = n > 0 ? (rest + n - 1) / n : 0;
+    p->head = kDeg + kN - 1;
+    p->segs.n = (int)segs.size();
     std::vector<int32_t> terms, off{0};
-    for (int j = 0; j <= n; ++j) {
-        int64_t start = words;
-        if (j < n) {
-            start = head + j * len;
+    for (size_t j = 0; j <= segs.size(); ++j) {
+        const int64_t start = j < segs.size() ? segs[j].first : words;
+        if (j < segs.size()) {
             p->segs.start[j] = start;
-            p->segs.len[j] = std::min<int64_t>(len, words - start);
+            p->segs.len[j] = segs[j].second;
         }
         const std::vector<int32_t> t = jump_terms(start - kN - 1);   // window at D = start - 624
         terms.insert(terms.end(), t.begin(), t.end());
@@ -204,7 +192,7 @@ MtJumpPlan *mt_jump_plan_create(int64_t words, int tail) {
     if (p->chunks < 16) p->chunks = 16;
     hipError_t e = hipMalloc(&p->terms, terms.size() * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&p->term_off, off.size() * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMalloc(&p->raw, (size_t)(n + 1) * kN * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&p->raw, (size_t)(p->segs.n + 1) * kN * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(p->terms, terms.data(), terms.size() * sizeof(int32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->term_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -213,6 +201,41 @@ MtJumpPlan *mt_jump_plan_create(int64_t words, int tail) {
         return nullptr;
     }
     return p;
+}
+
+MtJumpPlan *mt_jump_plan_create(int64_t words, int tail) {
+    using namespace mtj;
+    const int64_t head = kDeg + kN - 1;          // windows S_i, i < 19937, need x[0 .. 20560)
+    // a jump alone (tail 0) needs only its window stream; tail segments at least one head apart
+    if (words < (tail == 0 ? (int64_t)kN + 1 : 2 * head)) return nullptr;
+    // tail segments of ~20k words: each walks about as long as the head does
+#if RG_AB
+    const char *env = getenv("RG_MT_TAIL");
+#else
+    const char *env = nullptr;
+#endif
+    int n = env ? atoi(env) : (int)((words - head + 19999) / 20000);
+    n = n < 1 ? 1 : (n > kMtMaxTail ? kMtMaxTail : n);
+    if (tail >= 0) n = tail > kMtMaxTail ? kMtMaxTail : tail;   // 0: the jump alone
+    const int64_t rest = words - head, len = n > 0 ? (rest + n - 1) / n : 0;
+    std::vector<std::pair<int64_t, int64_t>> segs;
+    for (int j = 0; j < n; ++j) {
+        const int64_t start = head + j * len;
+        segs.emplace_back(start, std::min<int64_t>(len, words - start));
+    }
+    return plan_from(words, segs);
+}
+
+MtJumpPlan *mt_slice_plan_create(int64_t W, int64_t L, int64_t units) {
+    using namespace mtj;
+    const int64_t head = kDeg + kN - 1;
+    if (L < head || W < L || units < 1) return nullptr;
+    // the head walks the first slice's first `head` words; segment 0 the rest of it; segment k
+    // unit k's slice; the state ends units * W ahead (this rank's slice of the next slot's first unit)
+    std::vector<std::pair<int64_t, int64_t>> segs;
+    if (L > head) segs.emplace_back(head, L - head);
+    for (int64_t k = 1; k < units; ++k) segs.emplace_back(k * W, L);
+    return plan_from(units * W, segs);
 }
 
 void mt_jump_plan_destroy(MtJumpPlan *p) {

@@ -113,13 +113,16 @@ struct Stepper {
     int32_t cp_pos = 624;
     bool win_at[kSlots] = {false, false, false};   // form / position at each slot's start
     int32_t pos_at[kSlots] = {624, 624, 624};
-    // owner step over a communicator (dp_mode 2, world > 1; RG_OWNER_MT_SLICE=0: off): each rank
-    // walks only ITS slice of every unit's words (L = W / world words at offset rank * L; the device
-    // state then jumps W ahead of the slice's start), the slices are all-gathered on the generator
-    // stream (rg::comm_words_allgather), and gstate -- the global stream's state at the start of the
-    // next slot to produce, what the CPython state exports read -- is advanced by a jump of G * W
-    // per slot.  One rank's MT work per unit: an L-word walk and two one-window jumps, instead of
-    // the whole global draw's W words
+    // owner step over a communicator (dp_mode 2, world > 1; opt-in RG_OWNER_MT_SLICE=1 -- the
+    // emulated rank 0 of 8 measured 75.0 us per step with it, 74.6 without: the jump launches cost
+    // the same either way, and the slot's MT work already hides beside the step): each rank
+    // walks only ITS slice of every unit's words (L = W / world words at offset rank * L): a slot's
+    // G slices come from one head walk, one jump launch and G parallel segments, the device state
+    // ending G * W ahead; the slices are all-gathered on the generator stream
+    // (rg::comm_words_allgather), and gstate -- the global stream's state at the start of the next
+    // slot to produce, what the CPython state exports read -- is advanced by a jump of G * W per
+    // slot.  One rank's MT work per slot: G * L words walked G-wide and two jump launches, instead
+    // of the whole global draw's G * W words
     bool slice = false;
     int64_t L = 0;
     rg::MtJumpPlan *slice_plan = nullptr, *gjump = nullptr, *rjump = nullptr;
@@ -313,10 +316,9 @@ int generate_one(Stepper &st) {
         hipError_t e = hipMemcpyAsync(st.start_state[slot], st.gstate, 625 * sizeof(uint32_t),
                                       hipMemcpyDeviceToDevice, st.gen);
         if (e != hipSuccess) return hip_fail("stepper: slot start state", e);
-        const int64_t off = (int64_t)st.cfg.rank * st.L;
-        for (int64_t k = 0; k < st.G && rc == RG_OK; ++k)
-            rc = rg::mt_produce_jump(st.gen, *st.slice_plan, st.cfg.mt_state, st.words[slot] + k * st.W + off, nullptr,
-                                     st.L);
+        // the slot's G slices in one head + jump + parallel-segment production
+        rc = rg::mt_produce_jump(st.gen, *st.slice_plan, st.cfg.mt_state, st.words[slot] + (int64_t)st.cfg.rank * st.L,
+                                 nullptr, 0);
         if (rc == RG_OK) rc = rg::comm_words_allgather(st.cfg.comm, st.gen, st.words[slot], st.G, st.W, st.L);
         if (rc == RG_OK) rc = rg::mt_produce_jump(st.gen, *st.gjump, st.gstate, st.jscratch, nullptr, 0);
         st.window_form = true;
@@ -1650,11 +1652,12 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     // the jump-ahead walk (parallel segments) by default when every rank walks the global
     // stream of a multi-rank step: R times the words of one GPU's step
     if (cfg->dp_mode == 2 && cfg->comm && cfg->world > 1 && st->W % cfg->world == 0 && !st->inline_gen &&
-        env_flag("RG_OWNER_MT_SLICE", true)) {
+        st->G < rg::kMtMaxTail &&
+        env_flag("RG_OWNER_MT_SLICE", false)) {
         // each rank walks its slice of the global draw (see Stepper::slice); falls back to the
         // jump-ahead walk of the whole draw when a slice is shorter than a jump's stream window
         st->L = st->W / cfg->world;
-        st->slice_plan = rg::mt_jump_plan_create(st->W, 0);
+        st->slice_plan = rg::mt_slice_plan_create(st->W, st->L, st->G);
         st->gjump = rg::mt_jump_plan_create(st->G * st->W, 0);
         if (cfg->rank > 0) st->rjump = rg::mt_jump_plan_create((int64_t)cfg->rank * st->L, 0);
         st->slice = st->slice_plan && st->gjump && (cfg->rank == 0 || st->rjump) && st->L >= st->slice_plan->head;
