@@ -2380,6 +2380,9 @@ struct HotLaunchF {
 };
 }  // namespace
 
+#ifndef RG_BACK_V_NCF
+#define RG_BACK_V_NCF 1
+#endif
 namespace {
 struct BackLaunchF {
     ApplyArgs *a;
@@ -2395,9 +2398,10 @@ struct BackLaunchF {
     int operator()() {
         using LB = typename BackLayout<L>::type;
         if constexpr (!std::is_same<LB, L>::value) {
-            // the MF dense pass (single-GPU, or an owner rank's user rows) on its own row layout
-            // (RG_BACK_V64 / _V128)
-            if (!upd && !lazy && a->contrib == nullptr) return run<LB, true>();
+            // the dense pass (MF single-GPU, an owner rank's user rows, the NCF tail's embedding
+            // tables pulling their per-example gradient rows) on its own row layout (RG_BACK_V64 /
+            // _V128); element-wise arithmetic, so the same bits as the dispatch layout
+            if (!lazy && (a->contrib == nullptr || RG_BACK_V_NCF)) return run<LB, true>();
         }
         return run<L, false>();
     }
