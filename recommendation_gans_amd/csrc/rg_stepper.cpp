@@ -59,6 +59,9 @@ extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w
                           int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w);
 static int64_t g_x_paired = -1;   // timing prototype: the unit whose pair pass ran in the last launch
 #endif
+#ifndef RG_OWNER_USER_AFTER_DEFAULT
+#define RG_OWNER_USER_AFTER_DEFAULT 0
+#endif
 #ifndef RG_PIPE2_DEFAULT
 #define RG_PIPE2_DEFAULT 0
 #endif
@@ -1332,26 +1335,36 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         if (e == hipSuccess && !st.own_users) e = hipEventCreateWithFlags(&st.own_users, evf);
         if (e != hipSuccess) return hip_fail("stepper: owner events", e);
     }
-    // the user update starts after the backward (its lists), beside the item-gradient pull, the
-    // item exchange and the item update (they touch item rows; it touches user rows).  It is
-    // ENQUEUED first too: the host's launches of the pull and the exchange (a few us each) would
-    // otherwise hold it back
-    if ((rc = owner_backward(st, s, side ? st.own_grads : nullptr))) return rc;
-    if (side && (e = hipStreamWaitEvent(u, st.own_grads, 0)) != hipSuccess)
-        return hip_fail("stepper: order the user update", e);
+    // the user update (it touches user rows; the item pull, the item exchange and the item update
+    // touch item rows) runs on the communicator stream from the point RG_OWNER_USER_AFTER names:
+    // 0 the end of the backward (its lists are complete there), 1 the end of the item pull (the
+    // pull then has the GPU alone), 2 the item exchange's enqueue -- measured, emulated rank 0 of
+    // 8: 74.0-74.7 / 85.5-85.7 / 88.6-92.0 us per step (profiles/r5/owner/emul_order_r5x.txt).
+    // It is enqueued as soon as that point is: behind the host's later launches it starts late
+    static const int after = [] { const char *v = getenv("RG_OWNER_USER_AFTER"); return v ? atoi(v) : RG_OWNER_USER_AFTER_DEFAULT; }();
     const rg_opt_t o = opt_at(st, st.cfg.step + 1);
-    if (side) {
-        if ((rc = record(ev0, u))) return rc;
-        if ((rc = owner_user_update(st, u, next, o))) return rc;
-        if ((rc = record(ev1, u))) return rc;
-        if ((e = hipEventRecord(st.own_users, u)) != hipSuccess) return hip_fail("stepper: record the user update", e);
-    }
+    auto start_users = [&]() -> int {
+        if (!side) return RG_OK;
+        hipError_t e2 = hipEventRecord(st.own_grads, s);
+        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(u, st.own_grads, 0);
+        if (e2 != hipSuccess) return hip_fail("stepper: order the user update", e2);
+        int r2 = record(ev0, u);
+        if (r2 == RG_OK) r2 = owner_user_update(st, u, next, o);
+        if (r2 == RG_OK) r2 = record(ev1, u);
+        if (r2 == RG_OK && (e2 = hipEventRecord(st.own_users, u)) != hipSuccess)
+            r2 = hip_fail("stepper: record the user update", e2);
+        return r2;
+    };
+    if ((rc = owner_backward(st, s))) return rc;
+    if (after == 0 && (rc = start_users())) return rc;
     if ((rc = owner_item_grad(st, s, loss_out))) return rc;
+    if (after == 1 && (rc = start_users())) return rc;
     if (item_sharded(st))
         rc = rg::comm_reduce_scatter(st.cfg.comm, s, st.cfg.item_grad, rg_mf_item_grad_chunk(st.cfg.shard_items, tb->dim));
     else
         rc = rg::comm_allreduce_on(st.cfg.comm, s, st.cfg.item_grad, tb->num_items * (int64_t)(tb->dim + 1) + 1);
     if (rc) return rc;
+    if (after >= 2 && (rc = start_users())) return rc;
     st.cfg.step += 1;
     if (!side) {
         if ((rc = record(ev0, u))) return rc;
