@@ -759,9 +759,9 @@ int64_t rg_ncf_mlp_len(int32_t dim);
 /* NeuMF flat parameters (tower layers, then affine_output (1 x (8 + M)) and its bias) */
 int64_t rg_neumf_param_len(int32_t dim, int32_t mf_dim);
 int64_t rg_ncf_mask_units(int32_t dim);
-/* Tile geometry of a model: rows per tile (32 for every tower in the product build, the E = 64
- * MLP's wave kernel included; the 48-row wave tile exists only in the ncf48 A/B variant built
- * with -DRG_NCF_WAVE_ROWS=48), columns per tile (also the plan's units per block), tiles.
+/* Tile geometry of a model: rows per tile (48 for the E = 64 MLP's wave kernel since round 5,
+ * RG_NCF_WAVE_ROWS; 32 for the other towers and NeuMF), columns per tile (also the plan's units
+ * per block), tiles.
  * ABI 2 (rg_version "abi=2"): these three take (dim, mf_dim) / (n_neg, dim, mf_dim) /
  * (cols, n_neg, dim, mf_dim); ABI 1 took fewer arguments. */
 int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim);

@@ -2,7 +2,7 @@
 // implicit.py:347-364; layers [2E, E, ..., 8] -> 1 as ncf_spotlight.py:53-56).
 //
 // One workgroup (4 waves) walks tiles of kRows = 32 examples (the E = 64 MLP's wave kernel:
-// ncfw::kR = RG_NCF_WAVE_ROWS, 32 in the product build, 48 in the ncf48 A/B variant); a tile holds whole
+// ncfw::kR = RG_NCF_WAVE_ROWS = 48 in the product build); a tile holds whole
 // columns (a positive and its n negatives, pairs prepared by rg_mf_prepare), so
 // pairwise losses are resolved inside the tile.  Everything of a tile lives in
 // LDS: the MLP parameters (loaded once per workgroup), the activations of every
@@ -787,9 +787,10 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
 }
 
 // ============================================================================================
-// E = 64 tower (C3, mf_dim = 0): one WAVE per tile of RG_NCF_WAVE_ROWS rows -- 32 in the product
-// build (1,639 tiles at B = 8192, n = 5); the ncf48 A/B variant's 48-row tile (8 whole columns of
-// 1 + 5 rows: 1,024 tiles, one per wave of the 256 x 4-wave grid) measured no faster.
+// E = 64 tower (C3, mf_dim = 0): one WAVE per tile of RG_NCF_WAVE_ROWS rows -- 48 in the product
+// build since round 5 (8 whole columns of 1 + 5 rows: 1,024 tiles at B = 8192, n = 5, one per wave
+// of the 256 x 4-wave grid), the forward one example block at a time; 32-row tiles (1,639 tiles,
+// two rounds) measured 73.3 against 64.0 us.
 //
 // The tile kernel above keeps every activation in LDS and spreads a tile's MFMA tiles over 8
 // waves: ~12 workgroup barriers and an LDS -> MFMA -> LDS round trip per layer, 14 % of the
@@ -817,8 +818,19 @@ __global__ __launch_bounds__(256) void ncf_adapt_dp_kernel(const float *scores, 
 // ============================================================================================
 namespace ncfw {
 constexpr int kWaves = 4, kThreads = 64 * kWaves;
+// The forward one 16-example block at a time (as the backward), so a 48-row tile -- 8 whole
+// columns of 1 + 5 rows, 1,024 tiles at B = 8192: one per wave slot, no second round -- fits the
+// registers (12 B of scratch; 80 B with the forward over all blocks at once).  Measured (round 5,
+// profiles/r5/ncf/ncf_fwd_r6a.txt): 73.3 us per launch with 32-row tiles (1,639 tiles: two rounds
+// on 1,024 slots), 64.0 with these; 0: every block's forward at once (32 rows: 73.2 us)
+#ifndef RG_NCF_FWD_ROLLED
+#define RG_NCF_FWD_ROLLED 0      // 1: the blockwise forward's block loop kept rolled (400 B of scratch)
+#endif
+#ifndef RG_NCF_FWD_BLOCKWISE
+#define RG_NCF_FWD_BLOCKWISE 1
+#endif
 #ifndef RG_NCF_WAVE_ROWS
-#define RG_NCF_WAVE_ROWS 32   // 48 (8 whole columns, one tile per wave) measured 4 % slower per step
+#define RG_NCF_WAVE_ROWS 48   // 32: two rounds of tiles at B = 8192, n = 5 (1,639 tiles on 1,024 slots)
 #endif
 constexpr int kR = RG_NCF_WAVE_ROWS, NB = kR / 16;   // 48 rows = 3 example blocks of 16 (n = 5: 8 whole columns)
 // weights in LDS (floats): W_k row-major [out][in + 4] (b128 rows land on distinct 16-B slots),
@@ -994,6 +1006,23 @@ template <int T, int RS>
 __device__ __forceinline__ void stage1(const v4f (&y)[T], float *R, int row, int g) {
 #pragma unroll
     for (int t = 0; t < T; ++t) *reinterpret_cast<v4f *>(R + at<RS>(row, 16 * t + 4 * g)) = y[t];
+}
+
+// Y^T (TO tiles) = W X^T for one example block (the forward one 16-example block at a time)
+template <int TI, int TO>
+__device__ __forceinline__ void fwd1(const v4f (&x)[TI], v4f (&y)[TO], const float *W, int S, int g, int m) {
+#pragma unroll
+    for (int t = 0; t < TO; ++t) y[t] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti) {
+        v4f a[TO];
+#pragma unroll
+        for (int t = 0; t < TO; ++t) a[t] = *reinterpret_cast<const v4f *>(W + (16 * t + m) * S + 16 * ti + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TO; ++t) y[t] = mfma(a[t][r], x[ti][r], y[t]);
+    }
 }
 
 // bit of unit (t, nb, r) of a layer in its keep word
@@ -1293,6 +1322,60 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                         y[t][nb][r] = z * m;
                     }
         };
+#if RG_NCF_FWD_BLOCKWISE
+        // the forward one 16-example block at a time (as the backward): one block's activations
+        // live at once, so a 48-row tile (three blocks) fits the registers of a 32-row one
+        auto activate1 = [&](auto &y, const float *b, uint64_t kw, int bit0, int nb) {
+            constexpr int T = sizeof(y) / sizeof(y[0]);
+            v4f bv[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t) bv[t] = *reinterpret_cast<const v4f *>(b + 16 * t + 4 * g);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float z = y[t][r] + bv[t][r];
+                    const float m1 = z > 0.0f ? 1.0f : 0.1f;
+                    const float m = training ? (((kw >> (bit0 + kbit(t, nb, r))) & 1U) ? 2.0f * m1 : 0.0f) : m1;
+                    y[t][r] = z * m;
+                }
+        };
+        const float bo = sw[oBo];
+#if RG_NCF_FWD_ROLLED
+#pragma unroll 1
+#else
+#pragma unroll
+#endif
+        for (int nb = 0; nb < NB; ++nb) {
+            const int row = nb * 16 + j;
+            v4f xb[8], a1[4], a2[2], a3[1], a4[1], zb[1];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) xb[t] = x0[t][nb];
+            fwd1<8, 4>(xb, a1, W1s, S1, g, j);
+            activate1(a1, sw + oB1, kb1, 0, nb);
+            stage1<4, R1S>(a1, R1, row, g);
+            fwd1<4, 2>(a1, a2, W2s, S2, g, j);
+            activate1(a2, sw + oB2, kb2, 0, nb);
+            stage1<2, R2S>(a2, R2, row, g);
+            fwd1<2, 1>(a2, a3, W3s, S3, g, j);
+            activate1(a3, sw + oB3, kb2, 24, nb);
+            stage1<1, R3S>(a3, R3, row, g);
+            fwd1<1, 1>(a3, a4, W4s, S4, g, j);
+            activate1(a4, sw + oB4, kb2, 36, nb);
+            if (kBackward) {   // A_4 rows with a ones feature (8) for the output layer's bias gradient
+                v4f a4s[1] = {a4[0]};
+                if (g == 2) a4s[0][0] = 1.0f;
+                stage1<1, R4S>(a4s, R4, row, g);
+            }
+            fwd1<1, 1>(a4, zb, Wos, SO, g, j);
+            if (g == 0) {
+                const float p = sigmoidf_ref(zb[0][0] + bo);
+                sP[row] = p;
+                if (PHASE == kNcfScores) a.scores[tile * kR + row] = ue[nb] >= 0 ? p : 0.0f;
+            }
+        }
+        WS(3);
+#else
         v4f y1[4][NB], y2[2][NB], y3[1][NB], y4[1][NB];
         fwd<8, 4>(x0, y1, W1s, S1, g, j);
         WS(3);
@@ -1326,6 +1409,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                 if (PHASE == kNcfScores) a.scores[tile * kR + nb * 16 + j] = ue[nb] >= 0 ? p : 0.0f;
             }
         }
+#endif
         // list entries of the claimed slots (the atomics have returned by now)
         if (kBackward && lane < kR) {
             const int64_t ex = tile * kR + lane;
@@ -1732,9 +1816,9 @@ static int64_t ncf_param_len(const rg_ncf_model_t *m) {
     return m->mf_dim == 0 ? ncf_mlp_len(m->dim) : rg_neumf_param_len(m->dim, m->mf_dim);
 }
 extern "C" int64_t rg_ncf_mask_units(int32_t dim) { return ncf_mask_units(dim); }
-// rows per tile: RG_NCF_WAVE_ROWS for the wave kernel (E = 64 MLP; 32 in the product build, 48 --
-// 8 columns of 1 + 5 rows, one tile per wave -- only in the ncf48 A/B variant), 32 for the tile
-// kernel (the other towers, NeuMF)
+// rows per tile: RG_NCF_WAVE_ROWS for the wave kernel (E = 64 MLP; 48 in the product build --
+// 8 columns of 1 + 5 rows, one tile per wave at B = 8192), 32 for the tile kernel (the other
+// towers, NeuMF)
 extern "C" int64_t rg_ncf_rows_per_tile(int32_t dim, int32_t mf_dim) {
     if (ncf_mlp_len(dim) < 0 || mf_dim < 0 || mf_dim > RG_NEUMF_MAX_MF_DIM) return -1;
     return ncf_use_wave(dim, mf_dim) ? ncfw::kR : kRows;

@@ -121,8 +121,8 @@ def test_no_gpu_means_loud_failure():
 
 def test_ncf_launch_geometry():
     """Host-side shape functions (no GPU): the E = 64 MLP runs one wave per tile of
-    rg_ncf_rows_per_tile(64, 0) rows (32 in the product; 48 = 8 whole columns of 1 + 5 rows in the
-    -DRG_NCF_WAVE_ROWS=48 build), 4 waves per workgroup, at most 256 workgroups; the other towers
+    rg_ncf_rows_per_tile(64, 0) rows (48 = 8 whole columns of 1 + 5 rows in the product; 32 in a
+    -DRG_NCF_WAVE_ROWS=32 build), 4 waves per workgroup, at most 256 workgroups; the other towers
     and NeuMF keep the tile kernel's 32-row tiles and workgroup-per-tile count (capped by LDS)."""
     from recommendation_gans_amd import _lib
     L = _lib.load()
