@@ -80,5 +80,13 @@ def run_rms(name, A, lda, akm, Bm, ldb, bkm, M, N, K, reps=10):
     print(json.dumps({"shape": "torch rmsprop same size", "us": round(us2, 1)}), flush=True)
 
 
+if "--rms-sweep" in sys.argv:
+    # wave quantization of the W1S update: 4 x ceil(N / 128) tiles on 256 CUs x 3 workgroups
+    # (768 slots): N = 98,304 fills four rounds exactly, N = 100,540 (the model) spills 72 tiles
+    # into a fifth
+    # measured (round 5): 377 / 379 / 353 us at 2,976 / 3,072 / 3,076 tiles -- no round quantization
+    for n_ in (98304 - 128 * 24, 98304, 98304 + 128, KS - 4):
+        run_rms(f"D1 dW + RMSprop N={n_} tiles={4 * -(-n_ // 128)}", dl1, H2, 0, fake, KS, 0, H2, n_, B)
+    sys.exit(0)
 run_rms("D1 dW + RMSprop (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, KS - 4, B)
 run_rms("heads dW + RMSprop (AM,BN)", fake, KS, 0, a2, H, 0, KS - 4, H, B)
