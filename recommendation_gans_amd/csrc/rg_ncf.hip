@@ -823,6 +823,10 @@ constexpr int kWaves = 4, kThreads = 64 * kWaves;
 // registers (12 B of scratch; 80 B with the forward over all blocks at once).  Measured (round 5,
 // profiles/r5/ncf/ncf_fwd_r6a.txt): 73.3 us per launch with 32-row tiles (1,639 tiles: two rounds
 // on 1,024 slots), 64.0 with these; 0: every block's forward at once (32 rows: 73.2 us)
+#ifndef RG_NCF_EARLY_TILE
+#define RG_NCF_EARLY_TILE 0      // 1: the first tile begun before the weights' barrier (its loop-carried
+                                 // state costs 184 B of scratch: not measured, not kept on)
+#endif
 #ifndef RG_NCF_FWD_ROLLED
 #define RG_NCF_FWD_ROLLED 0      // 1: the blockwise forward's block loop kept rolled (400 B of scratch)
 #endif
@@ -1235,6 +1239,18 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int k = 0; k < PTT; ++k)
         if (tid + k * kThreads < kTail) sw[oW4 + tid + k * kThreads] = wvt[k];
+#if RG_NCF_EARLY_TILE
+    // the first tile's ids and its X0 gather issued before the weights' barrier (they touch only
+    // this wave's LDS rows and global memory): its latency overlaps the other waves' weight copy
+    int ru = -1, ri = -1, rps = -1, ue[NB], ie[NB], re[NB];
+    uint32_t ke[NB];
+    v4f x0[8][NB];
+    bool begun = false;
+    if (first < a.tiles) {
+        begin_tile(a.tc, ru, ri, rps, ue, ie, re, ke, x0);
+        begun = true;
+    }
+#endif
     __syncthreads();
     float warm = 0.0f;   // the next tile's embedding lines, touched during this tile's backward
     for (int64_t tile = first; tile < a.tiles; tile += waves_total) {
@@ -1243,10 +1259,15 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         const int tl_ = (int)((tile - first) / waves_total);
         (void)tl_;
         WS(0);
+#if RG_NCF_EARLY_TILE
+        if (!begun) begin_tile(tc, ru, ri, rps, ue, ie, re, ke, x0);
+        begun = false;
+#else
         int ru = -1, ri = -1, rps = -1, ue[NB], ie[NB], re[NB];
         uint32_t ke[NB];
         v4f x0[8][NB];
         begin_tile(tc, ru, ri, rps, ue, ie, re, ke, x0);
+#endif
         if (warm == 1.0e30f && a.n_pos < 0) a.scores[0] = warm;   // keeps the warm-up loads (never taken)
         WS(1);
         // dropout bits of every unit of the tile, computed while the gather is in flight
@@ -1610,7 +1631,11 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
                     *reinterpret_cast<v4f *>(a.contrib + (tile * kR + row) * (int64_t)128 + 32 * qq + 16 * t + 4 * g) = dx[t];
+#ifdef RG_X_NCF_NOOVF   // timing experiments only (wrong results): no overflow accumulation
+                if (false) {
+#else
                 if ((hh == 0 ? lu : li) >= kNcfCap) {
+#endif
                     const int64_t orow = hh == 0 ? (int64_t)ur : a.num_users + ir;
 #pragma unroll
                     for (int t = 0; t < 2; ++t)

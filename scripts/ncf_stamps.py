@@ -81,6 +81,8 @@ def wave_main(lib, e, tu, ti, plans, args, B):
     nw = e.blocks * 4
     buf = torch.zeros(nw * 3 * 16, dtype=torch.int64, device=tu.device)
     res = {p: [] for p in WAVE_PHASES}
+    tail = {p: [] for p in WAVE_PHASES}   # p95 over the waves of a phase
+    tile_p = []                           # p50 / p90 / max over the waves of a whole tile
     tile_us, first_us, kern_us, pro, red_us, wr_us, tiles_done, bar_wait, ends = [], [], [], [], [], [], [], [], []
     for s in range(args.steps):
         on = s >= args.steps // 2
@@ -95,6 +97,9 @@ def wave_main(lib, e, tu, ti, plans, args, B):
             ok0 = st[:, 0, 13] > 0
             for k, p in enumerate(WAVE_PHASES):
                 res[p].append(float(np.median(t[ok0, 0, k + 1] - t[ok0, 0, k])))
+                tail[p].append(float(np.percentile(t[ok0, 0, k + 1] - t[ok0, 0, k], 95)))
+            tw = t[ok0, 0, 13] - t[ok0, 0, 0]
+            tile_p.append([float(np.percentile(tw, 50)), float(np.percentile(tw, 90)), float(tw.max())])
             tile_us.append(float(np.median(t[ok0, 0, 13] - t[ok0, 0, 0])))
             first_us.append(float(np.percentile(t[ok0, 0, 0], 90)))
             # record 2 (kernel level): 0 entry, 1 tiles done, 2 after the workgroup barrier,
@@ -118,7 +123,9 @@ def wave_main(lib, e, tu, ti, plans, args, B):
                       "barrier_wait_us_median": round(float(np.median(bar_wait)), 2),
                       "reduction_us_median": round(float(np.median(red_us)), 2),
                       "partial_write_us_median": round(float(np.median(wr_us)), 2),
-                      "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()}}, indent=1))
+                      "tile_us_p50_p90_max": [round(float(np.median([x[i] for x in tile_p])), 2) for i in range(3)],
+                      "phase_median_us": {p: round(float(np.median(v)), 2) for p, v in res.items()},
+                      "phase_p95_us": {p: round(float(np.median(v)), 2) for p, v in tail.items()}}, indent=1))
 
 
 if __name__ == "__main__":
