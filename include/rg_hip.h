@@ -341,8 +341,8 @@ int rg_mf_pipe_step(void *stream, const rg_mf_tables_t *tables, rg_mf_work_t *wo
 int rg_mf_prepare_hot(void *stream, const rg_mf_batch_t *batch, const rg_mf_work_t *work, int32_t *hot_out,
                       int32_t *nhot_out);
 
-/* The single-GPU step as TWO launches per step t (the stepper's default for pointwise / bpr / hinge,
- * rg_mf_stepper_train_ahead), replacing run_train_iteration (implicit.py:347-364) of
+/* The single-GPU step as TWO launches per step t (opt-in, RG_PIPE2=1, for pointwise / bpr / hinge via
+ * rg_mf_stepper_train_ahead; measured slower than the split step), replacing run_train_iteration (implicit.py:347-364) of
  * step t+1 up to its backward and the optimizer step (implicit.py:363, spotlight/optimizers.py:10-16)
  * of step t, with step t+1's latency-bound pair pass beside the HBM-bound update of the rows it does
  * not read:

@@ -1,5 +1,5 @@
-"""The two-launch pipelined single-GPU MF step (rg_mf_pipe2_hot / rg_mf_pipe2_cold, the stepper's
-default: step t's dense update of the rows step t+1's pair pass reads, then that pair pass beside the
+"""The two-launch pipelined single-GPU MF step (rg_mf_pipe2_hot / rg_mf_pipe2_cold; opt-in,
+RG_PIPE2=1, measured slower than the split step: step t's dense update of the rows step t+1's pair pass reads, then that pair pass beside the
 update of every other row and step t+2's prepare) against the split step (RG_PIPE2=0): the same
 per-row and per-column arithmetic, so losses, tables, optimizer state and the MT stream are
 bit-identical -- after EVERY step, over several steps, with item plans and Zipf-hot rows overflowing
