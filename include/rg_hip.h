@@ -959,6 +959,13 @@ int rg_gemm_f32_rms(void *stream, const float *A, int64_t lda, int32_t a_kmajor,
                     int32_t b_kmajor, int64_t M, int64_t N, int64_t K, float *P, float *V, int64_t ldp, float lr,
                     float alpha, float eps);
 
+/* The optimizer GEMM's form (W1S / WH weight gradient fused with the update; test /
+ * measurement entry): mode 0 the 3-workgroup-per-CU kernel with the update in its epilogue
+ * (the product), 1 the wave-specialised persistent kernel (matrix, loader and update waves of
+ * one workgroup overlap; measured slower, A/B build only: -1 and rg_last_error elsewhere),
+ * < 0 leaves it.  Returns the form in force before the call.  Both give identical bits. */
+int rg_gemm_ws_mode(int32_t mode);
+
 /* Milliseconds between two timing events (hipEvent_t) recorded on a stream. */
 int rg_event_elapsed_ms(void *ev_begin, void *ev_end, float *ms);
 

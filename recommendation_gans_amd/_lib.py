@@ -185,6 +185,7 @@ SIGNATURES = [
                                      ctypes.c_void_p, ctypes.c_void_p]),
     ("rg_gan_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GANModel), ctypes.c_void_p,
                                        ctypes.POINTER(GANBatch), ctypes.c_void_p, ctypes.c_void_p]),
+    ("rg_gemm_ws_mode", ctypes.c_int, [ctypes.c_int32]),
     ("rg_gemm_f32_rms", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,

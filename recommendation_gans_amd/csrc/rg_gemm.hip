@@ -19,6 +19,8 @@
 // reduction, so every result is deterministic.
 #include "rg_gemm.h"
 
+#include <atomic>
+
 namespace rg {
 
 namespace {
@@ -417,6 +419,308 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONE ? 
     }
 }
 
+#if RG_AB   // measured slower than gemm_kernel's optimizer epilogue: A/B build only
+// ---------------------------------------------------------------- wave-specialised optimizer GEMM
+// The optimizer epilogue (kEpiOpt) with both operands M/N-major, as a persistent kernel of one
+// 512-thread workgroup per CU whose waves split the two phases of a tile: waves 0-3 run the K
+// loop of tile i (the 2 x 2 grid of 64 x 64 wave tiles above, operands staged by direct-to-LDS
+// loads two K steps ahead, synchronised by LDS counters -- no workgroup barrier), while waves 4-7
+// stream the optimizer update of tile i - 1 (P and its state, the HBM-bound half).  The matrix
+// cores and the HBM stream overlap inside one CU instead of across the three lock-prone
+// workgroups of gemm_kernel<.., kEpiOpt, true>.
+//
+// Same K order per lane (k = 16h + t at MFMA t, K steps in order), same hits order, same
+// update arithmetic: results are bit-identical to gemm_kernel's optimizer epilogue.
+constexpr int kWsThreads = 768;   // waves 0-3 matrix, 4-7 update, 8-11 loaders
+constexpr int kWsRows = 16;      // rows per update thread (128 rows over 8 row groups)
+constexpr int kWsQ = 4;          // rows of P / state in flight per update thread
+
+// LDS hand-over counters without fences: a workgroup-scope fence (even one naming only the local
+// address space) waits vmcnt(0), because a direct-to-LDS load in flight is a pending LDS write,
+// and would drain the operand pipeline at every signal.  Instead a wave's LDS operations execute
+// in order, so a count added after its LDS writes / reads is seen after them; the asm statements
+// keep the compiler from moving memory operations across the signal or the wait, and the
+// operand stages' own arrival is counted by hand (ws_vmcnt) before the `full` signal.
+__device__ __forceinline__ int lds_acquire(const int *p) {
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+// wait for an LDS counter; bounded (~0.5 s) so that a broken hand-over ends the kernel with
+// wrong bits the tests catch instead of a wave that never finishes
+__device__ __forceinline__ void lds_wait(const int *p, int target) {
+    for (int n = 0; lds_acquire(p) < target && n < (1 << 23); ++n) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void lds_release_add(int *p) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+
+// the loader waves' counter operations, hidden from hipcc's wait insertion (see above)
+__device__ __forceinline__ uint32_t lds_addr(const int *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)p;
+}
+
+__device__ __forceinline__ void asm_lds_add(int *p) {
+    asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr(p)), "v"(1) : "memory");
+}
+
+__device__ __forceinline__ void asm_lds_wait(const int *p, int target) {
+    for (int n = 0; n < (1 << 23); ++n) {
+        int v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Operand stages shared by the matrix waves: a K step's A panel [BK][128] and B panel
+// [BK][128] (M/N-major rows, unpadded: 2 k rows per 1-KB direct-to-LDS load), 32 KB, three of
+// them so that two K steps are in flight while one is read.  Each matrix wave issues 8 of a
+// stage's 32 global_load_lds_dwordx4 (no registers hold the operands in flight); a stage is
+// full when all four waves have counted their own loads landed (`full`), and free for the K
+// step three later when all four matrix waves have read their fragments from it (`empty`).
+// The result tile goes to the update waves in two 64-row halves through one half-tile buffer
+// (`ready` / `taken`), which keeps the workgroup at 130 KB of LDS.
+constexpr int kWsStages = 3;
+constexpr int kWsStage = 2 * BK * BM;           // floats per stage (A and B panels)
+constexpr int kWsLoads = 8;                     // direct-to-LDS loads per matrix wave per stage
+
+struct WsTile {
+    int64_t m0, n0;
+};
+
+// the global rows of a panel float4 (rows past the end clamped to the last whole float4 of the
+// row: they only reach discarded outputs)
+__device__ __forceinline__ const float *ws_src(const float *X, int64_t ld, int64_t R, int64_t row0, int64_t k,
+                                              int lane) {
+    const int64_t r4 = (R + 3) / 4 * 4;
+    return X + k * ld + min(row0 + (lane & 31) * 4, r4 - 4);
+}
+
+// wait until at most n of this wave's direct-to-LDS loads are outstanding (vmcnt; the loader
+// waves issue no other vector memory operation)
+__device__ __forceinline__ void ws_vmcnt(int n) {
+    static_assert(kWsStages <= 4 && kWsLoads == 8, "the counted waits below");
+    if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool CLAMP, bool HAS_M>
+__global__ __launch_bounds__(kWsThreads) void gemm_opt_ws_kernel(GemmDesc d) {
+    constexpr int LDE = BN + 4;
+    // ONE shared array (a second __shared__ object beside the direct-to-LDS stages makes hipcc
+    // wait vmcnt(0) before LDS reads): stages | half tile | counters
+    __shared__ __attribute__((aligned(16))) float lds[kWsStages * kWsStage + 64 * LDE + 16];
+    float *const stages = lds, *const half = lds + kWsStages * kWsStage;
+    int *const ctr = reinterpret_cast<int *>(half + 64 * LDE);
+    int *const ready = ctr, *const taken = ctr + 1, *const full = ctr + 2, *const empty = ctr + 2 + kWsStages;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 2 + 2 * kWsStages) ctr[tid] = 0;
+    __syncthreads();                                  // the only workgroup barrier
+    // 32-bit tile arithmetic in scalars (tile counts are far below 2^31)
+    const int tm = (int)gemm_tiles_m(d.M), tn = (int)gemm_tiles_n(d.N);
+    const bool m_small = tm <= tn;
+    const int t_small = m_small ? tm : tn, t_big = m_small ? tn : tm;
+    const int x = (int)(blockIdx.x & 7);
+    const int per_x = (int)((gridDim.x - x + 7) / 8), l = (int)(blockIdx.x >> 3);
+    const int tiles_x = t_small * ((t_big - x + 7) / 8);                     // this XCD's tiles
+    const int ntiles = l < tiles_x ? (tiles_x - l + per_x - 1) / per_x : 0;  // this workgroup's
+    // the n-th tile of this workgroup: panel x + 8 * (j / t_small) of its XCD, j = l + n * per_x
+    auto tile_of = [=](int n) -> WsTile {
+        const int j = l + n * per_x, panel = (j / t_small) * 8 + x, minor = j % t_small;
+        return m_small ? WsTile{(int64_t)minor * BM, (int64_t)panel * BN} : WsTile{(int64_t)panel * BM, (int64_t)minor * BN};
+    };
+
+    const int nk = (int)(d.K / BK);
+    const int T = ntiles * nk;                       // K steps of this workgroup, one stream G
+    if (wave >= 8) {
+        // ---- loader waves: the operand stages, two K steps ahead of the matrix waves.  Waves
+        // 8-9 load the A panel's k-row pairs, 10-11 the B panel's (8 each per stage).  They issue
+        // no other vector memory operation, so the counted vmcnt below is exact; their counter
+        // operations are asm (hipcc would otherwise wait vmcnt(0) before every LDS access that
+        // follows a direct-to-LDS load, draining the pipeline)
+        const int w = wave - 8;
+        const bool opa = w < 2;
+        const float *X = opa ? d.A : d.B;
+        const int64_t ld = opa ? d.lda : d.ldb, R = opa ? d.M : d.N;
+        const int kp0 = (w & 1) * kWsLoads;
+        float *const dst0 = stages + (opa ? 0 : BK * BM) + kp0 * 2 * BM;
+        auto issue = [=](int G) {
+            const WsTile tl = tile_of(G / nk);
+            const int64_t k0 = (int64_t)(G % nk) * BK;
+            const float *src = ws_src(X, ld, R, opa ? tl.m0 : tl.n0, k0 + 2 * kp0 + (lane >> 5), lane);
+            float *dst = dst0 + (G % kWsStages) * kWsStage;
+#pragma unroll
+            for (int i = 0; i < kWsLoads; ++i)
+                __builtin_amdgcn_global_load_lds(src + 2 * i * ld, dst + i * 2 * BM, 16, 0, 0);
+        };
+        for (int G = 0; G < T && G < kWsStages; ++G) issue(G);
+        for (int G = 0; G < T; ++G) {
+            const int st = G % kWsStages, use = G / kWsStages;
+            ws_vmcnt((min(T - 1, G + kWsStages - 1) - G) * kWsLoads);   // stage G landed
+            if (lane == 0) asm_lds_add(full + st);
+            if (G + kWsStages < T) {
+                asm_lds_wait(empty + st, 4 * (use + 1));               // every matrix wave read it
+                issue(G + kWsStages);
+            }
+        }
+        ws_vmcnt(0);
+        return;
+    }
+    if (wave < 4) {
+        // ---- matrix waves: the 2 x 2 grid of 64 x 64 wave tiles, fragments from the stages
+        const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+        v16f acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
+        for (int G = 0; G < T; ++G) {
+            const int st = G % kWsStages, use = G / kWsStages;
+            lds_wait(full + st, 4 * (use + 1));
+            const float *sa = stages + st * kWsStage, *sb = sa + BK * BM;
+            float a[2][16], b[2][16];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    a[i][t] = sa[(16 * h + t) * BM + wm * 64 + i * 32 + l32];
+                    b[i][t] = sb[(16 * h + t) * BN + wn * 64 + i * 32 + l32];
+                }
+            if (lane == 0) lds_release_add(empty + st);      // after the reads (in order)
+            if constexpr (CLAMP) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) b[i][t] = fminf(fmaxf(b[i][t], -d.clamp_b), d.clamp_b);
+            }
+#ifndef RG_X_WS_NOMFMA   // timing experiments only (wrong results): the matrix waves skip the MFMAs
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+                        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[jj][t], acc[i][jj], 0, 0, 0);
+#else
+            acc[0][0][0] += a[0][0] + b[0][0];
+#endif
+            if (G % nk == nk - 1) {
+                // hand the tile over: this wave's 64-row half u = 2n + wm, once halves < u are taken
+                const int u = 2 * (G / nk) + wm;
+                lds_wait(taken, 4 * u);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            half[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDE + wn * 64 + jj * 32 + l32] =
+                                acc[i][jj][r];
+                            acc[i][jj][r] = 0.0f;
+                        }
+                if (lane == 0) lds_release_add(ready);
+            }
+        }
+        return;
+    }
+    // ---- update waves: hits, then the optimizer over P and its state, rows as float4 groups
+    constexpr int Q = HAS_M ? 2 : kWsQ;             // rows in flight per thread (registers: Adam's m)
+    const int et = tid - 256, c4 = et & 31, r0 = et >> 5;
+    for (int n = 0; n < ntiles; ++n) {
+        const WsTile tl = tile_of(n);
+        const int64_t m0 = tl.m0, n0 = tl.n0, nn = n0 + 4 * c4;
+        float4 g[kWsRows];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            lds_wait(ready, 2 * (2 * n + hf + 1));   // the half's two matrix waves
+#pragma unroll
+            for (int q = 0; q < kWsRows / 2; ++q)
+                g[hf * (kWsRows / 2) + q] = *reinterpret_cast<const float4 *>(half + (r0 + 8 * q) * LDE + 4 * c4);
+            if (lane == 0) lds_release_add(taken);  // one count per wave, after its reads (in order)
+        }
+        // sparse extra gradient rows of this column tile (hits sorted by column), in hit order
+        const int64_t ntile = n0 / BN;
+        const int lo = d.n_hits > 0 ? d.hit_tile_off[ntile] : 0, hi = d.n_hits > 0 ? d.hit_tile_off[ntile + 1] : 0;
+        for (int hx = lo; hx < hi; ++hx) {
+            const int64_t c = d.hit_col[hx] - nn;
+            if (c < 0 || c > 3) continue;
+            const float *src = d.hit_src + (int64_t)d.hit_row[hx] * d.hit_ld;
+#pragma unroll
+            for (int q = 0; q < kWsRows; ++q) {
+                const int64_t m = m0 + r0 + 8 * q;
+                if (m >= d.M) continue;
+                const float sv = src[m];
+                if (c == 0) g[q].x += sv; else if (c == 1) g[q].y += sv; else if (c == 2) g[q].z += sv; else g[q].w += sv;
+            }
+        }
+#ifdef RG_X_WS_NOUPD   // timing experiments only (wrong results): the update waves only take the tiles
+        if (g[0].x != 12345.0f) continue;
+#endif
+        const bool vec = nn + 3 < d.N && (d.ldp & 3) == 0 && aligned16(d.P) && (!d.Ms || aligned16(d.Ms)) &&
+                         (!d.Vs || aligned16(d.Vs));
+#pragma unroll
+        for (int q0 = 0; q0 < kWsRows; q0 += Q) {
+            float4 pv[Q], mv[HAS_M ? Q : 1], vv[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int64_t m = m0 + r0 + 8 * (q0 + q), e = m * d.ldp + nn;
+                pv[q] = vv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (HAS_M) mv[HAS_M ? q : 0] = pv[q];
+                if (m < d.M && vec) {
+                    pv[q] = *reinterpret_cast<const float4 *>(d.P + e);
+                    if (HAS_M) mv[HAS_M ? q : 0] = *reinterpret_cast<const float4 *>(d.Ms + e);
+                    if (d.Vs) vv[q] = *reinterpret_cast<const float4 *>(d.Vs + e);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int64_t m = m0 + r0 + 8 * (q0 + q), e = m * d.ldp + nn;
+                if (m >= d.M) continue;
+                const float4 gg = g[q0 + q];
+                if (vec) {
+                    float4 mq = HAS_M ? mv[HAS_M ? q : 0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    opt4(d.opt, d.clamp_p, pv[q], gg, mq, vv[q]);
+                    *reinterpret_cast<float4 *>(d.P + e) = pv[q];
+                    if (HAS_M) *reinterpret_cast<float4 *>(d.Ms + e) = mq;
+                    if (d.Vs) *reinterpret_cast<float4 *>(d.Vs + e) = vv[q];
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        if (nn + c >= d.N) continue;
+                        float p = d.P[e + c], mm = HAS_M ? d.Ms[e + c] : 0.0f, v1 = d.Vs ? d.Vs[e + c] : 0.0f;
+                        const float gc = c == 0 ? gg.x : c == 1 ? gg.y : c == 2 ? gg.z : gg.w;
+                        opt1(d.opt, d.clamp_p, p, gc, mm, v1);
+                        d.P[e + c] = p;
+                        if (HAS_M) d.Ms[e + c] = mm;
+                        if (d.Vs) d.Vs[e + c] = v1;
+                    }
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// the optimizer GEMM's form: 1 the wave-specialised kernel, 0 gemm_kernel's epilogue
+// (RG_GEMM_WS at load, rg_gemm_ws_mode at run time)
+std::atomic<int> g_gemm_ws{[] { const char *v = getenv("RG_GEMM_WS"); return v ? atoi(v) : 0; }()};
+
+namespace {
+
+bool gemm_ws_enabled() { return g_gemm_ws.load(std::memory_order_relaxed) != 0; }
+#endif  // RG_AB
+
 template <bool AK, bool BKM>
 void launch_epi(hipStream_t stream, const GemmDesc &d, dim3 grid) {
     switch (d.epi) {
@@ -464,6 +768,21 @@ int gemm(hipStream_t stream, const GemmDesc &d) {
     if (d.n_hits > 0 && (!d.hit_tile_off || !d.hit_col || !d.hit_row || !d.hit_src))
         return fail_arg("gemm: hits need hit_col, hit_row, hit_src and per-tile offsets");
     if ((d.epi == kEpiStore || d.epi == kEpiPartial) && !d.C) return fail_arg("gemm: no C");
+#if RG_AB
+    // (K a whole number of K steps; byte offsets of both operands within 32 bits)
+    if (d.epi == kEpiOpt && !d.a_kmajor && !d.b_kmajor && d.K % BK == 0 && d.K > 0 &&
+        d.K * d.lda * 4 < INT32_MAX && d.K * d.ldb * 4 < INT32_MAX && gemm_ws_enabled()) {
+        // persistent: one workgroup per CU, a multiple of 8 (each XCD label owns its panels)
+        const int64_t wg = std::min<int64_t>(num_cus(), gemm_tiles_m(d.M) * gemm_tiles_n(d.N));
+        const dim3 grid((unsigned)(8 * ((wg + 7) / 8)));
+        const bool cl = d.clamp_b > 0.0f, hm = d.Ms != nullptr;
+        if (cl && hm) hipLaunchKernelGGL((gemm_opt_ws_kernel<true, true>), grid, dim3(kWsThreads), 0, stream, d);
+        else if (cl) hipLaunchKernelGGL((gemm_opt_ws_kernel<true, false>), grid, dim3(kWsThreads), 0, stream, d);
+        else if (hm) hipLaunchKernelGGL((gemm_opt_ws_kernel<false, true>), grid, dim3(kWsThreads), 0, stream, d);
+        else hipLaunchKernelGGL((gemm_opt_ws_kernel<false, false>), grid, dim3(kWsThreads), 0, stream, d);
+        return check_launch("gemm_opt_ws_kernel");
+    }
+#endif
     const dim3 grid((unsigned)TileMap(d).blocks());
     if (d.a_kmajor) {
         if (d.b_kmajor) launch_epi<true, true>(stream, d, grid);
@@ -514,4 +833,21 @@ extern "C" int rg_gemm_f32_rms(void *stream, const float *A, int64_t lda, int32_
     d.opt.lr = lr; d.opt.alpha = alpha; d.opt.eps = eps;
     d.opt.one_minus_alpha = (float)(1.0 - (double)alpha);
     return rg::gemm((hipStream_t)stream, d);
+}
+
+// the optimizer GEMM's form (test / measurement entry): mode 0 gemm_kernel's fused epilogue,
+// 1 the wave-specialised persistent kernel (A/B build only: -1 elsewhere), < 0 leaves it;
+// returns the form in force before
+extern "C" int rg_gemm_ws_mode(int32_t mode) {
+#if RG_AB
+    const int prev = rg::g_gemm_ws.load();
+    if (mode >= 0) rg::g_gemm_ws.store(mode != 0 ? 1 : 0);
+    return prev;
+#else
+    if (mode > 0) {
+        rg::set_error("rg_gemm_ws_mode: the wave-specialised optimizer GEMM is in the A/B build only (DESIGN 4.3)");
+        return -1;
+    }
+    return 0;
+#endif
 }

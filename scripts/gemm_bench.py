@@ -80,6 +80,14 @@ def run_rms(name, A, lda, akm, Bm, ldb, bkm, M, N, K, reps=10):
     print(json.dumps({"shape": "torch rmsprop same size", "us": round(us2, 1)}), flush=True)
 
 
+if "--ws-ab" in sys.argv:
+    # the two forms of the optimizer GEMM (rg_gemm_ws_mode 0: the update in gemm_kernel's
+    # epilogue, 1: the wave-specialised persistent kernel), alternating
+    for mode in (0, 1, 0, 1):
+        L.rg_gemm_ws_mode(mode)
+        run_rms(f"ws{mode} D1 dW + RMSprop (AM,BN)", dl1, H2, 0, fake, KS, 0, H2, KS - 4, B)
+        run_rms(f"ws{mode} heads dW + RMSprop (AM,BN)", fake, KS, 0, a2, H, 0, KS - 4, H, B)
+    sys.exit(0)
 if "--rms-sweep" in sys.argv:
     # wave quantization of the W1S update: 4 x ceil(N / 128) tiles on 256 CUs x 3 workgroups
     # (768 slots): N = 98,304 fills four rounds exactly, N = 100,540 (the model) spills 72 tiles

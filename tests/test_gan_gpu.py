@@ -66,10 +66,24 @@ def test_gemm_bias_tanh():
     assert (got.double() - ref).abs().max() < 2e-6
 
 
+@pytest.fixture(params=[0, 1], ids=["epilogue", "wave_specialised"])
+def gemm_ws(request):
+    """Both forms of the optimizer GEMM (rg_gemm_ws_mode): the update in gemm_kernel's
+    epilogue, and the wave-specialised persistent kernel."""
+    from recommendation_gans_amd import _lib
+    L = _lib.load()
+    if request.param and not _lib.ab_build():
+        assert L.rg_gemm_ws_mode(1) == -1     # the product refuses it
+        pytest.skip("wave-specialised form: A/B build only (scripts/gpu_ab_tests.sh)")
+    prev = L.rg_gemm_ws_mode(request.param)
+    yield request.param
+    L.rg_gemm_ws_mode(prev)
+
+
 @pytest.mark.parametrize("M,N,K,ldp", [(512, 20000, 256, 20000),   # several tiles per workgroup (persistent)
                                        (300, 1001, 64, 1004),      # K < 8 steps, ragged float4 tail column
                                        (130, 5003, 640, 5003)])    # K > 8 steps, rows not float4-aligned
-def test_gemm_rmsprop_matches_float64(M, N, K, ldp):
+def test_gemm_rmsprop_matches_float64(M, N, K, ldp, gemm_ws):
     """The gradient GEMM fused with the RMSprop update (the cGAN's W1S / WH path,
     CGANs.py:440-457 RMSprop on D and G) against a float64 product + update of the
     same fp32 operands: P within the f32 GEMM bound propagated through the update."""
@@ -99,6 +113,42 @@ def test_gemm_rmsprop_matches_float64(M, N, K, ldp):
     # d(lr g / sqrt(v)) / dg <= lr * 2 / sqrt(v): the GEMM bound carried through, plus f32 rounding
     assert ((Pg[:, :N] - pd).abs() <= 2 * lr * gb / vd.sqrt() + 1e-6 * pd.abs() + 1e-9).all()
     assert torch.equal(P.cpu()[:, N:], p0[:, N:]) and torch.equal(V.cpu()[:, N:], v0[:, N:]), "pad columns touched"
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 100540, 256),   # C4's W1S: 3,144 tiles over 256 persistent workgroups
+                                   (100540, 256, 256),   # C4's WH (the long dimension in M)
+                                   (130, 5003, 640)])    # ragged rows and columns
+def test_gemm_rmsprop_forms_bit_identical(M, N, K):
+    """The wave-specialised optimizer GEMM (A/B build; measured slower) gives the
+    same bits as the epilogue form: same per-lane K order, same update arithmetic
+    (rg_gemm.hip gemm_opt_ws_kernel)."""
+    from recommendation_gans_amd import _lib
+    from recommendation_gans_amd.gan_engine import ptr
+    import ctypes
+    L = _lib.load()
+    if not _lib.ab_build():
+        pytest.skip("wave-specialised form: A/B build only (scripts/gpu_ab_tests.sh)")
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    m4, n4 = (M + 3) // 4 * 4, (N + 3) // 4 * 4
+    A = torch.randn(K, m4, device="cuda", generator=g)
+    B = torch.randn(K, n4, device="cuda", generator=g)
+    p0 = torch.randn(M, n4, device="cuda", generator=g) * 0.01
+    v0 = torch.rand(M, n4, device="cuda", generator=g) * 1e-3
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = []
+    prev = L.rg_gemm_ws_mode(-1)
+    try:
+        for mode in (0, 1):
+            L.rg_gemm_ws_mode(mode)
+            P, V = p0.clone(), v0.clone()
+            _lib.check(L.rg_gemm_f32_rms(st, ptr(A), m4, 0, ptr(B), n4, 0, M, N, K, ptr(P), ptr(V), n4,
+                                         1e-3, 0.99, 1e-8), "rg_gemm_f32_rms")
+            torch.cuda.synchronize()
+            out.append((P, V))
+    finally:
+        L.rg_gemm_ws_mode(prev)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert not torch.equal(out[0][0], p0)
 
 
 CASES = ["gan_rms_n50", "gan_adam_n50", "gan_sgd_n64"]
