@@ -5,7 +5,9 @@ the MT state bit-exact (exit status 1 otherwise); at the checked steps every ele
 tables through tests/parity_report.check (the band, the counts outside 1e-5, the reference's own
 count in another fp32 order), appended to gpurun_out/parity_elementwise.jsonl.
 
-    python scripts/parity_long.py [--steps 60] [--loss bpr]
+    python tests/parity_long.py [--steps 60] [--loss bpr] [--dim 64]
+
+(Test infrastructure: it lives under tests/ because it runs the oracle; pytest does not collect it.)
 """
 import argparse
 import json

@@ -1,0 +1,90 @@
+"""C3 (ncf_spotlight.py at ML-20M shape: mlp_embedding_dim 64, tower [128, 64, 32, 16, 8],
+B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5) run longer than the test suite does
+(tests/test_configs_gpu.py::test_ncf_full_size_steps runs 10): S native steps (default 20) with
+item plans and recorded dropout masks against oracle/ncf.py in fp32, fp64 and two more fp32
+restatements summing in other orders.  Every step: the loss within 1e-5 relative and the MT
+state bit-exact (exit status 1 otherwise); at the checked steps every parameter through
+tests/parity_report.check, one JSON line per step.
+
+    python tests/parity_long_ncf.py [--steps 20]
+
+(Test infrastructure: it lives under tests/ because it runs the oracle; pytest does not collect it.)
+"""
+import argparse
+import json
+import os
+import sys
+import warnings
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from oracle import ncf as oncf  # noqa: E402
+from oracle import rng as orng  # noqa: E402
+from tests import parity_report  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.synthetic import ML20M, movielens_like
+    warnings.simplefilter("ignore")
+    data = movielens_like(ML20M, seed=0)
+    dev = torch.device("cuda:0")
+    U, I, E, B, n, steps = data.num_users, data.num_items, 64, 8192, 5, args.steps
+    torch.manual_seed(0)                                   # ncf_spotlight.py: MLP(...) init
+    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    names = [k for k, _ in net.named_parameters()]
+    params = [p.detach().clone() for p in net.parameters()]
+    mt = orng.py_seed_state(0)
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                  device=dev, **kw)
+    o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o32b = [oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k,
+                           **kw) for k in (1, 2)]
+    widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
+    rs = np.random.RandomState(5)
+    checked = {0, 9, steps - 1}
+    worst, bad, tbad = 0.0, 0, 0
+    for s in range(steps):
+        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
+        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
+        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
+        prev = [t.detach().cpu().clone() for t in e.params()]
+        pi_d = torch.from_numpy(pi).to(dev)
+        got = float(e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)[0])
+        l32 = o32.step(pu, pi, mp, mn)
+        o64.step(pu, pi, mp, mn)
+        for ob in o32b:
+            ob.step(pu, pi, mp, mn)
+        torch.cuda.synchronize()
+        rel = abs(got - l32) / abs(l32)
+        worst = max(worst, rel)
+        mt_ok = bool((e.mt_state() == o32.state).all())
+        bad += int(rel > 1e-5 or not mt_ok)
+        line = {"step": s, "loss_gpu": got, "loss_ref32": l32, "loss_rel": rel, "mt_exact": mt_ok}
+        if s in checked:
+            line["tables"] = []
+            for k, (nm, p, r32, r64) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t)):
+                ok, msg = parity_report.check(f"C3 ncf long step {s} {nm}", p.reshape(r32.shape), r32, r64,
+                                              before=prev[k].reshape(r32.shape), alt32=[ob.P.t[k] for ob in o32b])
+                line["tables"].append({"param": nm, "ok": ok, "msg": msg})
+                tbad += int(not ok)
+        print(json.dumps(line), flush=True)
+    print(json.dumps({"steps": steps, "worst_loss_rel": worst, "steps_failing_loss_or_mt": bad,
+                      "table_checks_failing": tbad}), flush=True)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
