@@ -6,7 +6,10 @@ restatements summing in other orders.  Every step: the loss within 1e-5 relative
 state bit-exact (exit status 1 otherwise); at the checked steps every parameter through
 tests/parity_report.check, one JSON line per step.
 
-    python tests/parity_long_ncf.py [--steps 20]
+    python tests/parity_long_ncf.py [--steps 20] [--neumf]
+
+--neumf: neuMF_spotlight.py's defaults instead (mlp_embedding_dim 16, mf_embedding_dim 50; the
+GMF tables included), as tests/test_configs_gpu.py::test_neumf_full_size_steps for 10 steps.
 
 (Test infrastructure: it lives under tests/ because it runs the oracle; pytest does not collect it.)
 """
@@ -29,29 +32,39 @@ from tests import parity_report  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--neumf", action="store_true")
     args = ap.parse_args()
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.ncf_spotlight import mlp_layers
     from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
     warnings.simplefilter("ignore")
     data = movielens_like(ML20M, seed=0)
     dev = torch.device("cuda:0")
-    U, I, E, B, n, steps = data.num_users, data.num_items, 64, 8192, 5, args.steps
-    torch.manual_seed(0)                                   # ncf_spotlight.py: MLP(...) init
-    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
+    E = 16 if args.neumf else 64
+    U, I, B, n, steps = data.num_users, data.num_items, 8192, 5, args.steps
+    torch.manual_seed(0)                                   # ncf_spotlight.py / neuMF_spotlight.py init
+    net = (NeuMF(mlp_layers(E), U, I, mf_embedding_dim=50, mlp_embedding_dim=E) if args.neumf
+           else MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E))
     names = [k for k, _ in net.named_parameters()]
     params = [p.detach().clone() for p in net.parameters()]
     mt = orng.py_seed_state(0)
     kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
-    e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
-                  device=dev, **kw)
-    o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o32b = [oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k,
-                           **kw) for k in (1, 2)]
+    if args.neumf:
+        e = NCFEngine(params[0], params[1], params[4:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                      device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
+    else:
+        e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                      device=dev, **kw)
+    Oracle = oncf.NeuMFOracle if args.neumf else oncf.NCFOracle
+    o32 = Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o64 = Oracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
+    o32b = [Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k, **kw)
+            for k in (1, 2)]
     widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
-    rs = np.random.RandomState(5)
+    rs = np.random.RandomState(6 if args.neumf else 5)
+    tag = "NeuMF" if args.neumf else "C3 ncf"
     checked = {0, 9, steps - 1}
     worst, bad, tbad = 0.0, 0, 0
     for s in range(steps):
@@ -76,7 +89,7 @@ def main():
         if s in checked:
             line["tables"] = []
             for k, (nm, p, r32, r64) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t)):
-                ok, msg = parity_report.check(f"C3 ncf long step {s} {nm}", p.reshape(r32.shape), r32, r64,
+                ok, msg = parity_report.check(f"{tag} long step {s} {nm}", p.reshape(r32.shape), r32, r64,
                                               before=prev[k].reshape(r32.shape), alt32=[ob.P.t[k] for ob in o32b])
                 line["tables"].append({"param": nm, "ok": ok, "msg": msg})
                 tbad += int(not ok)
