@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--neumf", action="store_true")
+    ap.add_argument("--dump", type=int, default=0,
+                    help="at the last step print the N elements farthest outside the fp32 orders' spread")
     args = ap.parse_args()
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.ncf_spotlight import mlp_layers
@@ -94,6 +96,28 @@ def main():
                 line["tables"].append({"param": nm, "ok": ok, "msg": msg})
                 tbad += int(not ok)
         print(json.dumps(line), flush=True)
+        if args.dump and s == steps - 1:
+            seen = np.concatenate([data.train_u[:steps * B]]).astype(np.int64)
+            cnt = np.bincount(seen, minlength=U)
+            last = np.bincount(pu, minlength=U)
+            for k, (nm, p, r32, r64) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t)):
+                g = p.detach().cpu().double().reshape(-1)
+                r64d, r32d = r64.double().reshape(-1), r32.double().reshape(-1)
+                spread = (r32d - r64d).abs()
+                for ob in o32b:
+                    spread = torch.maximum(spread, (ob.P.t[k].double().reshape(-1) - r64d).abs())
+                score = (g - r64d).abs() / (spread + 1e-7 * r64d.abs() + 1e-30)
+                top = torch.topk(score, min(args.dump, score.numel())).indices.tolist()
+                shape = tuple(r32.shape)
+                for ix in top[:args.dump]:
+                    row, col = (ix // shape[1], ix % shape[1]) if len(shape) == 2 else (ix, 0)
+                    rec = {"param": nm, "row": row, "col": col, "score": float(score[ix]), "gpu": float(g[ix]),
+                           "ref32": float(r32d[ix]), "ref64": float(r64d[ix]),
+                           "alt32": [float(ob.P.t[k].double().reshape(-1)[ix]) for ob in o32b]}
+                    if "user" in nm and len(shape) == 2:
+                        rec["user_positives_so_far"] = int(cnt[row])
+                        rec["user_positives_last_step"] = int(last[row])
+                    print(json.dumps({"dump": rec}), flush=True)
     print(json.dumps({"steps": steps, "worst_loss_rel": worst, "steps_failing_loss_or_mt": bad,
                       "table_checks_failing": tbad}), flush=True)
     return 1 if bad else 0
