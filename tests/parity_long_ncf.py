@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--neumf", action="store_true")
     ap.add_argument("--dump", type=int, default=0,
                     help="at the last step print the N elements farthest outside the fp32 orders' spread")
+    ap.add_argument("--track", default="", metavar="PARAM:ROW,...",
+                    help="print every step's max |GPU - fp32 reference| over these parameter rows")
     args = ap.parse_args()
     from recommendation_gans_amd.ncf_engine import NCFEngine
     from recommendation_gans_amd.ncf_spotlight import mlp_layers
@@ -88,6 +90,11 @@ def main():
         mt_ok = bool((e.mt_state() == o32.state).all())
         bad += int(rel > 1e-5 or not mt_ok)
         line = {"step": s, "loss_gpu": got, "loss_ref32": l32, "loss_rel": rel, "mt_exact": mt_ok}
+        for tr in filter(None, args.track.split(",")):
+            pname, prow = tr.rsplit(":", 1)
+            k = names.index(pname)
+            gp = e.params()[k].detach().cpu().reshape(o32.P.t[k].shape)
+            line[f"track {tr}"] = float((gp[int(prow)].double() - o32.P.t[k][int(prow)].double()).abs().max())
         if s in checked:
             line["tables"] = []
             for k, (nm, p, r32, r64) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t)):
