@@ -375,6 +375,24 @@ def gan_flops(N, S, H, E, Z, B):
     return d_step, g_step
 
 
+def gan_bytes(N, S, H, E, Z, B):
+    """Algorithmic HBM bytes of one discriminator and one generator iteration: the streams of size
+    S*N (the slate axis: the 2H x S*N layer-1 weight W1S of D, the S*N x H heads WH of G, the B x S*N
+    fake slates and their gradient), each read or written once per use; everything else (the small
+    layers, histories, the real slates' sparse columns) is < 1 % and not counted.
+      D iteration (CGANs.py:410-457): G(z) reads WH and writes the fake slates; D(fake) reads them
+      and W1S; layer 1's dW (fused with RMSprop) reads them again and moves W1S and its square
+      average v in and out (4 x W1S).
+      G iteration (CGANs.py:370-408): G(z) reads WH, writes the fake slates; D(fake) reads them and
+      W1S; D's backward to the slates reads W1S and writes dfake; the heads' dW (fused with RMSprop)
+      reads dfake and moves WH and v in and out (4 x WH); the eval inference reads WH again."""
+    f = 4
+    w1s, wh, fake = 2 * H * S * N * f, S * N * H * f, B * S * N * f
+    d_it = wh + fake + (fake + w1s) + (fake + 4 * w1s)
+    g_it = (wh + fake) + (fake + w1s) + (w1s + fake) + (fake + 4 * wh) + wh
+    return d_it, g_it
+
+
 def gan_cpu_baseline(g_sd, d_sd, np_batches, N, S, H, E, Z, budget_s):
     """The oracle's cGAN iterations (oracle/gan.py, float64 NumPy, the reference's
     CGANs.py:370-457 restated) at the bench's full size: D iterations with a G iteration
@@ -467,6 +485,12 @@ def bench_gan(args):
     fd, fg = gan_flops(N, S, H, E, Z, B)
     flops = steps * fd + steps // 5 * fg
     ach = flops / (ms_ev * 1e-3) / 1e12
+    # both legs of the roofline: the iteration moves ~1.4 GB of weight / optimizer-state / slate
+    # streams besides its FLOPs; frac = max(flop time at peak, byte time at peak) / measured
+    bd, bg = gan_bytes(N, S, H, E, Z, B)
+    nbytes = steps * bd + steps // 5 * bg
+    t_meas = ms_ev * 1e-3
+    t_flop, t_byte = flops / (HIDDEN_FP32_MFMA_TFLOPS * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)
     out = {"metric": "train slates/sec, cGAN slate_size=5 gan_hidden_layer=256 MovieLens-20M (config 4)",
            "value": steps * B / el, "unit": "slates/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
            "ms_per_step": el / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -474,11 +498,19 @@ def bench_gan(args):
            "config": {"workload": f"cGAN G hidden [{H // 2}, {H}], D hidden [{2 * H}, {H}, {H // 2}], S={S}, E={E}, "
                                   f"z=100, batch {B}, RMSprop lr 1e-3, n_critic 5 (1 D iteration per step, 1 G "
                                   f"iteration per 5 steps)", "global_batch": B, "parallelism": "dp1"},
-           "roofline": {"bound": "mfma", "kernel": "whole D/G iterations (gemm_kernel + small kernels)",
+           "roofline": {"bound": "mfma" if t_flop >= t_byte else "hbm",
+                        "kernel": "whole D/G iterations (gemm_kernel + small kernels)",
                         "achieved": ach, "peak": HIDDEN_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                        "frac": ach / HIDDEN_FP32_MFMA_TFLOPS, "traffic": None,
+                        "frac": max(t_flop, t_byte) / t_meas, "traffic": None,
                         "algorithmic_flops_per_step": flops / steps, "d_iter_gflop": fd / 1e9,
-                        "g_iter_gflop": fg / 1e9},
+                        "g_iter_gflop": fg / 1e9,
+                        "legs": {"mfma": {"time_at_peak_us_per_step": t_flop / steps * 1e6,
+                                          "frac": ach / HIDDEN_FP32_MFMA_TFLOPS},
+                                 "hbm": {"algorithmic_bytes_per_step": nbytes / steps, "d_iter_MB": bd / 1e6,
+                                         "g_iter_MB": bg / 1e6, "achieved_GBs": nbytes / t_meas / 1e9,
+                                         "peak_GBs": HBM_PEAK_GBS, "time_at_peak_us_per_step": t_byte / steps * 1e6,
+                                         "frac": nbytes / t_meas / 1e9 / HBM_PEAK_GBS}},
+                        "frac_rule": "max(flop time at the fp32 MFMA peak, byte time at the HBM peak) / measured"},
            "cpu_baseline": None,
            "final": [float(x) for x in eng.d_step(batches[0]).cpu()]}
     if not args.no_cpu_baseline:

@@ -17,8 +17,39 @@ reference's NCF training step:
 Dropout masks are inputs (the reference draws them from torch's CPU generator;
 tests/golden records them with forward hooks), scaled by 1 / (1 - 0.5) = 2.
 Pinned by tests/golden/mlp_*.npz and neumf_*.npz (made by importing the reference).
+
+Samples of the fp32 rounding noise (tests/parity_report.py's elementwise band): ``order_seed``
+runs a step with the examples, the input features and every hidden layer's units in seeded
+orders (every batch sum and every product's inner sum re-ordered, forward and backward);
+``kink_flip`` decides every LeakyReLU (mlp.py:36, neuMF.py:48) whose pre-activation lies within
+fp32 rounding of the kink the other way from its exact value -- the activation decision a
+different fp32 order of the forward dot product can take (see ``kink_band``).
 """
+import math
+
 import torch
+
+U32 = 2.0 ** -24          # fp32 unit roundoff
+
+
+def kink_band(a, W, b, c):
+    """The exact (float64) pre-activations z of a @ W.T + b and the rounding band c * u *
+    sqrt(K + 1) * S around them (S = |a| @ |W|.T + |b|, K inputs): the typical size of an fp32
+    dot product's rounding error in some summation order is u * sqrt(K) * S, so a z inside the
+    band is a decision on which fp32 orders of the same sum disagree."""
+    a64, W64, b64 = a.double(), W.double(), b.double()
+    z64 = a64.mm(W64.t()) + b64
+    S = a64.abs().mm(W64.abs().t()) + b64.abs()
+    return z64, c * U32 * math.sqrt(W.shape[1] + 1) * S
+
+
+def _decide(z, a, W, b, flip):
+    """The LeakyReLU branch (True: z > 0 side) and the number of flipped decisions."""
+    if flip is None:
+        return z > 0, None
+    z64, band = kink_band(a, W, b, flip)
+    amb = z64.abs() <= band
+    return torch.where(amb, z64 <= 0, z > 0), amb
 
 from . import mf as omf
 from . import rng as orng
@@ -50,22 +81,34 @@ class MLPParams:
         return [(self.t[k], self.t[k + 1]) for k in range(2, len(self.t), 2)]
 
 
-def forward(P, u, i, masks, xperm=None):
+def _tower(lin, x, masks, cache, flip):
+    """Hidden layers: Linear -> LeakyReLU(0.1) -> Dropout(0.5) (mlp.py:30-41, neuMF.py:43-49)."""
+    a = x
+    for k, (W, b) in enumerate(lin):
+        z = a.mm(W.t()) + b
+        pos, amb = _decide(z, a, W, b, flip)
+        r = torch.where(pos, z, z * LRELU)
+        keep = masks[k].to(z.dtype)
+        a = r * (keep * DROP_SCALE)
+        cache["z"].append(z)
+        cache["pos"].append(pos)
+        cache["a"].append(a)
+        if amb is not None:   # flipped decisions that reach the loss (dropout keeps the unit)
+            cache["flips"] += int((amb & (keep > 0)).sum())
+    return a
+
+
+def forward(P, u, i, masks, xperm=None, flip=None):
     """Returns p (N,1) and the cache for backward.  ``masks``: per hidden layer (N, out) 0/1.
-    ``xperm``: the input features in that order (P's first layer permuted to match)."""
+    ``xperm``: the input features in that order (P's first layer permuted to match).
+    ``flip``: kink_flip's c (None: every branch by the sign of the fp32 pre-activation)."""
     Ue, Ie = P.emb()
     x = torch.cat([Ue[u], Ie[i]], dim=-1)
     if xperm is not None:
         x = x[:, xperm]
     lin = P.linears()
-    cache = {"x": x, "z": [], "a": [x]}
-    a = x
-    for k, (W, b) in enumerate(lin[:-1]):
-        z = a.mm(W.t()) + b
-        r = torch.where(z > 0, z, z * LRELU)
-        a = r * (masks[k].to(z.dtype) * DROP_SCALE)
-        cache["z"].append(z)
-        cache["a"].append(a)
+    cache = {"x": x, "z": [], "pos": [], "a": [x], "flips": 0}
+    a = _tower(lin[:-1], x, masks, cache, flip)
     W, b = lin[-1]
     logit = a.mm(W.t()) + b
     p = torch.sigmoid(logit)
@@ -89,7 +132,7 @@ def backward(P, u, i, masks, cache, dp, xperm=None):
         if k > 0:
             z = cache["z"][k - 1]
             da = da * (masks[k - 1].to(z.dtype) * DROP_SCALE)
-            dz = torch.where(z > 0, da, da * LRELU)
+            dz = torch.where(cache["pos"][k - 1], da, da * LRELU)
         else:
             dx = da
     grads_lin.reverse()
@@ -108,8 +151,10 @@ def backward(P, u, i, masks, cache, dp, xperm=None):
 class NCFOracle:
     """One run_train_iteration (implicit.py:347-364) of the NCF MLP per ``step``."""
 
+    N_EMB = 2                     # embedding tables before the Linears in parameter order
+
     def __init__(self, tensors, names, pool_u, pool_i, mt_state, loss="pointwise", lr=1e-2, weight_decay=1e-5,
-                 n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None):
+                 n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None, kink_flip=None):
         self.P = MLPParams(tensors, names)
         # order_seed (pointwise, test infrastructure): run the step over the examples, the input
         # features and every hidden layer's units in seeded orders -- the same arithmetic summed
@@ -117,6 +162,11 @@ class NCFOracle:
         # the rounding noise for tests/parity_report.py's elementwise band
         assert order_seed is None or loss == "pointwise"
         self.order = None if order_seed is None else torch.Generator().manual_seed(order_seed)
+        # kink_flip (test infrastructure): c of kink_band -- every LeakyReLU decision within
+        # rounding of the kink goes the other way from the exact sign of this run's own state; the
+        # count of such decisions that reach the loss, per step, in self.flips
+        self.kink_flip = kink_flip
+        self.flips = []
         self.loss_kind = loss
         self.n, self.batch_size = n_neg, batch_size
         self.opt_lr, self.opt_wd, self.opt_betas = lr, weight_decay, betas
@@ -139,31 +189,40 @@ class NCFOracle:
     def _unit_orders(self):
         """order_seed: the input features and every hidden layer's units in a seeded order (the
         same function; every product sums over its inner dimension in another order).  Returns
-        (P', masks -> masks', grads' -> grads, xperm); identity without order_seed."""
+        (P', masks -> masks', grads' -> grads, xperm); identity without order_seed.  The output
+        Linear's inputs past the tower's last hidden layer (NeuMF's GMF products) keep their
+        order."""
         if self.order is None:
             return self.P, (lambda m: m), (lambda g: g), None
+        ne = self.N_EMB
         lin = self.P.linears()
         E2 = lin[0][0].shape[1]
         xperm = torch.randperm(E2, generator=self.order)
         hperm = [torch.randperm(W.shape[0], generator=self.order) for W, _ in lin[:-1]]
         ins = [xperm] + hperm                                 # input order of linear k
-        t = list(self.P.t[:2])
+        Wo = lin[-1][0]
+        if Wo.shape[1] > len(ins[-1]):
+            ins[-1] = torch.cat([ins[-1], torch.arange(len(ins[-1]), Wo.shape[1])])
+        t = list(self.P.t[:ne])
         for k, (W, b) in enumerate(lin):
             rows = hperm[k] if k < len(hperm) else torch.arange(W.shape[0])
             t += [W[rows][:, ins[k]], b[rows]]
-        Pp = MLPParams(t, self.P.names)
+        Pp = type(self.P)(t, self.P.names)
 
         def masks_p(ms):
             return [m[:, hperm[k]] for k, m in enumerate(ms)]
 
         def grads_back(g):
-            out = list(g[:2])
+            out = list(g[:ne])
             for k in range(len(lin)):
-                dW, db = g[2 + 2 * k], g[3 + 2 * k]
+                dW, db = g[ne + 2 * k], g[ne + 1 + 2 * k]
                 rows = torch.argsort(hperm[k]) if k < len(hperm) else torch.arange(dW.shape[0])
                 out += [dW[rows][:, torch.argsort(ins[k])], db[rows]]
             return out
         return Pp, masks_p, grads_back, xperm
+
+    _fwd = staticmethod(forward)
+    _bwd = staticmethod(backward)
 
     def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
         u = torch.as_tensor(pos_u).long()
@@ -171,15 +230,16 @@ class NCFOracle:
         u, i, masks_pos = self._permuted(u, i, masks_pos)
         P, mperm, gback, xperm = self._unit_orders()
         masks_pos = mperm(masks_pos)
-        p_pos, c_pos = forward(P, u, i, masks_pos, xperm)
+        p_pos, c_pos = self._fwd(P, u, i, masks_pos, xperm, self.kink_flip)
         idx, nu, ni = self.draw(self.n * self.batch_size)
         nu, ni, masks_neg = self._permuted(nu, ni, masks_neg)
         masks_neg = mperm(masks_neg)
-        p_neg, c_neg = forward(P, nu, ni, masks_neg, xperm)
+        p_neg, c_neg = self._fwd(P, nu, ni, masks_neg, xperm, self.kink_flip)
+        self.flips.append(c_pos["flips"] + c_neg["flips"])
         kind = self.loss_kind
         loss, dpp, dpn = omf.loss_and_dp(kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n, self.batch_size)
-        g1 = backward(P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1), xperm)
-        g2 = backward(P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1), xperm)
+        g1 = self._bwd(P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1), xperm)
+        g2 = self._bwd(P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1), xperm)
         grads = gback([a + b for a, b in zip(g1, g2)])
         self.opt.step(self.P.t, grads)
         if return_all:
@@ -201,21 +261,17 @@ class NeuMFParams(MLPParams):
         return [(self.t[k], self.t[k + 1]) for k in range(4, len(self.t), 2)]
 
 
-def neumf_forward(P, u, i, masks):
+def neumf_forward(P, u, i, masks, xperm=None, flip=None):
     """neuMF.py:34-55: tower over cat(U_mlp[u], I_mlp[i]), GMF = U_mf[u] * I_mf[i],
-    sigmoid(affine_output(cat(tower, GMF)))."""
+    sigmoid(affine_output(cat(tower, GMF))).  ``xperm`` / ``flip`` as forward's."""
     Ue, Ie = P.emb()
     Um, Im = P.emb_mf()
     x = torch.cat([Ue[u], Ie[i]], dim=-1)
+    if xperm is not None:
+        x = x[:, xperm]
     lin = P.linears()
-    cache = {"z": [], "a": [x]}
-    a = x
-    for k, (W, b) in enumerate(lin[:-1]):
-        z = a.mm(W.t()) + b
-        r = torch.where(z > 0, z, z * LRELU)
-        a = r * (masks[k].to(z.dtype) * DROP_SCALE)
-        cache["z"].append(z)
-        cache["a"].append(a)
+    cache = {"z": [], "pos": [], "a": [x], "flips": 0}
+    a = _tower(lin[:-1], x, masks, cache, flip)
     gmf = Um[u] * Im[i]
     v = torch.cat([a, gmf], dim=-1)
     W, b = lin[-1]
@@ -224,7 +280,7 @@ def neumf_forward(P, u, i, masks):
     return p, cache
 
 
-def neumf_backward(P, u, i, masks, cache, dp):
+def neumf_backward(P, u, i, masks, cache, dp, xperm=None):
     """Dense grads in parameter order (the reference's autograd, restated)."""
     p = cache["p"]
     dz = dp * (1 - p) * p
@@ -241,13 +297,15 @@ def neumf_backward(P, u, i, masks, cache, dp):
         Wk, bk = lin[k]
         z = cache["z"][k]
         da = da * (masks[k].to(z.dtype) * DROP_SCALE)
-        dzk = torch.where(z > 0, da, da * LRELU)
+        dzk = torch.where(cache["pos"][k], da, da * LRELU)
         grads_lin.append((dzk.t().mm(cache["a"][k]), dzk.sum(0)))
         da = dzk.mm(Wk)
     grads_lin.reverse()
     Ue, Ie = P.emb()
     Um, Im = P.emb_mf()
     E = Ue.shape[1]
+    if xperm is not None:
+        da = da[:, torch.argsort(xperm)]
     out = [torch.zeros_like(Ue).index_add_(0, u, da[:, :E]), torch.zeros_like(Ie).index_add_(0, i, da[:, E:]),
            torch.zeros_like(Um).index_add_(0, u, dUm_rows), torch.zeros_like(Im).index_add_(0, i, dIm_rows)]
     for dW, db in grads_lin:
@@ -258,25 +316,11 @@ def neumf_backward(P, u, i, masks, cache, dp):
 class NeuMFOracle(NCFOracle):
     """One run_train_iteration (implicit.py:347-364) of NeuMF per ``step``."""
 
+    N_EMB = 4
+    _fwd = staticmethod(neumf_forward)
+    _bwd = staticmethod(neumf_backward)
+
     def __init__(self, tensors, names, *a, **k):
         super().__init__(tensors, names, *a, **k)
         self.P = NeuMFParams(tensors, names)
         self.opt = omf.Optim("adam", self.P.t, self.opt_lr, self.opt_wd, betas=self.opt_betas)
-
-    def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
-        u = torch.as_tensor(pos_u).long()
-        i = torch.as_tensor(pos_i).long()
-        u, i, masks_pos = self._permuted(u, i, masks_pos)
-        p_pos, c_pos = neumf_forward(self.P, u, i, masks_pos)
-        idx, nu, ni = self.draw(self.n * self.batch_size)
-        nu, ni, masks_neg = self._permuted(nu, ni, masks_neg)
-        p_neg, c_neg = neumf_forward(self.P, nu, ni, masks_neg)
-        loss, dpp, dpn = omf.loss_and_dp(self.loss_kind, p_pos.reshape(-1), p_neg.reshape(-1), self.n,
-                                         self.batch_size)
-        g1 = neumf_backward(self.P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1))
-        g2 = neumf_backward(self.P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1))
-        grads = [a + b for a, b in zip(g1, g2)]
-        self.opt.step(self.P.t, grads)
-        if return_all:
-            return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx, neg_u=nu, neg_i=ni, grads=grads)
-        return float(loss)

@@ -64,14 +64,20 @@ struct Comm {
     std::thread watchdog;
     std::atomic<bool> stop{false};
     std::mutex mu;
-    // recorded after EVERY collective (re-recorded while still pending, so it always covers the
-    // newest one); track_t0 = when the oldest collective not yet seen complete was enqueued, so any
-    // collective that stalls -- the first of a run included -- reaches the deadline even when the
-    // host then blocks on a sync and enqueues nothing more
-    hipEvent_t ev_track = nullptr;
-    std::chrono::steady_clock::time_point track_t0;
-    bool tracking = false;
-    int64_t ncoll = 0, track_first = 0;
+    // completion tracking of every collective (RCCL ones on either communicator): a FIFO of
+    // (event recorded after the collective, enqueue time, collective number) in a ring of kTrack
+    // events.  Completed entries are popped from the head (by the watchdog and at every enqueue);
+    // the deadline applies to the head's age -- the oldest collective not yet complete -- so a
+    // stalled collective reaches it even when the host then blocks on a sync and enqueues
+    // nothing more, and a healthy run whose host stays ahead of the GPU never does (each entry
+    // completes in turn).  A full ring folds newer collectives into its newest entry (re-recorded,
+    // keeping its older time): the host is then kTrack collectives ahead, so the head is old.
+    static constexpr int kTrack = 64;
+    hipEvent_t ev_ring[kTrack] = {};
+    std::chrono::steady_clock::time_point t0_ring[kTrack];
+    int64_t id_ring[kTrack] = {};
+    int track_head = 0, track_size = 0;
+    int64_t ncoll = 0;
     double timeout_s = 600.0;
 };
 
@@ -93,8 +99,17 @@ static double env_seconds(const char *name, double dflt) {
     fprintf(stderr, "[librg_hip] rank %d of %d: %s; aborting the RCCL communicator and exiting\n", c->rank, c->world,
             why.c_str());
     fflush(stderr);
+    if (c->comm_words) ncclCommAbort(c->comm_words);
     if (c->comm) ncclCommAbort(c->comm);
     std::_Exit(3);
+}
+
+// pop the completed collectives off the head of the tracking FIFO (c->mu held)
+static void track_pop_done(Comm *c) {
+    while (c->track_size > 0 && hipEventQuery(c->ev_ring[c->track_head]) == hipSuccess) {
+        c->track_head = (c->track_head + 1) % Comm::kTrack;
+        --c->track_size;
+    }
 }
 
 static void watchdog_loop(Comm *c) {
@@ -108,14 +123,32 @@ static void watchdog_loop(Comm *c) {
             ae != ncclInProgress)
             comm_die(c, std::string("RCCL asynchronous error (word all-gather): ") + ncclGetErrorString(ae));
         std::lock_guard<std::mutex> g(c->mu);
-        if (!c->tracking) continue;
-        if (hipEventQuery(c->ev_track) == hipSuccess) { c->tracking = false; continue; }
-        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->track_t0).count();
+        track_pop_done(c);
+        if (c->track_size == 0) continue;
+        const double waited =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - c->t0_ring[c->track_head]).count();
         if (waited > c->timeout_s)
-            comm_die(c, "collective #" + std::to_string(c->track_first) + " (of " + std::to_string(c->ncoll) +
-                            " enqueued) not complete after " + std::to_string((int)waited) +
+            comm_die(c, "collective #" + std::to_string(c->id_ring[c->track_head]) + " (of " +
+                            std::to_string(c->ncoll) + " enqueued) not complete after " + std::to_string((int)waited) +
                             " s (RG_COMM_TIMEOUT_S; a peer rank failed or diverged)");
     }
+}
+
+// arm the watchdog on the completion of the collective just enqueued on `stream`
+static void track(Comm *c, hipStream_t stream) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ++c->ncoll;
+    if (!c->ev_ring[0]) return;            // stand-ins: no watchdog
+    track_pop_done(c);
+    if (c->track_size == Comm::kTrack) {   // full: fold into the newest entry (keeps its time)
+        (void)hipEventRecord(c->ev_ring[(c->track_head + c->track_size - 1) % Comm::kTrack], stream);
+        return;
+    }
+    const int k = (c->track_head + c->track_size) % Comm::kTrack;
+    if (hipEventRecord(c->ev_ring[k], stream) != hipSuccess) return;
+    c->t0_ring[k] = std::chrono::steady_clock::now();
+    c->id_ring[k] = c->ncoll;
+    ++c->track_size;
 }
 
 // after an RCCL call on `stream`: wait out ncclInProgress (non-blocking communicator) within
@@ -133,14 +166,7 @@ static int nccl_after(Comm *c, hipStream_t stream, ncclResult_t r, const char *w
         set_error(std::string(what) + ": " + ncclGetErrorString(r));
         return RG_E_LAUNCH;
     }
-    std::lock_guard<std::mutex> g(c->mu);
-    ++c->ncoll;
-    if (c->tracking && hipEventQuery(c->ev_track) == hipSuccess) c->tracking = false;   // caught up
-    if (c->ev_track && hipEventRecord(c->ev_track, stream) == hipSuccess && !c->tracking) {
-        c->tracking = true;                 // pending already: keep the older start time
-        c->track_t0 = std::chrono::steady_clock::now();
-        c->track_first = c->ncoll;
-    }
+    track(c, stream);
     return RG_OK;
 }
 
@@ -336,7 +362,9 @@ int comm_words_allgather(void *h, hipStream_t stream, uint32_t *words, int64_t u
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess && r != ncclInProgress) return nccl_fail("ncclAllGather (words)", r);
     r = nccl_settle(c, c->comm_words, r2, "ncclAllGather (words)");
-    return r == ncclSuccess ? RG_OK : nccl_fail("ncclAllGather (words, group)", r);
+    if (r != ncclSuccess) return nccl_fail("ncclAllGather (words, group)", r);
+    track(c, stream);                      // under the same deadline as the step's collectives
+    return RG_OK;
 }
 
 }  // namespace rg
@@ -389,7 +417,7 @@ extern "C" void *rg_comm_create(const uint8_t *id, int32_t world, int32_t rank, 
         delete c;
         return nullptr;
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_track, evf);
+    for (int k = 0; k < rg::Comm::kTrack && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->ev_ring[k], evf);
     if (e != hipSuccess) {
         rg::hip_fail("rg_comm_create", e);
         rg_comm_destroy(c);
@@ -479,7 +507,8 @@ extern "C" int rg_comm_destroy(void *h) {
     c->stop = true;
     if (c->watchdog.joinable()) c->watchdog.join();
     if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->ev_track) hipEventDestroy(c->ev_track);
+    for (int k = 0; k < rg::Comm::kTrack; ++k)
+        if (c->ev_ring[k]) hipEventDestroy(c->ev_ring[k]);
     if (c->scratch) hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->comm_words) ncclCommDestroy(c->comm_words);

@@ -2241,7 +2241,11 @@ extern "C" int rg_mf_prepare_marked(void *stream, const rg_mf_batch_t *b, const 
     int rc = prepare_args(b, w, mark, a);
     if (rc) return rc;
     const int64_t total = prepare_threads(b->cols, b->n_neg);
+#if RG_AB
     static const int prio = [] { const char *e = getenv("RG_PREP_PRIO"); return e ? atoi(e) : 1; }();
+#else
+    constexpr int prio = 1;
+#endif
     hipLaunchKernelGGL(mf_prepare_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        (hipStream_t)stream, a, reinterpret_cast<int2 *>(b->pairs), prio);
     return check_launch("rg_mf_prepare");

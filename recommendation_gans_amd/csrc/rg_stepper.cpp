@@ -54,11 +54,6 @@
 #define RG_PIPE_DEFAULT 0
 #endif
 
-#ifdef RG_X_PIPE2
-extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
-                          int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w);
-static int64_t g_x_paired = -1;   // timing prototype: the unit whose pair pass ran in the last launch
-#endif
 #ifndef RG_OWNER_USER_AFTER_DEFAULT
 #define RG_OWNER_USER_AFTER_DEFAULT 0
 #endif
@@ -72,6 +67,7 @@ constexpr int kAheadSlots = 2;   // slots generated ahead of the one being consu
 
 struct Stepper {
     rg_mf_stepper_config_t cfg;
+    bool failed = false;          // a step stopped half applied (pipe2's cold launch refused): unusable
     hipStream_t gen = nullptr, prep = nullptr;
     int64_t W = 0;                        // words per unit
     int64_t G = 1;                        // units per ring slot
@@ -629,15 +625,9 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
         nw = train_work(st, *next, unit + 1);
         if ((rc = rg_mf_pairs_prepare(s, tb, &batch, &w, &nbatch, &nw, nullptr, 0))) return rc;
     }
-#ifdef RG_X_PIPE2
-    else if (g_x_paired != unit && (rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
-        return rc;
-    }
-#elif !defined(RG_X_NOPAIR)   // timing experiments only (wrong results): the split step without its pair pass
     else if ((rc = rg_mf_pairs(s, tb, &batch, &w, 1))) {
         return rc;
     }
-#endif
     if ((rc = release(st, s))) return rc;
     if (next && !pip) {
         if (!st.inline_gen && (rc = keep_ahead(st, unit + 1))) return rc;
@@ -668,29 +658,11 @@ int train_split(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
             return rc;
     }
     rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // timed by the dispatch itself
-#ifdef RG_X_PIPE2
-    // timing prototype (wrong results): launch A = the last H users + every item (+ next prepare,
-    // walk, loss); launch B = the NEXT step's pair pass beside the dense update of users [0, U - H)
-    static const int64_t xh = [] { const char *e = getenv("RG_X_H"); return e ? atoll(e) : 36000LL; }();
-    const int64_t hb = next && !st.cfg.item_grad ? (U > xh ? U - xh : 0) : 0;
-    rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, hb, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
-                                 next && !pip ? &nbatch : nullptr, next && !pip ? &nw : nullptr,
-                                 gen_slot >= 0 ? &gen : nullptr);
-    rg::launch_events() = rg::LaunchEvents{};
-    if (rc) return rc;
-    g_x_paired = -1;
-    if (hb > 0) {
-        rg_mf_batch_t nb2 = nbatch;
-        if ((rc = rg_x_pipe2(s, tb, &w, &o, 0, hb, &nb2, &nw))) return rc;
-        g_x_paired = unit + 1;
-    }
-#else
     rc = rg_mf_apply_prepare_gen(s, tb, &w, &o, 0, st.cfg.item_grad ? U : R, st.cfg.item_grad ? nullptr : &l,
                                  next && !pip ? &nbatch : nullptr, next && !pip ? &nw : nullptr,
                                  gen_slot >= 0 ? &gen : nullptr);
     rg::launch_events() = rg::LaunchEvents{};
     if (rc) return rc;
-#endif
     if (gen_slot >= 0) end_production(st, s, gen_slot);
     if (st.cfg.item_grad) {
         if (st.cfg.comm && (rc = rg::comm_end(st.cfg.comm, s))) return rc;
@@ -962,14 +934,20 @@ int train_pipe2(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     }
     const int64_t hot_cap = std::min<int64_t>(U, (int64_t)(1 + st.cfg.n_neg) * st.cfg.cols);
     if ((rc = rg_mf_pipe2_hot(s, tb, &w, &o, &l, st.hot[u1 % 3], nhot + u1 % 3, hot_cap,
-                              next2 ? nhot + u2 % 3 : nullptr, nullptr)))
+                              next2 ? nhot + u2 % 3 : nullptr, nullptr))) {
+        st.cfg.step -= 1;                          // nothing of this step ran
         return rc;
+    }
     rg::launch_events() = rg::LaunchEvents{(hipEvent_t)ev0, (hipEvent_t)ev1};   // the cold launch
     rc = rg_mf_pipe2_cold(s, tb, &w, &o, &b1, &w1, st.pcounts[u1 % 3], next2 ? &b2 : nullptr,
                           next2 ? &w2 : nullptr, next2 ? st.hot[u2 % 3] : nullptr, next2 ? nhot + u2 % 3 : nullptr,
                           gen_slot >= 0 ? &gen : nullptr);
     rg::launch_events() = rg::LaunchEvents{};
-    if (rc) return rc;
+    if (rc) {
+        // the hot launch updated part of the rows: the step is half applied and cannot be resumed
+        st.failed = true;
+        return rc;
+    }
     if (gen_slot >= 0) end_production(st, s, gen_slot);
     st.pdirty[unit % 3] = false;                 // the two launches consumed and reset its claims
     st.pair_dirty[unit % 2] = false;             // and its overflow accumulators
@@ -1341,7 +1319,7 @@ int train_owner(Stepper &st, hipStream_t s, const rg_mf_step_in_t &cur, const rg
     // pull then has the GPU alone), 2 the item exchange's enqueue -- measured, emulated rank 0 of
     // 8: 74.0-74.7 / 85.5-85.7 / 88.6-92.0 us per step (profiles/r5/owner/emul_order_r5x.txt).
     // It is enqueued as soon as that point is: behind the host's later launches it starts late
-    static const int after = [] { const char *v = getenv("RG_OWNER_USER_AFTER"); return v ? atoi(v) : RG_OWNER_USER_AFTER_DEFAULT; }();
+    static const int after = ab_int("RG_OWNER_USER_AFTER", RG_OWNER_USER_AFTER_DEFAULT);
     const rg_opt_t o = opt_at(st, st.cfg.step + 1);
     auto start_users = [&]() -> int {
         if (!side) return RG_OK;
@@ -1633,7 +1611,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     // two-launch pipelined step (rg_mf_pipe2_hot / _cold) for the single-rank losses with claimed
     // slots: RG_PIPE2=1 selects it, RG_PIPE2_DEFAULT the build's default (0: the split step, which
     // measures faster -- DESIGN §4.1)
-    st->pipe2 = !st->pipe && env_flag("RG_PIPE2", RG_PIPE2_DEFAULT != 0) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
+    st->pipe2 = !st->pipe && ab_flag("RG_PIPE2", RG_PIPE2_DEFAULT != 0) && st->claim && cfg->dp_mode == 0 && !st->prep_in_pairs &&
                 (cfg->loss == RG_LOSS_POINTWISE || cfg->loss == RG_LOSS_BPR || cfg->loss == RG_LOSS_HINGE) &&
                 cfg->work.part_row && cfg->work.part_bias && cfg->work.loss_partials && cfg->n_partials > 0;
     if (st->pipe || st->pipe2) {
@@ -1666,7 +1644,7 @@ extern "C" void *rg_mf_stepper_create(const rg_mf_stepper_config_t *cfg) {
     // stream of a multi-rank step: R times the words of one GPU's step
     if (cfg->dp_mode == 2 && cfg->comm && cfg->world > 1 && st->W % cfg->world == 0 && !st->inline_gen &&
         st->G < rg::kMtMaxTail &&
-        env_flag("RG_OWNER_MT_SLICE", false)) {
+        ab_flag("RG_OWNER_MT_SLICE", false)) {
         // each rank walks its slice of the global draw (see Stepper::slice); falls back to the
         // jump-ahead walk of the whole draw when a slice is shorter than a jump's stream window
         st->L = st->W / cfg->world;
@@ -1715,6 +1693,7 @@ extern "C" int rg_mf_stepper_train(void *h, void *stream, const rg_mf_step_in_t 
                                    float *loss_out, void *ev_apply_begin, void *ev_apply_end) {
     Stepper *st = static_cast<Stepper *>(h);
     if (!st || !cur) return rg::fail_arg("rg_mf_stepper_train: null handle/input");
+    if (st->failed) return rg::fail_arg("rg_mf_stepper_train: an earlier step stopped half applied; rebuild the stepper");
     hipStream_t s = (hipStream_t)stream;
     if (st->cfg.dp_mode == 1) {
         if (!st->cfg.comm) return rg::fail_arg("rg_mf_stepper_train: replicated DP step needs a communicator "

@@ -231,12 +231,12 @@ class MFEngine:
             self.shard_users = -(-self.U // self.world)
             self.shard_items = -(-self.I // self.world)
             rows = (self.shard_users * self.world, self.shard_items * self.world)
-        elif dp == "owner" and comm is not None and self.world > 1 and \
+        elif dp == "owner" and comm is not None and self.world > 1 and _lib.ab_build() and \
                 os.environ.get("RG_OWNER_ITEM_SHARD", "0") == "1":
             # the owner step's sharded item update (reduce-scatter -> this rank's 1/R of the items'
-            # optimizer update -> all-gather): item tables allocated with world * shard rows.  Opt-in:
-            # with local-copy exchanges rank 0 of 8 measured 84.9 us against 79.4 for the all-reduce
-            # and the full item update
+            # optimizer update -> all-gather): item tables allocated with world * shard rows.  A/B
+            # build only: with local-copy exchanges rank 0 of 8 measured 81.0 us against 74.6 for
+            # the all-reduce and the full item update
             self.shard_users, self.shard_items = 0, -(-self.I // self.world)
             rows = (self.U, self.shard_items * self.world)
         else:
@@ -747,5 +747,10 @@ class MFEngine:
               "rg_mf_stepper_sync_mt")
 
     def optimizer_state(self):
+        if self.dp == "owner" and self.shard_items:
+            # each rank updates (and holds current moments for) only its shard of the item rows;
+            # the other rows' m / v are stale, so a checkpoint from them would be wrong
+            raise NotImplementedError("optimizer_state: the sharded item update (RG_OWNER_ITEM_SHARD, A/B build) "
+                                      "keeps each rank's item moments only for its own shard")
         self.flush()
         return {"step": self.t, "m": self.m, "v": self.v}

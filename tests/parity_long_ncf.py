@@ -2,7 +2,8 @@
 B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5) run longer than the test suite does
 (tests/test_configs_gpu.py::test_ncf_full_size_steps runs 10): S native steps (default 20) with
 item plans and recorded dropout masks against oracle/ncf.py in fp32, fp64 and two more fp32
-restatements summing in other orders.  Every step: the loss within 1e-5 relative and the MT
+restatements summing in other orders, and one deciding every LeakyReLU within fp32 rounding of
+its kink the other way (oracle/ncf.py kink_flip).  Every step: the loss within 1e-5 relative and the MT
 state bit-exact (exit status 1 otherwise); at the checked steps every parameter through
 tests/parity_report.check, one JSON line per step.
 
@@ -64,8 +65,9 @@ def main():
     Oracle = oncf.NeuMFOracle if args.neumf else oncf.NCFOracle
     o32 = Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
     o64 = Oracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o32b = [Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k, **kw)
-            for k in (1, 2)]
+    o32b = ([Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k, **kw)
+             for k in (1, 2)] +
+            [Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), kink_flip=4.0, **kw)])
     widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
     rs = np.random.RandomState(6 if args.neumf else 5)
     tag = "NeuMF" if args.neumf else "C3 ncf"
@@ -89,7 +91,8 @@ def main():
         worst = max(worst, rel)
         mt_ok = bool((e.mt_state() == o32.state).all())
         bad += int(rel > 1e-5 or not mt_ok)
-        line = {"step": s, "loss_gpu": got, "loss_ref32": l32, "loss_rel": rel, "mt_exact": mt_ok}
+        line = {"step": s, "loss_gpu": got, "loss_ref32": l32, "loss_rel": rel, "mt_exact": mt_ok,
+                "kink_flips": o32b[-1].flips[-1]}
         for tr in filter(None, args.track.split(",")):
             pname, prow = tr.rsplit(":", 1)
             k = names.index(pname)

@@ -56,3 +56,45 @@ def test_stalled_collective_exits_with_status_3(tmp_path):
     assert "rank 0 of 2" in err, err[-2000:]
     assert "rank 0 returned" not in out
     assert time.time() - t0 < 85
+
+
+AHEAD_SCRIPT = r"""
+import os, sys, time
+import torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from recommendation_gans_amd.comm import RcclComm
+torch.cuda.set_device(0)
+dist.init_process_group("gloo", rank=0, world_size=1)
+comm = RcclComm(torch.device("cuda", 0))
+x = torch.ones(4 << 20, device="cuda")
+buf = torch.ones(1 << 10, device="cuda")
+evs, t0, n = [], time.time(), 0
+while time.time() - t0 < 4 * float(os.environ["RG_COMM_TIMEOUT_S"]):
+    for _ in range(4):
+        x.mul_(1.0000001)
+    comm.allreduce_(buf)
+    e = torch.cuda.Event()
+    e.record()
+    evs.append(e)
+    if len(evs) > 50:          # the host stays 50 iterations ahead of the GPU, never syncing it
+        evs.pop(0).synchronize()
+    n += 1
+torch.cuda.synchronize()
+print("host-ahead run finished", n, flush=True)
+"""
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_host_ahead_run_is_not_killed(tmp_path):
+    """a healthy run whose host stays ahead of the GPU (enqueueing collectives, never
+    waiting for the newest one) must not reach the deadline -- the watchdog times the OLDEST
+    collective not yet complete (a FIFO of events), not the newest one's re-recorded event.  One
+    rank (an RCCL communicator of one: rg_comm_allreduce_sum_f32 still launches ncclAllReduce)
+    for four deadlines' time with RG_COMM_TIMEOUT_S = 2."""
+    script = tmp_path / "ahead.py"
+    script.write_text(AHEAD_SCRIPT)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29733", RG_COMM_TIMEOUT_S="2",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, str(script), ROOT], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, (p.returncode, p.stdout, p.stderr[-2000:])
+    assert "host-ahead run finished" in p.stdout

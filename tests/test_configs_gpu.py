@@ -349,14 +349,28 @@ def test_gan_full_size_iterations(ml20m, refinit):
         assert ok, f"G {k}: {msg}"
 
 
-# C3 and NeuMF run 10 steps: loss and MT state at every step, every parameter element at steps
-# 0, 1 and 9 (each check needs the whole tables on the host)
-NCF_STEPS, NCF_CHECKED = 10, (0, 1, 9)
+# C3 and NeuMF run 20 steps: loss and MT state at every step, every parameter element at steps
+# 0, 1, 9 and 19 (each check needs the whole tables on the host).  The elementwise band
+# (tests/parity_report.py) is sampled by three further fp32 restatements: two in seeded orders
+# of the examples, input features and hidden units (every forward and backward sum re-ordered)
+# and one deciding every LeakyReLU within fp32 rounding of its kink the other way
+# (NCFOracle(kink_flip=4)): a pre-activation that close to 0 is decided by the summation order
+# (tests/neumf_relu_probe.py names such an order), and the decision moves its example's rows by
+# a whole Adam step -- per-element membership, no count rule
+NCF_STEPS, NCF_CHECKED = 20, (0, 1, 9, 19)
+KINK_C = 4.0
+
+
+def _ncf_samples(Oracle, params, names, data, mt, kw):
+    """The three further fp32 restatements of the band (see NCF_STEPS)."""
+    return ([Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k, **kw)
+             for k in (1, 2)] +
+            [Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), kink_flip=KINK_C, **kw)])
 
 
 def test_ncf_full_size_steps(ml20m):
     """C3 (ncf_spotlight.py at ML-20M shape: mlp_embedding_dim 64, tower [128, 64, 32, 16, 8],
-    B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5): ten native steps with item plans and
+    B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5): twenty native steps with item plans and
     recorded dropout masks against the oracle (oracle/ncf.py) run in fp32 and fp64 from the
     same MLP(...) init: MT state bit-exact, loss 1e-5 relative, every parameter by tensor
     parity (oracle.mf.tensor_parity, as the golden-size NCF test)."""
@@ -377,11 +391,7 @@ def test_ncf_full_size_steps(ml20m):
                   device=dev, **kw)
     o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
     o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    # a second fp32 restatement summing over the examples in another order: with the first, the
-    # elementwise band's sample of the fp32 rounding noise (tests/parity_report.py)
-    # (two such orders: a two-sample band under-covers an element now and then -- 1 in 8.7M at step 1)
-    o32b = [oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k,
-                           **kw) for k in (1, 2)]
+    o32b = _ncf_samples(oncf.NCFOracle, params, names, data, mt, kw)
     widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
     rs = np.random.RandomState(5)
     for s in range(NCF_STEPS):
@@ -410,7 +420,7 @@ def test_ncf_full_size_steps(ml20m):
 
 def test_neumf_full_size_steps(ml20m):
     """neuMF_spotlight.py's defaults at ML-20M shape (mlp_embedding_dim 16, mf_embedding_dim 50,
-    B = 8192, n = 5, pointwise, Adam lr 1e-3): ten native steps with item plans and recorded
+    B = 8192, n = 5, pointwise, Adam lr 1e-3): twenty native steps with item plans and recorded
     dropout masks against oracle/ncf.py's NeuMFOracle in fp32 and fp64 from the same NeuMF(...)
     init: MT state bit-exact, loss 1e-5 relative, every parameter (GMF tables included) by
     tensor parity."""
@@ -431,8 +441,7 @@ def test_neumf_full_size_steps(ml20m):
                   device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
     o32 = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
     o64 = oncf.NeuMFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o32b = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=1,
-                            **kw)
+    o32b = _ncf_samples(oncf.NeuMFOracle, params, names, data, mt, kw)
     widths = oncf.layer_sizes(E)[1:]
     rs = np.random.RandomState(6)
     for s in range(NCF_STEPS):
@@ -446,13 +455,14 @@ def test_neumf_full_size_steps(ml20m):
         got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
         l32 = o32.step(pu, pi, mp, mn)
         o64.step(pu, pi, mp, mn)
-        o32b.step(pu, pi, mp, mn)
+        for ob in o32b:
+            ob.step(pu, pi, mp, mn)
         torch.cuda.synchronize()
         assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
         assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
         if s not in NCF_CHECKED:
             continue
-        for nm, p, r32, r64, b, rb in zip(names, e.params(), o32.P.t, o64.P.t, prev, o32b.P.t):
+        for k, (nm, p, r32, r64, b) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t, prev)):
             ok, msg = parity_report.check(f"NeuMF step {s} {nm}", p.reshape(r32.shape), r32, r64,
-                                          before=b.reshape(r32.shape), alt32=rb)
+                                          before=b.reshape(r32.shape), alt32=[ob.P.t[k] for ob in o32b])
             assert ok, f"step {s} {nm}: {msg}"

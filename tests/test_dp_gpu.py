@@ -29,6 +29,14 @@ from tests import dp_common as dc
 pytestmark = pytest.mark.gpu
 
 
+def _ab_only(needed):
+    """The sharded item update and the MT rank slices were measured slower or equal:
+    the A/B build carries them (scripts/gpu_ab_tests.sh)."""
+    from recommendation_gans_amd import _lib
+    if needed and not _lib.ab_build():
+        pytest.skip("A/B build only (RG_LIB=recommendation_gans_amd/_variants/librg_hip_ab.so)")
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -367,6 +375,7 @@ def test_owner_native_rccl_world1():
 @pytest.mark.parametrize("loss,item_shard", [("bpr", "0"), ("adaptive_hinge", "0"), ("bpr", "1"),
                                               ("adaptive_hinge", "1")])
 def test_owner_native_concurrent_step_world2(loss, item_shard):
+    _ab_only(item_shard == "1")
     """The whole native owner step (rg_mf_stepper_train, train_owner's stream placement: the score
     all-reduce and the item-gradient all-reduce on the main stream, where RCCL takes them; the
     user update and the next owner prepare on the communicator stream beside the item exchange
@@ -425,6 +434,7 @@ def _worker_own_slices(rank, world, port, loss, slice_flag, out):
 
 @pytest.mark.parametrize("loss", ["bpr", "pointwise"])
 def test_owner_mt_slices_match_the_full_walk(loss):
+    _ab_only(True)
     """The owner step's MT words by rank slices (each rank walks 2 n B of every step's 2 n R B words
     and jumps the rest; the slices all-gathered; the exported state advanced by a jump per slot)
     against every rank walking the whole global draw (RG_OWNER_MT_SLICE=0): per-step losses, the

@@ -105,3 +105,78 @@ def test_ncf_two_order_band_covers_a_third_order():
             ok, st_ = omf.elementwise_parity(c.P.t[k], a.P.t[k], r.P.t[k], alt32=b.P.t[k])
             assert ok, (s, k, st_)
             assert torch.allclose(r2.P.t[k], r.P.t[k], rtol=1e-9, atol=1e-12), (s, k)
+
+
+def _neumf_small(E=8, M=6, U=1500, I=200):
+    import numpy as np
+    from oracle import ncf as oncf
+    torch.manual_seed(1)
+    sizes = oncf.layer_sizes(E)
+    params = [torch.randn(U, E), torch.randn(I, E), torch.randn(U, M), torch.randn(I, M)]
+    ins = sizes[:-1]
+    outs = sizes[1:]
+    for a_, b_ in zip(ins, outs):
+        w = torch.empty(b_, a_)
+        torch.nn.init.xavier_uniform_(w)
+        params += [w, torch.full((b_,), 0.01)]
+    w = torch.empty(1, sizes[-1] + M)
+    torch.nn.init.xavier_uniform_(w)
+    params += [w, torch.full((1,), 0.01)]
+    rs = np.random.RandomState(3)
+    return params, [f"p{k}" for k in range(len(params))], rs.randint(0, U, 8000), rs.randint(0, I, 8000), sizes[1:]
+
+
+def test_neumf_unit_orders_and_kink_flips():
+    """NeuMF's further fp32 samples (oracle/ncf.py): order_seed re-orders the examples, the
+    tower's input features and hidden units (forward and backward inner sums) -- in float64 the
+    same function as the canonical order; kink_flip decides the LeakyReLUs within rounding of the
+    kink the other way -- with c = 0 it is the canonical restatement bit for bit, with c = 4 it
+    flips a few decisions a step (counted in .flips) and moves only the rows they touch."""
+    import numpy as np
+    from oracle import ncf as oncf
+    from oracle import rng as orng
+    params, names, pool_u, pool_i, widths = _neumf_small()
+    U, I = params[0].shape[0], params[1].shape[0]
+    B, n = 512, 5
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    st = orng.py_seed_state(0)
+
+    def mk(dtype, **k):
+        return oncf.NeuMFOracle([t.to(dtype).clone() for t in params], names, pool_u, pool_i, st.copy(), **kw, **k)
+    r, r2 = mk(torch.float64), mk(torch.float64, order_seed=3)
+    a, a0, f = mk(torch.float32), mk(torch.float32, kink_flip=0.0), mk(torch.float32, kink_flip=4.0)
+    f64 = mk(torch.float64, kink_flip=1e9)   # every kept decision flipped: a different function
+    rs = np.random.RandomState(0)
+    for s in range(3):
+        pu, pi = rs.randint(0, U, B), np.minimum(rs.zipf(1.3, B) - 1, I - 1)
+        mp = [torch.from_numpy((rs.rand(B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        for o in (r, r2, a, a0, f, f64):
+            o.step(pu, pi, mp, mn)
+        for k in range(len(params)):
+            assert torch.allclose(r2.P.t[k], r.P.t[k], rtol=1e-9, atol=1e-12), (s, k)
+            assert torch.equal(a0.P.t[k], a.P.t[k]), (s, k)
+    assert a0.flips == [0, 0, 0]
+    assert f64.flips[0] > 1000
+    assert not torch.allclose(f64.P.t[4], r.P.t[4], rtol=1e-4)
+    # the c = 4 sample: a handful of flips at most at this size, each moving its example's rows only
+    assert sum(f.flips) <= 20
+    moved = (f.P.t[0].double() - r.P.t[0]).abs().max(1).values > 1e-5
+    assert int(moved.sum()) <= 2 * sum(f.flips) + 1
+
+
+def test_kink_band_covers_seeded_orders():
+    """kink_flip's c = 4: the distance of a seeded-order fp32 pre-activation from its exact value is
+    within one band width (c = 1) on every decision of a batch; c = 4 leaves a 4x margin."""
+    from oracle import ncf as oncf
+    torch.manual_seed(2)
+    K, N, H = 128, 4096, 64
+    a = torch.randn(N, K)
+    W = torch.empty(H, K)
+    torch.nn.init.xavier_uniform_(W)
+    b = torch.full((H,), 0.01)
+    z64, band = oncf.kink_band(a, W, b, 1.0)
+    for seed in range(3):
+        p = torch.randperm(K, generator=torch.Generator().manual_seed(seed))
+        z32 = a[:, p].mm(W[:, p].t()) + b
+        assert float(((z32.double() - z64).abs() / band).max()) <= 1.0

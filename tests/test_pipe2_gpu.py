@@ -1,4 +1,4 @@
-"""The two-launch pipelined single-GPU MF step (rg_mf_pipe2_hot / rg_mf_pipe2_cold; opt-in,
+"""The two-launch pipelined single-GPU MF step (rg_mf_pipe2_hot / rg_mf_pipe2_cold; A/B build,
 RG_PIPE2=1, measured slower than the split step: step t's dense update of the rows step t+1's pair pass reads, then that pair pass beside the
 update of every other row and step t+2's prepare) against the split step (RG_PIPE2=0): the same
 per-row and per-column arithmetic, so losses, tables, optimizer state and the MT stream are
@@ -13,6 +13,16 @@ import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _ab_only():
+    from recommendation_gans_amd import _lib
+    _lib.load()
+    if not _lib.ab_build():
+        # measured slower than the split step: the A/B build carries it,
+        # scripts/gpu_ab_tests.sh runs this file with RG_LIB pointing at that build
+        pytest.skip("A/B build only (RG_LIB=recommendation_gans_amd/_variants/librg_hip_ab.so)")
 
 
 def _engine(pipe2, loss, d, U, I, B, n, seed=0):
