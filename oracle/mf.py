@@ -479,7 +479,7 @@ def tensor_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, alt3
     return ok, (f"rel-to-fp32 {e32 / max(n32, 1e-30):.2e}; |gpu-fp64| {eg:.3e} vs |fp32-fp64| {er:.3e}{extra}")
 
 
-def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, noise=None, alt32=None):
+def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None, noise=None, alt32=None, kink=None):
     """Elementwise companion of tensor_parity (a norm can hide a few bad elements).
 
     Element e passes if |got - ref32| <= rtol * |ref32| + floor (floor = rtol * 1e-3 *
@@ -521,7 +521,8 @@ def elementwise_parity(got, ref32, ref64=None, rtol=1e-5, band=3.0, before=None,
             alts = alt32 if isinstance(alt32, (list, tuple)) else ([] if alt32 is None else [alt32])
             for alt in alts:
                 dist = torch.maximum(dist, (torch.as_tensor(alt).double().reshape(-1) - r64).abs())
-            ok_e |= (g - r64).abs() <= band * dist + 0.1 * rtol * r64.abs() + floor
+            extra = 0.0 if kink is None else torch.as_tensor(kink).double().reshape(-1)
+            ok_e |= (g - r64).abs() <= band * dist + 0.1 * rtol * r64.abs() + floor + extra
     n = int(r.numel())
     n_out = int((~in_tol).sum())
     bad = (~ok_e).nonzero().flatten()[:4].tolist()

@@ -132,6 +132,7 @@ def backward(P, u, i, masks, cache, dp, xperm=None):
         if k > 0:
             z = cache["z"][k - 1]
             da = da * (masks[k - 1].to(z.dtype) * DROP_SCALE)
+            cache.setdefault("gr", {})[k - 1] = da
             dz = torch.where(cache["pos"][k - 1], da, da * LRELU)
         else:
             dx = da
@@ -148,13 +149,52 @@ def backward(P, u, i, masks, cache, dp, xperm=None):
     return out
 
 
+def kink_envelope(P, u, i, masks, cache, c, env, n_emb):
+    """Adds to ``env`` (per parameter, float64, the oracle's parameter order) the absolute change
+    of this batch's gradient that flipping each LeakyReLU decision within kink_band(c) of the
+    kink would make -- the reachable set of any fp32 order's decisions at rounding level, by the
+    triangle inequality over the flips.  A flip of unit k of hidden layer L for example e changes
+    its slope s -> s' (1 <-> 0.1): dz_L[e, k] moves by (s' - s) * gr (gr: the gradient at the
+    unit's LeakyReLU output, dropout applied), which moves dW_L[k, :], db_L[k] and, through the
+    example's own backward, every lower layer and the example's user / item embedding rows.  The
+    forward value moves by (s' - s) |z| <= the band itself, a second-order change neglected here.
+    Returns the number of kept decisions inside the band.  (Call after the backward, float64.)"""
+    lin = P.linears()
+    hid = lin[:-1]
+    E = P.emb()[0].shape[1]
+    count = 0
+    for L, (W, b) in enumerate(hid):
+        a_in = cache["a"][L]
+        z64, band = kink_band(a_in, W, b, c)
+        keep = masks[L] > 0
+        amb = (z64.abs() <= band) & keep
+        for e, k in amb.nonzero().tolist():
+            count += 1
+            pos = bool(cache["pos"][L][e, k])
+            d = float(cache["gr"][L][e, k]) * ((LRELU - 1.0) if pos else (1.0 - LRELU))
+            ddz = torch.zeros(W.shape[0], dtype=torch.float64)
+            ddz[k] = d
+            for j in range(L, -1, -1):              # the example's backward from layer L down
+                Wj = hid[j][0].double()
+                env[n_emb + 2 * j] += ddz.abs()[:, None] * cache["a"][j][e].double().abs()[None, :]
+                env[n_emb + 2 * j + 1] += ddz.abs()
+                dda = ddz @ Wj
+                if j > 0:
+                    keepj = masks[j - 1][e].double() * DROP_SCALE
+                    slope = torch.where(cache["pos"][j - 1][e], 1.0, LRELU).double()
+                    ddz = dda * keepj * slope
+            env[0][u[e]] += dda[:E].abs()
+            env[1][i[e]] += dda[E:].abs()
+    return count
+
+
 class NCFOracle:
     """One run_train_iteration (implicit.py:347-364) of the NCF MLP per ``step``."""
 
     N_EMB = 2                     # embedding tables before the Linears in parameter order
 
     def __init__(self, tensors, names, pool_u, pool_i, mt_state, loss="pointwise", lr=1e-2, weight_decay=1e-5,
-                 n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None, kink_flip=None):
+                 n_neg=5, batch_size=256, betas=(0.5, 0.999), order_seed=None, kink_flip=None, kink_env=None):
         self.P = MLPParams(tensors, names)
         # order_seed (pointwise, test infrastructure): run the step over the examples, the input
         # features and every hidden layer's units in seeded orders -- the same arithmetic summed
@@ -167,6 +207,13 @@ class NCFOracle:
         # count of such decisions that reach the loss, per step, in self.flips
         self.kink_flip = kink_flip
         self.flips = []
+        # kink_env (float64, test infrastructure): c of kink_band -- each step also bounds, per
+        # element, how far flipping any subset of the kept LeakyReLU decisions within the band
+        # moves the parameters after the optimizer (kink_envelope through Optim.sensitivity):
+        # self.kink_noise, with the count of such decisions in self.kink_count
+        assert kink_env is None or order_seed is None
+        self.kink_env = kink_env
+        self.kink_noise, self.kink_count = None, []
         self.loss_kind = loss
         self.n, self.batch_size = n_neg, batch_size
         self.opt_lr, self.opt_wd, self.opt_betas = lr, weight_decay, betas
@@ -224,6 +271,15 @@ class NCFOracle:
     _fwd = staticmethod(forward)
     _bwd = staticmethod(backward)
 
+    def _envelope(self, P, pos, neg, grads):
+        if self.kink_env is None:
+            return
+        env = [torch.zeros(t.shape, dtype=torch.float64) for t in self.P.t]
+        n = sum(kink_envelope(P, uu, ii, mm, cc, self.kink_env, env, self.N_EMB) for uu, ii, mm, cc in (pos, neg))
+        self.kink_count.append(n)
+        dstate = [(torch.zeros_like(e), torch.zeros_like(e)) for e in env]
+        self.kink_noise = self.opt.sensitivity(self.P.t, grads, env, dstate)
+
     def step(self, pos_u, pos_i, masks_pos, masks_neg, return_all=False):
         u = torch.as_tensor(pos_u).long()
         i = torch.as_tensor(pos_i).long()
@@ -241,6 +297,7 @@ class NCFOracle:
         g1 = self._bwd(P, u, i, masks_pos, c_pos, dpp.reshape(-1, 1), xperm)
         g2 = self._bwd(P, nu, ni, masks_neg, c_neg, dpn.reshape(-1, 1), xperm)
         grads = gback([a + b for a, b in zip(g1, g2)])
+        self._envelope(P, (u, i, masks_pos, c_pos), (nu, ni, masks_neg, c_neg), grads)
         self.opt.step(self.P.t, grads)
         if return_all:
             return dict(loss=float(loss), p_pos=p_pos, p_neg=p_neg, neg_idx=idx, neg_u=nu, neg_i=ni, grads=grads)
@@ -297,6 +354,7 @@ def neumf_backward(P, u, i, masks, cache, dp, xperm=None):
         Wk, bk = lin[k]
         z = cache["z"][k]
         da = da * (masks[k].to(z.dtype) * DROP_SCALE)
+        cache.setdefault("gr", {})[k] = da
         dzk = torch.where(cache["pos"][k], da, da * LRELU)
         grads_lin.append((dzk.t().mm(cache["a"][k]), dzk.sum(0)))
         da = dzk.mm(Wk)

@@ -36,12 +36,16 @@ def order_stats(got, ref32, order32, rtol=1e-5):
             "max_ref_rel": float((a - r).abs().max()) / max(mx, 1e-30) if r.numel() else 0.0}
 
 
-def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None, alt32=None, order32=None):
+def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=None, alt32=None, order32=None,
+          elementwise=True, kink=None):
+    """``elementwise`` False: the verdict is the norm rule's alone, the elementwise figures are
+    reported (a free-running trajectory past the depth where equally valid fp32 orders part
+    element by element, tests/test_configs_gpu.py NCF_STEPS)."""
     ok_n, msg = omf.tensor_parity(got, ref32, ref64, rtol=rtol, band=band, before=before, alt32=alt32)
     ok_e, st = omf.elementwise_parity(got, ref32, ref64, rtol=rtol, band=band, before=before, noise=noise,
-                                      alt32=alt32)
-    line = (f"{tag}: max|d|/max|ref| {st['max_rel']:.2e}, outside 1e-5 {st['n_out']}/{st['n']} "
-            f"({st['frac_out']:.2e}), ill-conditioned {st['n_ill']}, failing the fp64 band too {st['n_fail']}")
+                                      alt32=alt32, kink=kink)
+    line = (f"{tag}{'' if elementwise else ' (reported)'}: max|d|/max|ref| {st['max_rel']:.2e}, "
+            f"outside 1e-5 {st['n_out']}/{st['n']} ({st['frac_out']:.2e}), ill-conditioned {st['n_ill']}, failing the fp64 band too {st['n_fail']}")
     if order32 is not None:
         st["order"] = order_stats(got, ref32, order32, rtol)
         o = st["order"]
@@ -51,7 +55,8 @@ def check(tag, got, ref32, ref64=None, before=None, rtol=1e-5, band=3.0, noise=N
     try:
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         with open(os.path.join(ROOT, "gpurun_out", "parity_elementwise.jsonl"), "a") as f:
-            f.write(json.dumps({"tag": tag, "norm_ok": ok_n, "norm": msg, **st}) + "\n")
+            f.write(json.dumps({"tag": tag, "norm_ok": ok_n, "norm": msg, "elementwise_asserted": elementwise,
+                                **st}) + "\n")
     except OSError:
         pass
-    return ok_n and ok_e, f"{msg}; {line}"
+    return ok_n and (ok_e or not elementwise), f"{msg}; {line}"

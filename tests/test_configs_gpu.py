@@ -16,8 +16,9 @@
 * C4 (cGAN, N = 20,108, S = 5, H = 256, E = 5, B = 256, histories of the synthetic
   ML-20M users): one discriminator iteration and one generator iteration with
   recorded z and dropout masks against the float64 oracle (oracle/gan.py);
-* C3 (NCF, ML-20M-shaped, mlp_embedding_dim 64, B = 8192): ten native steps with
-  item plans and recorded dropout masks against oracle/ncf.py in fp32 and fp64;
+* C3 (NCF, ML-20M-shaped, mlp_embedding_dim 64, B = 8192): twenty native steps with
+  item plans and recorded dropout masks against oracle/ncf.py in fp32 and fp64, the trajectory
+  and each step from the GPU's own state at depth (NCF_STEPS below);
   NeuMF (neuMF_spotlight.py defaults, mlp 16 / mf 50) the same way.
 
 The CPU oracle runs at these sizes in a few seconds per step on the box's host cores."""
@@ -349,120 +350,149 @@ def test_gan_full_size_iterations(ml20m, refinit):
         assert ok, f"G {k}: {msg}"
 
 
-# C3 and NeuMF run 20 steps: loss and MT state at every step, every parameter element at steps
-# 0, 1, 9 and 19 (each check needs the whole tables on the host).  The elementwise band
-# (tests/parity_report.py) is sampled by three further fp32 restatements: two in seeded orders
-# of the examples, input features and hidden units (every forward and backward sum re-ordered)
-# and one deciding every LeakyReLU within fp32 rounding of its kink the other way
-# (NCFOracle(kink_flip=4)): a pre-activation that close to 0 is decided by the summation order
-# (tests/neumf_relu_probe.py names such an order), and the decision moves its example's rows by
-# a whole Adam step -- per-element membership, no count rule
-NCF_STEPS, NCF_CHECKED = 20, (0, 1, 9, 19)
+# C3 and NeuMF run 20 steps, checked two ways (DESIGN.md §5 "Depth"):
+#  * the trajectory: GPU and oracles run free from the same init -- the loss within 1e-5 and the
+#    MT state exact at EVERY step; every parameter by the norm rule at steps 0, 1, 9 and 19, and
+#    every ELEMENT inside the band at steps 0 and 1;
+#  * each step at depth: before steps 9 and 19 fresh oracles start from the GPU's own state
+#    (parameters, Adam moments and step, MT state) and take that one step -- every element of the
+#    GPU's result inside the band plus the kink envelope: the float64 restatement's bound, per
+#    element, on what flipping any subset of the step's rounding-level LeakyReLU decisions moves
+#    after Adam (NCFOracle(kink_env=4), oracle/ncf.py kink_envelope; on the CPU it covers the
+#    kink-flip sample on every element, tests/test_parity_cpu.py).
+# The band (tests/parity_report.py, per element, no count rule) is sampled by further fp32
+# restatements: two in seeded orders of the examples, input features and hidden units (every
+# forward and backward sum re-ordered) and, for the elementwise checks, one deciding every
+# LeakyReLU within fp32 rounding of its kink the other way (NCFOracle(kink_flip=4)): a
+# pre-activation that close to 0 is decided by the summation order (tests/neumf_relu_probe.py
+# names such an order) and moves its example's rows by a whole Adam step.  Free-running fp32 runs
+# of the reference in different orders part element by element faster than a finite sample of
+# them covers: at step 9 a held-out order already falls outside the band of the others on ~10^3
+# elements and at step 19 on ~10^4 (tests/parity_chaos.py, profiles/r6/parity/chaos_*.jsonl), so
+# the trajectory is held per element only while it is well posed (steps 0, 1) and to the norm rule
+# after, while the step itself is held per element at every checked depth.
+NCF_STEPS, NCF_CHECKED, NCF_ELEMENTWISE, NCF_RESTART = 20, (0, 1, 9, 19), (0, 1), (9, 19)
 KINK_C = 4.0
 
 
-def _ncf_samples(Oracle, params, names, data, mt, kw):
+def _ncf_samples(Oracle, params, names, data, mt, kw, t=0, moments=None):
     """The three further fp32 restatements of the band (see NCF_STEPS)."""
-    return ([Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), order_seed=k, **kw)
-             for k in (1, 2)] +
-            [Oracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), kink_flip=KINK_C, **kw)])
+    return [_ncf_oracle(Oracle, params, names, data, mt, kw, torch.float32, t, moments, order_seed=k)
+            for k in (1, 2)] + \
+        [_ncf_oracle(Oracle, params, names, data, mt, kw, torch.float32, t, moments, kink_flip=KINK_C)]
+
+
+def _ncf_oracle(Oracle, params, names, data, mt, kw, dtype, t=0, moments=None, **extra):
+    o = Oracle([torch.as_tensor(p).to(dtype).clone() for p in params], names, data.pool_u, data.pool_i,
+               np.array(mt, dtype=np.uint32).copy(), **kw, **extra)
+    if moments is not None:      # started from an engine's state: its Adam moments and step count
+        o.opt.t = t
+        o.opt.state = [(m.to(dtype).clone(), v.to(dtype).clone()) for m, v in moments]
+    return o
+
+
+def _ncf_engine_state(e):
+    """The engine's parameters (named_parameters() order), Adam (m, v) per parameter, step and MT
+    state, on the host."""
+    def split(flat):
+        out, o = [], 0
+        for shp in e.mlp_shapes:
+            k = int(np.prod(shp))
+            out.append(flat[o:o + k].view(shp).detach().cpu().clone())
+            o += k
+        return out
+    tabs = [0, 1] + ([3, 4] if e.neumf else [])
+    ms = [e.m[k].detach().cpu().clone() for k in tabs] + split(e.m[2])
+    vs = [e.v[k].detach().cpu().clone() for k in tabs] + split(e.v[2])
+    ps = [p.detach().cpu().clone() for p in e.params()]
+    return ps, list(zip(ms, vs)), e.t, e.mt_state()
+
+
+def _ncf_depth_run(data, neumf):
+    from oracle import ncf as oncf
+    from recommendation_gans_amd.ncf_engine import NCFEngine
+    from recommendation_gans_amd.ncf_spotlight import mlp_layers
+    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
+    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
+    dev = torch.device("cuda:0")
+    E = 16 if neumf else 64
+    U, I, B, n = data.num_users, data.num_items, 8192, 5
+    torch.manual_seed(0)                                   # ncf_spotlight.py / neuMF_spotlight.py init
+    net = (NeuMF(mlp_layers(E), U, I, mf_embedding_dim=50, mlp_embedding_dim=E) if neumf
+           else MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E))
+    names = [k for k, _ in net.named_parameters()]
+    params = [p.detach().clone() for p in net.parameters()]
+    mt = orng.py_seed_state(0)
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    if neumf:
+        e = NCFEngine(params[0], params[1], params[4:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                      device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
+    else:
+        e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
+                      device=dev, **kw)
+    Oracle = oncf.NeuMFOracle if neumf else oncf.NCFOracle
+    tag = "NeuMF" if neumf else "C3 ncf"
+    o32 = _ncf_oracle(Oracle, params, names, data, mt, kw, torch.float32)
+    o64 = _ncf_oracle(Oracle, params, names, data, mt, kw, torch.float64)
+    o32b = _ncf_samples(Oracle, params, names, data, mt, kw)
+    widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
+    rs = np.random.RandomState(6 if neumf else 5)
+    for s in range(NCF_STEPS):
+        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
+        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
+        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
+        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
+        start = _ncf_engine_state(e) if s in NCF_RESTART else None
+        prev = [t.detach().cpu().clone() for t in e.params()]
+        pi_d = torch.from_numpy(pi).to(dev)
+        got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
+        l32 = o32.step(pu, pi, mp, mn)
+        o64.step(pu, pi, mp, mn)
+        for ob in o32b:
+            ob.step(pu, pi, mp, mn)
+        torch.cuda.synchronize()
+        assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
+        assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
+        gpu = [p.detach().cpu().reshape(r.shape) for p, r in zip(e.params(), o32.P.t)]
+        if s in NCF_CHECKED:
+            ew = s in NCF_ELEMENTWISE
+            band = o32b if ew else o32b[:2]             # the kink-flip sample for the elementwise checks
+            for k, nm in enumerate(names):
+                ok, msg = parity_report.check(f"{tag} step {s} {nm}", gpu[k], o32.P.t[k], o64.P.t[k],
+                                              before=prev[k].reshape(gpu[k].shape), alt32=[ob.P.t[k] for ob in band],
+                                              elementwise=ew)
+                assert ok, f"step {s} {nm}: {msg}"
+        if start is not None:
+            # the step from the GPU's own state: fp32, fp64 and the three band samples re-started there
+            ps, mom, t0, st0 = start
+            r32 = _ncf_oracle(Oracle, ps, names, data, st0, kw, torch.float32, t0, mom)
+            r64 = _ncf_oracle(Oracle, ps, names, data, st0, kw, torch.float64, t0, mom, kink_env=KINK_C)
+            rb = _ncf_samples(Oracle, ps, names, data, st0, kw, t0, mom)
+            lr32 = r32.step(pu, pi, mp, mn)
+            r64.step(pu, pi, mp, mn)
+            for ob in rb:
+                ob.step(pu, pi, mp, mn)
+            assert abs(float(got[0]) - lr32) <= 1e-5 * abs(lr32), (s, "restart", float(got[0]), lr32)
+            for k, nm in enumerate(names):
+                ok, msg = parity_report.check(f"{tag} step {s} from the GPU's state {nm}", gpu[k], r32.P.t[k],
+                                              r64.P.t[k], before=ps[k], alt32=[ob.P.t[k] for ob in rb],
+                                              kink=r64.kink_noise[k])
+                assert ok, f"step {s} (from the GPU's state) {nm}: {msg}"
+            del r32, r64, rb
 
 
 def test_ncf_full_size_steps(ml20m):
     """C3 (ncf_spotlight.py at ML-20M shape: mlp_embedding_dim 64, tower [128, 64, 32, 16, 8],
     B = 8192, n = 5, pointwise, Adam lr 1e-3, wd 1e-5): twenty native steps with item plans and
-    recorded dropout masks against the oracle (oracle/ncf.py) run in fp32 and fp64 from the
-    same MLP(...) init: MT state bit-exact, loss 1e-5 relative, every parameter by tensor
-    parity (oracle.mf.tensor_parity, as the golden-size NCF test)."""
-    from oracle import ncf as oncf
-    from recommendation_gans_amd.ncf_engine import NCFEngine
-    from recommendation_gans_amd.ncf_spotlight import mlp_layers
-    from recommendation_gans_amd.spotlight.dnn_models.mlp import MLP
-    data = ml20m
-    dev = torch.device("cuda:0")
-    U, I, E, B, n = data.num_users, data.num_items, 64, 8192, 5
-    torch.manual_seed(0)                                   # ncf_spotlight.py: MLP(...) init
-    net = MLP(layers=mlp_layers(E), num_users=U, num_items=I, embedding_dim=E)
-    names = [k for k, _ in net.named_parameters()]
-    params = [p.detach().clone() for p in net.parameters()]
-    mt = orng.py_seed_state(0)
-    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
-    e = NCFEngine(params[0], params[1], params[2:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
-                  device=dev, **kw)
-    o32 = oncf.NCFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o64 = oncf.NCFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o32b = _ncf_samples(oncf.NCFOracle, params, names, data, mt, kw)
-    widths = oncf.layer_sizes(E)[1:]                        # one dropout per hidden Linear
-    rs = np.random.RandomState(5)
-    for s in range(NCF_STEPS):
-        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
-        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
-        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
-        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
-        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
-        prev = [t.detach().cpu().clone() for t in e.params()]
-        pi_d = torch.from_numpy(pi).to(dev)
-        got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
-        l32 = o32.step(pu, pi, mp, mn)
-        o64.step(pu, pi, mp, mn)
-        for ob in o32b:
-            ob.step(pu, pi, mp, mn)
-        torch.cuda.synchronize()
-        assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
-        assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
-        if s not in NCF_CHECKED:
-            continue
-        for k, (nm, p, r32, r64) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t)):
-            ok, msg = parity_report.check(f"C3 ncf step {s} {nm}", p.reshape(r32.shape), r32, r64,
-                                          before=prev[k].reshape(r32.shape), alt32=[ob.P.t[k] for ob in o32b])
-            assert ok, f"step {s} {nm}: {msg}"
+    recorded dropout masks against the oracle (oracle/ncf.py) from the same MLP(...) init, checked
+    as NCF_STEPS says."""
+    _ncf_depth_run(ml20m, neumf=False)
 
 
 def test_neumf_full_size_steps(ml20m):
     """neuMF_spotlight.py's defaults at ML-20M shape (mlp_embedding_dim 16, mf_embedding_dim 50,
     B = 8192, n = 5, pointwise, Adam lr 1e-3): twenty native steps with item plans and recorded
-    dropout masks against oracle/ncf.py's NeuMFOracle in fp32 and fp64 from the same NeuMF(...)
-    init: MT state bit-exact, loss 1e-5 relative, every parameter (GMF tables included) by
-    tensor parity."""
-    from oracle import ncf as oncf
-    from recommendation_gans_amd.ncf_engine import NCFEngine
-    from recommendation_gans_amd.ncf_spotlight import mlp_layers
-    from recommendation_gans_amd.spotlight.dnn_models.neuMF import NeuMF
-    data = ml20m
-    dev = torch.device("cuda:0")
-    U, I, E, M, B, n = data.num_users, data.num_items, 16, 50, 8192, 5
-    torch.manual_seed(0)
-    net = NeuMF(mlp_layers(E), U, I, mf_embedding_dim=M, mlp_embedding_dim=E)
-    names = [k for k, _ in net.named_parameters()]
-    params = [p.detach().clone() for p in net.parameters()]
-    mt = orng.py_seed_state(0)
-    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
-    e = NCFEngine(params[0], params[1], params[4:], data.pool_u, data.pool_i, mt.copy(), optimizer="adam",
-                  device=dev, mf_user_w=params[2], mf_item_w=params[3], **kw)
-    o32 = oncf.NeuMFOracle([t.clone() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o64 = oncf.NeuMFOracle([t.double() for t in params], names, data.pool_u, data.pool_i, mt.copy(), **kw)
-    o32b = _ncf_samples(oncf.NeuMFOracle, params, names, data, mt, kw)
-    widths = oncf.layer_sizes(E)[1:]
-    rs = np.random.RandomState(6)
-    for s in range(NCF_STEPS):
-        pu = data.train_u[s * B:(s + 1) * B].astype(np.int64)
-        pi = data.train_i[s * B:(s + 1) * B].astype(np.int64)
-        mp = [torch.from_numpy((rs.rand(B, w) >= 0.5).astype(np.uint8)) for w in widths]
-        mn = [torch.from_numpy((rs.rand(n * B, w) >= 0.5).astype(np.uint8)) for w in widths]
-        masks = (torch.cat(mp, 1).to(dev).contiguous(), torch.cat(mn, 1).to(dev).contiguous())
-        prev = [t.detach().cpu().clone() for t in e.params()]
-        pi_d = torch.from_numpy(pi).to(dev)
-        got = e.train_step(torch.from_numpy(pu).to(dev), pi_d, plan=e.make_plan(pi_d), masks=masks)
-        l32 = o32.step(pu, pi, mp, mn)
-        o64.step(pu, pi, mp, mn)
-        for ob in o32b:
-            ob.step(pu, pi, mp, mn)
-        torch.cuda.synchronize()
-        assert abs(float(got[0]) - l32) <= 1e-5 * abs(l32), (s, float(got[0]), l32)
-        assert (e.mt_state() == o32.state).all(), f"MT state after step {s}"
-        if s not in NCF_CHECKED:
-            continue
-        for k, (nm, p, r32, r64, b) in enumerate(zip(names, e.params(), o32.P.t, o64.P.t, prev)):
-            ok, msg = parity_report.check(f"NeuMF step {s} {nm}", p.reshape(r32.shape), r32, r64,
-                                          before=b.reshape(r32.shape), alt32=[ob.P.t[k] for ob in o32b])
-            assert ok, f"step {s} {nm}: {msg}"
+    dropout masks against oracle/ncf.py's NeuMFOracle from the same NeuMF(...) init (GMF tables
+    included), checked as NCF_STEPS says."""
+    _ncf_depth_run(ml20m, neumf=True)

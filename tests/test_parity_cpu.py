@@ -180,3 +180,51 @@ def test_kink_band_covers_seeded_orders():
         p = torch.randperm(K, generator=torch.Generator().manual_seed(seed))
         z32 = a[:, p].mm(W[:, p].t()) + b
         assert float(((z32.double() - z64).abs() / band).max()) <= 1.0
+
+
+def test_kink_envelope_covers_the_kink_flip_sample():
+    """NCFOracle(kink_env=c) (float64): its per-element bound on what flipping any subset of the
+    step's rounding-level LeakyReLU decisions moves after Adam covers the fp32 sample that flips
+    ALL of them (kink_flip=c) on every element of every parameter, from the same state; without
+    the envelope the same sample falls outside the two-order band.  NeuMF at a small size, one
+    step from a state three steps in.  c = 200 (fifty times the tests' 4) so that this small batch
+    has flips to check."""
+    import numpy as np
+    C = 200.0
+    from oracle import ncf as oncf
+    from oracle import rng as orng
+    params, names, pool_u, pool_i, widths = _neumf_small(E=16, M=8, U=3000, I=400)
+    B, n = 2048, 5
+    kw = dict(loss="pointwise", lr=1e-3, weight_decay=1e-5, n_neg=n, batch_size=B)
+    rs = np.random.RandomState(4)
+
+    def batch():
+        pu, pi = rs.randint(0, 3000, B), np.minimum(rs.zipf(1.3, B) - 1, 399)
+        mp = [torch.from_numpy((rs.rand(B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        mn = [torch.from_numpy((rs.rand(n * B, w_) >= 0.5).astype(np.uint8)) for w_ in widths]
+        return pu, pi, mp, mn
+    run = oncf.NeuMFOracle([t.clone() for t in params], names, pool_u, pool_i, orng.py_seed_state(0), **kw)
+    for _ in range(3):
+        run.step(*batch())
+    ps, st, t = [p.clone() for p in run.P.t], run.state.copy(), run.opt.t
+    mom = [(m.clone(), v.clone()) for m, v in run.opt.state]
+
+    def mk(dtype, **k):
+        o = oncf.NeuMFOracle([p.to(dtype).clone() for p in ps], names, pool_u, pool_i, st.copy(), **kw, **k)
+        o.opt.t, o.opt.state = t, [(m.to(dtype).clone(), v.to(dtype).clone()) for m, v in mom]
+        return o
+    r32, r64 = mk(torch.float32), mk(torch.float64, kink_env=C)
+    alts = [mk(torch.float32, order_seed=k) for k in (1, 2)]
+    flip = mk(torch.float32, kink_flip=C)
+    b = batch()
+    for o in [r32, r64, flip] + alts:
+        o.step(*b)
+    assert r64.kink_count[-1] == flip.flips[-1] > 0
+    fail_env = fail_band = 0
+    for k in range(len(names)):
+        _, s1 = omf.elementwise_parity(flip.P.t[k], r32.P.t[k], r64.P.t[k], alt32=[a.P.t[k] for a in alts],
+                                       kink=r64.kink_noise[k])
+        _, s2 = omf.elementwise_parity(flip.P.t[k], r32.P.t[k], r64.P.t[k], alt32=[a.P.t[k] for a in alts])
+        fail_env += s1["n_fail"]
+        fail_band += s2["n_fail"]
+    assert fail_env == 0 and fail_band > 0, (fail_env, fail_band)
