@@ -603,7 +603,6 @@ __global__ __launch_bounds__(kWsThreads) void gemm_opt_ws_kernel(GemmDesc d) {
 #pragma unroll
                     for (int t = 0; t < 16; ++t) b[i][t] = fminf(fmaxf(b[i][t], -d.clamp_b), d.clamp_b);
             }
-#ifndef RG_X_WS_NOMFMA   // timing experiments only (wrong results): the matrix waves skip the MFMAs
 #pragma unroll
             for (int t = 0; t < 16; ++t)
 #pragma unroll
@@ -611,9 +610,6 @@ __global__ __launch_bounds__(kWsThreads) void gemm_opt_ws_kernel(GemmDesc d) {
 #pragma unroll
                     for (int jj = 0; jj < 2; ++jj)
                         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t], b[jj][t], acc[i][jj], 0, 0, 0);
-#else
-            acc[0][0][0] += a[0][0] + b[0][0];
-#endif
             if (G % nk == nk - 1) {
                 // hand the tile over: this wave's 64-row half u = 2n + wm, once halves < u are taken
                 const int u = 2 * (G / nk) + wm;
@@ -663,9 +659,6 @@ __global__ __launch_bounds__(kWsThreads) void gemm_opt_ws_kernel(GemmDesc d) {
                 if (c == 0) g[q].x += sv; else if (c == 1) g[q].y += sv; else if (c == 2) g[q].z += sv; else g[q].w += sv;
             }
         }
-#ifdef RG_X_WS_NOUPD   // timing experiments only (wrong results): the update waves only take the tiles
-        if (g[0].x != 12345.0f) continue;
-#endif
         const bool vec = nn + 3 < d.N && (d.ldp & 3) == 0 && aligned16(d.P) && (!d.Ms || aligned16(d.Ms)) &&
                          (!d.Vs || aligned16(d.Vs));
 #pragma unroll

@@ -639,11 +639,6 @@ struct ApplyArgs {
 #ifndef RG_DENSE_WT
 #define RG_DENSE_WT 0
 #endif
-#ifdef RG_X_STREAMONLY
-#define RG_X_SO 1
-#else
-#define RG_X_SO 0
-#endif
 #ifndef RG_MF_SORTED_PULL
 #define RG_MF_SORTED_PULL 1
 #endif
@@ -881,11 +876,9 @@ __device__ __forceinline__ void lean_load(const ApplyArgs &a, const int64_t r, c
         if (adam) x.mb = a.b_m[t][lr_];
         if (has_v) x.vb = a.b_v[t][lr_];
     }
-#ifndef RG_X_STREAMONLY   // timing experiments only (wrong results): p, m, v and biases alone
     x.c = a.row_count[r];
     if (sub < kCap) x.ent = a.row_list[r * kCap + sub];
     if (t == 1 && a.item_slot_off != nullptr) { x.s0 = a.item_slot_off[lr_]; x.s1 = a.item_slot_off[lr_ + 1]; }
-#endif
 }
 
 template <class L, bool WT = false>
@@ -912,11 +905,7 @@ __device__ __forceinline__ void lean_finish(const ApplyArgs &a, const int64_t r,
 #endif
         const float *other = a.contrib ? a.contrib + t * D : a.w_in[t ^ 1];
         const int64_t ostride = a.contrib ? a.contrib_stride : (int64_t)D;
-#ifdef RG_X_NOFIX   // timing experiments only (wrong results for overflowed rows)
-        const bool fixp = false;
-#else
         const bool fixp = c > kCap;   // an overflowed row sums list and surplus in fixed point
-#endif
         long long gf[EPL];
         long long gbf = 0;
 #pragma unroll
@@ -1122,19 +1111,13 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         L::load(g, gbase, gkk, D, sub);
         if (sub == 0) gb = a.grad[gbi];
     } else if (!COLD) {
-#if defined(RG_X_STREAMONLY)   // timing experiments only (wrong results): p, m, v and biases alone
-        const int c = 0;
-#elif defined(RG_X_NOPULL)   // timing experiments only (wrong results): the pass without the pulls
-        const int c = a.row_count[r] < 0 ? 1 : 0;
-#else
         const int c = lz ? cnt : (COLD ? 0 : a.row_count[r]);
-#endif
         // SPEC: the list and the item's partial-slot range are loaded beside the count
         // (entries past the count are stale and never used), so a touched row's partner
         // rows are its only dependent round trip
         int2 spec[SPEC ? kCap : 1];
         int s0 = 0, s1 = 0;
-        if (SPEC && !lz && !RG_X_SO) {
+        if (SPEC && !lz) {
             const int4 *lst = reinterpret_cast<const int4 *>(a.row_list + r * kCap);
 #pragma unroll
             for (int e = 0; e < kCap / 2; ++e) {
@@ -1151,7 +1134,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         constexpr bool kOneTrip = MODE == kGradOnly && SPEC;
         float h0[kOneTrip ? 4 : 1][EPL];
         float hb0[kOneTrip ? 4 : 1];
-        const bool parts = !RG_X_SO && t == 1 && a.item_slot_off != nullptr;
+        const bool parts = t == 1 && a.item_slot_off != nullptr;
         if (kOneTrip && parts && s1 > s0) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1221,11 +1204,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
                     }
                 }
             }
-#ifdef RG_X_NOOVF   // timing experiments only (wrong results): overflowed rows skip their accumulators
-            if (false) {
-#else
             if (fixp) {
-#endif
                 // the surplus' accumulators (fixed point), read and reset
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
@@ -1246,11 +1225,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
             }
             if (sub == 0 && !a.keep_count) a.row_count[r] = 0;
         }
-#ifdef RG_X_NOPART  // timing experiments only (wrong results): no planned partials
-        if (false) {
-#else
         if (parts && !guarded) {   // planned positive partials of this item
-#endif
             if (!SPEC || lz) { s0 = a.item_slot_off[lr_]; s1 = a.item_slot_off[lr_ + 1]; }
             for (int sl = s0; sl < s1; sl += 4) {
                 float h[4][EPL];
@@ -1473,9 +1448,6 @@ __global__ __launch_bounds__(kBlock) RG_BACK_ATTR void mf_back_kernel(ApplyArgs 
     // overlaps the streaming rows instead of trailing the grid (RG_PREP_FIRST=0: last)
     if (bg.prep_first) {
         if (blk < bg.prep_blocks) {
-#ifdef RG_X_NOPREP   // timing experiments only
-            return;
-#endif
             if (OWN) owner_prepare_block(own, blk);
             else prepare_one(prep, prep_out, blk * kBlock + threadIdx.x);
             return;
@@ -1624,27 +1596,6 @@ __global__ __launch_bounds__(kBlock) void mf_pipe2_cold_kernel(ApplyArgs a, Pair
 #endif
 }
 
-#ifdef RG_X_PIPE2
-// Timing prototype only (wrong results): step t+1's pair pass (blocks [0, pair_blocks), pair-pass
-// layout LP) in the same launch as the dense update of rows [row_begin, row_end) (layout LD): does a
-// latency-bound pair pass hide under an HBM-bound stream when they share a launch?
-template <class LP, class LD, int NMAX>
-__global__ __launch_bounds__(kBlock) void mf_pipe2_kernel(ApplyArgs a, PairsArgs pa, int64_t pair_blocks) {
-    int64_t blk = blockIdx.x;
-    if (blk < pair_blocks) {
-        pairs_body<LP, kFused, NMAX>(pa, blk);
-        return;
-    }
-    blk -= pair_blocks;
-    constexpr int LPU = LD::LPU, UPW = LD::UPW;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int sub = lane & (LPU - 1);
-    const int64_t wave = (blk * kBlock + threadIdx.x) >> 6;
-    const int64_t k = wave * UPW + (lane / LPU);
-    if (k >= a.row_end - a.row_begin) return;
-    apply_row<LD, kApplyPull, 0, false, true>(a, a.row_begin + k, sub);
-}
-#endif
 
 // The single-GPU dense pass as a software pipeline (the default split step): a grid of a few
 // workgroups per CU whose waves each walk a contiguous chunk of row groups (UPW rows per group),
@@ -2758,42 +2709,6 @@ extern "C" int rg_mf_pipe2_cold(void *stream, const rg_mf_tables_t *t, rg_mf_wor
     return dispatch_dim(t->dim, f);
 }
 
-#ifdef RG_X_PIPE2
-namespace {
-struct Pipe2LaunchF {
-    ApplyArgs *a;
-    PairsArgs *pa;
-    hipStream_t s;
-    template <class L>
-    int operator()() {
-        using LB = typename BackLayout<L>::type;
-        const int64_t pb = pairs_blocks<L>(pa->cols);
-        const int64_t rows = a->row_end - a->row_begin;
-        const int64_t nb = ((rows + LB::UPW - 1) / LB::UPW + kBlock / kWave - 1) / (kBlock / kWave);
-        if (pa->n_neg <= 5)
-            hipLaunchKernelGGL((mf_pipe2_kernel<L, LB, 5>), dim3((unsigned)(pb + nb)), dim3(kBlock), 0, s, *a, *pa, pb);
-        else
-            hipLaunchKernelGGL((mf_pipe2_kernel<L, LB, kNMax>), dim3((unsigned)(pb + nb)), dim3(kBlock), 0, s, *a, *pa, pb);
-        return check_launch("rg_x_pipe2");
-    }
-};
-}  // namespace
-
-// timing prototype only: the pair pass of `pair_b` (on the tables' out set) and the dense update of
-// rows [row_begin, row_end) in ONE launch
-extern "C" int rg_x_pipe2(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
-                          int64_t row_begin, int64_t row_end, const rg_mf_batch_t *pair_b, rg_mf_work_t *pair_w) {
-    ApplyArgs a;
-    int rc = apply_args(t, w, nullptr, nullptr, opt, row_begin, row_end, nullptr, nullptr, kApplyPull, a);
-    if (rc) return rc;
-    rg_mf_tables_t pt = *t;
-    pt.user_w = t->user_w_out; pt.item_w = t->item_w_out; pt.user_b = t->user_b_out; pt.item_b = t->item_b_out;
-    PairsArgs pa;
-    if ((rc = pairs_args(&pt, pair_b, pair_w, 1, pa))) return rc;
-    Pipe2LaunchF f{&a, &pa, (hipStream_t)stream};
-    return dispatch_dim(t->dim, f);
-}
-#endif
 
 extern "C" int rg_mf_apply_prepare(void *stream, const rg_mf_tables_t *t, rg_mf_work_t *w, const rg_opt_t *opt,
                                    int64_t row_begin, int64_t row_end, const rg_mf_loss_t *loss,
@@ -2821,16 +2736,6 @@ extern "C" int rg_mf_apply_prepare_gen(void *stream, const rg_mf_tables_t *t, rg
         prep_out = reinterpret_cast<int2 *>(next->pairs);
         prep_blocks = (prepare_threads(next->cols, next->n_neg) + kBlock - 1) / kBlock;
     }
-#ifdef RG_X_PREP_SPLIT   // timing experiments only: the next prepare as its own launch in front
-    if (prep_blocks > 0) {
-        hipLaunchKernelGGL(mf_prepare_kernel, dim3((unsigned)prep_blocks), dim3(kBlock), 0, (hipStream_t)stream, prep,
-                           prep_out, 0);
-        prep_blocks = 0;
-    }
-#endif
-#ifdef RG_X_NOGEN   // timing experiments only (wrong results: the ring slot is never walked)
-    g.nwords = 0;
-#endif
     BackLaunchF f{&a, &prep, prep_out, prep_blocks, g, (hipStream_t)stream};
     return dispatch_dim(t->dim, f);
 }

@@ -1045,6 +1045,12 @@ __device__ __forceinline__ constexpr int kbit(int t, int nb, int r) { return (t 
             if (lane == 0) g_ncf_stamps[(((int64_t)blockIdx.x * ncfw::kWaves + wave) * 3 + tl_) * 16 + (k)] = t_; \
         }                                                                                                  \
     } while (0)
+// stamps inside the backward's block loop: block 0's only (the later blocks' phases are the
+// "blocks 1.." stamp pair, so no stamp is overwritten by a later block)
+#define WSB(k)          \
+    do {                \
+        if (nb == 0) WS(k); \
+    } while (0)
 #define WSK(k)                                                                                             \
     do {                                                                                                   \
         if (g_ncf_stamps) {                                                                                \
@@ -1059,6 +1065,9 @@ __device__ __forceinline__ constexpr int kbit(int t, int nb, int r) { return (t 
     do {      \
     } while (0)
 #define WSK(k) \
+    do {      \
+    } while (0)
+#define WSB(k) \
     do {      \
     } while (0)
 #endif
@@ -1598,13 +1607,13 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             wave_sync();
             stage1<2, R2S>(d2b, R2, row, g);
             wave_sync();
-            WS(7);
+            WSB(7);
             dw1b<2, 4, R2S, R1S>(gW2, bB2, R2, R1, g, j, s0);
-            WS(8);
+            WSB(8);
             wave_sync();
             stage1<4, R1S>(d1b, R1, row, g);
             wave_sync();
-            WS(9);
+            WSB(9);
             // dW1 += delta1^T X0 (the block's k-steps), db1 alongside
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
@@ -1618,7 +1627,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                     bB1[to] += av[to];
                 }
             }
-            WS(10);
+            WSB(10);
             // dX0^T = W1^T delta1^T: the block's input gradient rows, in four quarters of 32
             // columns (user 0-31, 32-63, item 0-31, 32-63), each stored at once, overflow rows
             // (lists full) in fixed point
@@ -1631,11 +1640,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
                     *reinterpret_cast<v4f *>(a.contrib + (tile * kR + row) * (int64_t)128 + 32 * qq + 16 * t + 4 * g) = dx[t];
-#ifdef RG_X_NCF_NOOVF   // timing experiments only (wrong results): no overflow accumulation
-                if (false) {
-#else
                 if ((hh == 0 ? lu : li) >= kNcfCap) {
-#endif
                     const int64_t orow = hh == 0 ? (int64_t)ur : a.num_users + ir;
 #pragma unroll
                     for (int t = 0; t < 2; ++t)
@@ -1643,7 +1648,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                         for (int r = 0; r < 4; ++r) fix_add(a.hot_grad + orow * 64 + c0 + 16 * t + 4 * g + r, dx[t][r]);
                 }
             }
-            WS(11);
+            WSB(11);
         }
         WS(12);
         if (a.pos_slot != nullptr) {

@@ -1,5 +1,6 @@
 # GPU box: attribution of the MF dense pass (mf_back_kernel) by timing-only library variants
-# (build.py --variant NAME --only rg_mf.hip -DRG_X_...; results of the X variants are wrong, the
+# (build.py --variant NAME --only rg_mf.hip -DRG_X_...: round 6 removed the RG_X_ blocks from the
+# sources, their results are under profiles/ and the code in the history; results of X variants are wrong, the
 # timings are what they are for).  Per variant: a 20-step bench line and a 50-step rocprofv3
 # kernel trace (average mf_back / mf_pairs / mf_prepare durations).
 # Usage: bash scripts/gpu_attr.sh TAG name[:ENV=VAL] ...   (base* = the product library; a variant

@@ -20,8 +20,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from recommendation_gans_amd import _lib, build  # noqa: E402
 
-WAVE_PHASES = ["ids+slots", "gather issue", "gather + fwd layer 1", "fwd rest + output", "loss", "dW4 dA3 dW3",
-               "X0 re-read issue + dA2", "dW2", "dA1 + stage", "dW1", "dX0", "contrib stores", "overflow + planned"]
+# the backward runs one 16-example block at a time (three per 48-row tile): the stamps inside its
+# block loop are block 0's (round 6; before, each block overwrote them, so the phase then named
+# "X0 re-read issue + dA2" spanned blocks 0 and 1 whole and block 2 up to dA2)
+WAVE_PHASES = ["ids+slots", "gather issue", "gather + fwd layer 1", "fwd rest + output", "loss + next-tile warm",
+               "(backward entry)", "blk0: X0 re-read issue, out layer, dW4, dA3, dW3, dA2", "blk0: dW2",
+               "blk0: dA1 + stage", "blk0: dW1", "blk0: dX0 + contrib stores", "blocks 1-2: whole backward",
+               "overflow + planned"]
 PHASES = ["ids+slots", "gather", "forward layer 0", "forward rest + output", "loss", "backward first layer", "backward rest + rows"]
 
 
