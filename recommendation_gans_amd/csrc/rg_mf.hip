@@ -636,9 +636,6 @@ struct ApplyArgs {
     const int32_t *guard;
 };
 
-#ifndef RG_DENSE_WT
-#define RG_DENSE_WT 0
-#endif
 #ifndef RG_MF_SORTED_PULL
 #define RG_MF_SORTED_PULL 1
 #endif
@@ -1275,10 +1272,6 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
         L::store_nt(a.w_out[t], lr_, D, sub, p);
         if (adam) L::store_nt(a.w_m[t], lr_, D, sub, m);
         if (has_v) L::store_nt(a.w_v[t], lr_, D, sub, v);
-    } else if (RG_DENSE_WT) {
-        L::store_wt(a.w_out[t], lr_, D, sub, p);
-        if (adam) L::store_wt(a.w_m[t], lr_, D, sub, m);
-        if (has_v) L::store_wt(a.w_v[t], lr_, D, sub, v);
     } else {
         L::store(a.w_out[t], lr_, D, sub, p);
         if (adam) L::store(a.w_m[t], lr_, D, sub, m);
@@ -1286,15 +1279,9 @@ __device__ __forceinline__ void apply_row(const ApplyArgs &a, const int64_t r, c
     }
     if (sub == 0 && a.has_bias) {
         pb = opt_update(a.opt, pb, gb, mb, vb);
-        if (RG_DENSE_WT) {
-            L::store1_wt(a.b_out[t] + lr_, pb);
-            if (adam) L::store1_wt(a.b_m[t] + lr_, mb);
-            if (has_v) L::store1_wt(a.b_v[t] + lr_, vb);
-        } else {
-            a.b_out[t][lr_] = pb;
-            if (adam) a.b_m[t][lr_] = mb;
-            if (has_v) a.b_v[t][lr_] = vb;
-        }
+        a.b_out[t][lr_] = pb;
+        if (adam) a.b_m[t][lr_] = mb;
+        if (has_v) a.b_v[t][lr_] = vb;
     }
     if (lz && sub == 0) {
         a.last_rel[r] = (int32_t)((int64_t)a.lazy_t - a.lazy_base);
