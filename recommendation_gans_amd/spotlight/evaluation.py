@@ -57,6 +57,32 @@ def _ranked(model, test_csr, train_csr=None, block=4096, k=None):
         yield u, idx, pred.argsort(axis=0)
 
 
+def _topk_hits(model, test_csr, train_csr, k, block=4096):
+    """The device top-k path of the metrics (model.topk_users, k <= TOPK_MAX), vectorised over
+    the users instead of a Python loop per user (the loop took 0.7 s per 125 k users): the users
+    with test items, their top-k rankings, hits[u, j] = ranking j of user u is one of its test
+    items (the rankings are distinct ids, so the count of hits in the first x ranks is the
+    reference's |set(ranking[:x]) & set(targets)|), and each user's number of test items."""
+    users = np.flatnonzero(np.diff(test_csr.indptr) > 0)
+    if not len(users):
+        return users, np.zeros((0, k), bool), np.zeros(0, np.int64)
+    I = np.int64(test_csr.shape[1])
+    rows = np.repeat(np.arange(test_csr.shape[0], dtype=np.int64), np.diff(test_csr.indptr))
+    keys = np.sort(rows * I + test_csr.indices.astype(np.int64))
+    hits = np.empty((len(users), k), bool)
+    for s in range(0, len(users), block):
+        ub = users[s:s + block]
+        top = np.asarray(model.topk_users(ub, int(k), train_csr), dtype=np.int64)[:, :k]
+        q = ub[:, None].astype(np.int64) * I + top
+        pos = np.minimum(np.searchsorted(keys, q), len(keys) - 1)
+        hits[s:s + len(ub)] = keys[pos] == q
+    return users, hits, np.diff(test_csr.indptr)[users].astype(np.int64)
+
+
+def _device_topk(model, k):
+    return k <= TOPK_MAX and hasattr(model, "topk_users")
+
+
 def mrr_score(model, test, train=None):
     """Mean reciprocal rank of each test user's items (evaluation.py:13-60): ranks of
     -score with ties averaged (scipy rankdata), train items pushed to the end."""
@@ -81,6 +107,16 @@ def precision_recall_score(model, test, train=None, k=10):
     test_csr = test.tocsr()
     train_csr = train.tocsr() if train is not None else None
     ks = np.array([k]) if np.isscalar(k) else np.asarray(k)
+    if _device_topk(model, int(ks.max())):
+        users, hits, n_t = _topk_hits(model, test_csr, train_csr, int(ks.max()))
+        if train_csr is not None:
+            print("Cold start users: ", int((np.diff(train_csr.indptr)[users] == 0).sum()))
+        else:
+            print("Cold start users: ", 0)
+        c = np.cumsum(hits, axis=1)
+        num = np.stack([c[:, int(x) - 1] for x in ks], axis=1).astype(np.float64)
+        return (np.mean((num / ks.astype(np.float64)[None, :]).squeeze()),
+                np.mean((num / n_t[:, None].astype(np.float64)).squeeze()))
     precision, recall = [], []
     cold = 0
     for u, targets, ranking in _ranked(model, test_csr, train_csr, k=int(ks.max())):
@@ -126,6 +162,18 @@ def mapk(actual, predicted, k=10):
 
 
 def map_at_k(model, test, k=5):
+    if _device_topk(model, k):
+        # apk over every user at once, its sums in apk's order (one position at a time)
+        test_csr = test.tocsr()
+        users, hits, n_t = _topk_hits(model, test_csr, None, k)
+        cum = np.cumsum(hits, axis=1).astype(np.float64)
+        score = np.zeros(len(users))
+        for i in range(k):
+            score = np.where(hits[:, i], score + cum[:, i] / (i + 1.0), score)
+        first = test_csr.indices[test_csr.indptr[users]]
+        only_zero = (n_t == 1) & (first == 0)          # apk: `not actual.any()` -> 0
+        vals = np.where(only_zero, 0.0, score / np.minimum(n_t, k).astype(np.float64))
+        return np.mean(vals.squeeze())
     vals = [apk(targets, ranking, k=k) for _, targets, ranking in _ranked(model, test.tocsr(), k=k)]
     return np.mean(np.array(vals).squeeze())
 
