@@ -443,8 +443,7 @@ __device__ __forceinline__ void pairs_body(const PairsArgs &a, const int64_t blk
                     const int u = tu[j], i = ti[j];
                     const int64_t row = (t & 1) ? a.num_users + i : (int64_t)u;
                     if (slot[j] < kCap) {
-                        if (!RG_DIAG_FLAG(1))
-                            a.row_list[row * kCap + slot[j]] = make_int2((t & 1) ? u : i, __float_as_int(ldz[ublk * NP + q]));
+                        if (!RG_DIAG_FLAG(1)) store_entry(a.row_list + row * kCap + slot[j], (t & 1) ? u : i, ldz[ublk * NP + q]);
                     }
                     else
                         ovf = true;
@@ -575,7 +574,7 @@ __global__ __launch_bounds__(kWave) void mf_adapt_max_kernel(PairsArgs a) {
         if (sub == 0) sl = atomicAdd(a.row_count + row, 1);
         sl = __shfl(sl, 0);
         if (sl < kCap) {
-            if (sub == 0) a.row_list[row * kCap + sl] = make_int2(side ? pr.x : pr.y, __float_as_int(dz));
+            if (sub == 0) store_entry(a.row_list + row * kCap + sl, side ? pr.x : pr.y, dz);
         } else {
             overflow_add<L>(a.hot_grad, row, a.dim, sub, dz, side ? ur : ir);
             if (sub == 0) fix_add(a.hot_bias_grad + row, dz);

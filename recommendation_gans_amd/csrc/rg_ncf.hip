@@ -306,19 +306,19 @@ __global__ __launch_bounds__(ncf_threads<E>()) void ncf_pairs_kernel(NcfArgs a) 
                 li = nli;
                 ps = nps;
                 const int64_t ex = tile * kRows + r;
-                if (lu >= 0 && lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+                if (lu >= 0 && lu < kNcfCap) store_entry(a.row_list + (int64_t)u * kNcfCap + lu, (int)ex, 1.0f);
                 if (li >= 0 && li < kNcfCap)
-                    a.row_list[(a.num_users + i) * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+                    store_entry(a.row_list + (a.num_users + i) * kNcfCap + li, (int)ex, 1.0f);
             } else if (kBackward && u >= 0) {
                 const int64_t ex = tile * kRows + r;
                 lu = atomicAdd(a.row_count + u, 1);
-                if (lu < kNcfCap) a.row_list[(int64_t)u * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+                if (lu < kNcfCap) store_entry(a.row_list + (int64_t)u * kNcfCap + lu, (int)ex, 1.0f);
                 if (q == 0 && a.pos_slot != nullptr) {
                     ps = a.pos_slot[s];
                 } else {
                     const int64_t row = a.num_users + i;
                     li = atomicAdd(a.row_count + row, 1);
-                    if (li < kNcfCap) a.row_list[row * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+                    if (li < kNcfCap) store_entry(a.row_list + row * kNcfCap + li, (int)ex, 1.0f);
                 }
             }
             sLu[r] = lu;
@@ -1443,9 +1443,9 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
         // list entries of the claimed slots (the atomics have returned by now)
         if (kBackward && lane < kR) {
             const int64_t ex = tile * kR + lane;
-            if (lu >= 0 && lu < kNcfCap) a.row_list[(int64_t)ru * kNcfCap + lu] = make_int2((int)ex, __float_as_int(1.0f));
+            if (lu >= 0 && lu < kNcfCap) store_entry(a.row_list + (int64_t)ru * kNcfCap + lu, (int)ex, 1.0f);
             if (li >= 0 && li < kNcfCap)
-                a.row_list[(a.num_users + ri) * kNcfCap + li] = make_int2((int)ex, __float_as_int(1.0f));
+                store_entry(a.row_list + (a.num_users + ri) * kNcfCap + li, (int)ex, 1.0f);
             sLu[lane] = lu;
             sLi[lane] = li;
         }

@@ -51,7 +51,7 @@ __device__ __forceinline__ void append(const OwnWork &w, const OwnTables &t, int
     if (sub == 0) sl = atomicAdd(w.row_count + row, 1);
     sl = __shfl(sl, ubase);
     if (sl < kCapO) {
-        if (sub == 0) w.row_list[row * kCapO + sl] = make_int2(other, __float_as_int(dz));
+        if (sub == 0) store_entry(w.row_list + row * kCapO + sl, other, dz);
     } else {
         float o[L::EPL];
         L::load(o, partner_table, other, t.dim, sub);
@@ -65,7 +65,7 @@ template <class L>
 __device__ __forceinline__ void append_at(const OwnWork &w, const OwnTables &t, int64_t row, int other,
                                           const float *partner_table, float dz, int sub, int sl) {
     if (sl < kCapO) {
-        if (sub == 0) w.row_list[row * kCapO + sl] = make_int2(other, __float_as_int(dz));
+        if (sub == 0) store_entry(w.row_list + row * kCapO + sl, other, dz);
     } else {
         float o[L::EPL];
         L::load(o, partner_table, other, t.dim, sub);
