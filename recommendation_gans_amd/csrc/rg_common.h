@@ -284,24 +284,22 @@ struct RowLayout {
     // each flavour")
     // write-through store (sc1) of a row slice: one 16-byte buffer store per lane, so every
     // 128-byte row reaches memory as whole lines (two interleaved 8-byte halves would each write
-    // half of every sector).
+    // half of every sector).  The table must be < 2 GiB (32-bit offsets; the one caller,
+    // rg_mf_pipe_step's pipelined kernel (A/B build), checks).  The resource is built from the table's base, which is
+    // wave-uniform: a resource per row would be a per-lane value, which buffer instructions take
+    // only through a waterfall loop.
     __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int D, int sub,
                                                     const float (&v)[EPL]) {
-        // the resource starts at the row (64-bit address arithmetic), so the 32-bit offset is within
-        // the row whatever the table's size
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xffffffff, 0x00020000);
         if constexpr (VEC) {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(base + row * (int64_t)(4 * LPU), 0, 0xffffffff, 0x00020000);
             typedef float v4f __attribute__((ext_vector_type(4)));
             const v4f t = {v[0], v[1], v[2], v[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(t, rs, sub * 16, 0, kSc1);
+            __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, kSc1);
         } else {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(base + row * (int64_t)D, 0, 0xffffffff, 0x00020000);
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
                 const int c = sub + LPU * e;
-                if (c < D) __builtin_amdgcn_raw_buffer_store_b32(v[e], rs, c * 4, 0, kSc1);
+                if (c < D) __builtin_amdgcn_raw_buffer_store_b32(v[e], rs, (int)((row * D + c) * 4), 0, kSc1);
             }
         }
     }
@@ -310,22 +308,20 @@ struct RowLayout {
     }
 
     // load past the CU's L1 (sc1: served by L2 / memory): reads rows another workgroup of the
-    // same launch wrote with write-through stores (the pipelined MF step's pair pass)
+    // same launch wrote with write-through stores (the pipelined MF step's pair pass); < 2 GiB
     __device__ static __forceinline__ void load_sc1(float (&v)[EPL], const float *__restrict__ base,
                                                     int64_t row, int D, int sub) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0xffffffff,
+                                                                           0x00020000);
         if constexpr (VEC) {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float *>(base) + row * (int64_t)(4 * LPU), 0, 0xffffffff, 0x00020000);
             typedef float v4f __attribute__((ext_vector_type(4)));
-            const v4f t = __builtin_amdgcn_raw_buffer_load_b128(rs, sub * 16, 0, kSc1);
+            const v4f t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((row * (4 * LPU) + sub * 4) * 4), 0, kSc1);
             v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
         } else {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float *>(base) + row * (int64_t)D, 0, 0xffffffff, 0x00020000);
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
                 const int c = sub + LPU * e;
-                v[e] = c < D ? __builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, kSc1) : 0.0f;
+                v[e] = c < D ? __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((row * D + c) * 4), 0, kSc1) : 0.0f;
             }
         }
     }
@@ -408,13 +404,12 @@ struct RowLayoutV {
     }
     __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int, int sub,
                                                     const float (&v)[EPL]) {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(base + row * (int64_t)D, 0, 0xffffffff, 0x00020000);   // per row: no wrap
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xffffffff, 0x00020000);
         typedef float v4f __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             const v4f t = {v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(t, rs, ((c * LPU + sub) * 4) * 4, 0, kSc1);
+            __builtin_amdgcn_raw_buffer_store_b128(t, rs, (int)((row * D + (c * LPU + sub) * 4) * 4), 0, kSc1);
         }
     }
     __device__ static __forceinline__ void store1_wt(float *p, float v) {
