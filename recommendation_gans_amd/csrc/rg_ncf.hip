@@ -1632,6 +1632,7 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
             // columns (user 0-31, 32-63, item 0-31, 32-63), each stored at once, overflow rows
             // (lists full) in fixed point
             const int lu = sLu[row], li = sLi[row], ur = sU[row], ir = sI[row];
+            float *ctile = a.contrib + (int64_t)__builtin_amdgcn_readfirstlane((int)tile) * (kR * 128);
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
                 const int hh = qq >> 1, c0 = 32 * (qq & 1);   // table half, first column in the row
@@ -1639,7 +1640,13 @@ __global__ __launch_bounds__(ncfw::kThreads) __attribute__((amdgpu_waves_per_eu(
                 bwd1<2, 4>(d1b, dx, W1s + 32 * qq, S1, g, j);
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
-                    *reinterpret_cast<v4f *>(a.contrib + (tile * kR + row) * (int64_t)128 + 32 * qq + 16 * t + 4 * g) = dx[t];
+                    // write-through (16-B sc1): these 25 MB of rows leave the XCD's L2 as they are
+                    // written instead of waiting dirty for the kernel's end-of-kernel write-back
+                    // (measured: ncf_wave_kernel 63.7-64.1 -> 62.5-63.0 us, profiles/r6/ncf/); the
+                    // resource starts at this wave's tile (a wave-uniform base, small offsets)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        dx[t], __builtin_amdgcn_make_buffer_rsrc(ctile, 0, 0xffffffff, 0x00020000),
+                        (row * 128 + 32 * qq + 16 * t + 4 * g) * 4, 0, kSc1);
                 if ((hh == 0 ? lu : li) >= kNcfCap) {
                     const int64_t orow = hh == 0 ? (int64_t)ur : a.num_users + ir;
 #pragma unroll
@@ -1936,6 +1943,7 @@ extern "C" int rg_ncf_pairs(void *stream, const rg_ncf_model_t *m, const rg_mf_b
         return fail_arg("rg_ncf_pairs: ncf_work.tile_rows must be rg_ncf_rows_per_tile(dim, mf_dim)");
     a.tc = (int)rg_ncf_cols_per_tile(b->n_neg, m->dim, m->mf_dim);
     a.tiles = rg_ncf_tiles(b->cols, b->n_neg, m->dim, m->mf_dim);
+    if (a.tiles >= ((int64_t)1 << 31)) return fail_arg("rg_ncf_pairs: more than 2^31 tiles");
     const int64_t negc = b->neg_cols > 0 ? b->neg_cols : b->global_cols;
     switch (b->loss) {
         case RG_LOSS_POINTWISE: a.n_a = (float)b->global_pos; a.n_b = (float)((int64_t)b->n_neg * negc); break;
