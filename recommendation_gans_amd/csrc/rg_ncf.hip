@@ -825,7 +825,8 @@ constexpr int kWaves = 4, kThreads = 64 * kWaves;
 // on 1,024 slots), 64.0 with these; 0: every block's forward at once (32 rows: 73.2 us)
 #ifndef RG_NCF_EARLY_TILE
 #define RG_NCF_EARLY_TILE 0      // 1: the first tile begun before the weights' barrier (its loop-carried
-                                 // state costs 184 B of scratch: not measured, not kept on)
+                                 // state costs 156 B of scratch: 67.7-68.3 vs 62.3-63.0 us per launch,
+                                 // same box, profiles/r6/ncf/ncf_early_tile_ab_r6l.txt)
 #endif
 #ifndef RG_NCF_FWD_ROLLED
 #define RG_NCF_FWD_ROLLED 0      // 1: the blockwise forward's block loop kept rolled (400 B of scratch)

@@ -1,10 +1,11 @@
 """Print VGPR / SGPR / scratch / occupancy per kernel from hipcc's resource remarks.
-    python scripts/kernel_resources.py recommendation_gans_amd/csrc/rg_mf.hip [filter]"""
+    python scripts/kernel_resources.py recommendation_gans_amd/csrc/rg_mf.hip [filter] [-DNAME=VAL ...]"""
 import re, subprocess, sys
 src = sys.argv[1]
-flt = sys.argv[2] if len(sys.argv) > 2 else ""
+flt = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("-D") else ""
+defs = [a for a in sys.argv[2:] if a.startswith("-D")]
 out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I", "include",
-                      "-x", "hip", "-c", src, "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"],
+                      *defs, "-x", "hip", "-c", src, "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"],
                      capture_output=True, text=True).stderr
 cur = None
 rows = {}
