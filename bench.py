@@ -518,6 +518,20 @@ def bench_gan(args):
     print(json.dumps(out), flush=True)
 
 
+def eval_model(tabs, num_items, dev):
+    """A stand-in for a fitted MF ImplicitFactorizationModel holding `tabs` (user_w, item_w,
+    user_b, item_b): the model's own evaluation methods (implicit.py _tables / _device_scores /
+    score_users / topk_users) bound to it, so the bench times the drop-in's evaluation path
+    without a fit."""
+    import types
+    from recommendation_gans_amd.implicit import ImplicitFactorizationModel
+    m = types.SimpleNamespace(_kind="mf", _num_items=num_items, _full_tables=None,
+                              _engine=types.SimpleNamespace(device=dev, params=lambda: tabs))
+    for name in ("_tables", "_device_scores", "score_users", "topk_users"):
+        setattr(m, name, types.MethodType(getattr(ImplicitFactorizationModel, name), m))
+    return m
+
+
 def bench_eval(args):
     """ImplicitFactorizationModel.test's ranking metrics
     (precision_recall_score + map_at_k, k = 5, evaluation.py:115-185, 334-353) over the
@@ -527,7 +541,6 @@ def bench_eval(args):
     leg is the reference's ranking (numpy argsort of each user's scores) on a bounded
     sample of users."""
     import types
-    from recommendation_gans_amd.implicit import ImplicitFactorizationModel
     from recommendation_gans_amd.spotlight import evaluation
     from recommendation_gans_amd.spotlight.interactions import Interactions
     from recommendation_gans_amd.synthetic import ML20M, movielens_like
@@ -539,10 +552,7 @@ def bench_eval(args):
     torch.manual_seed(0)
     tabs = [torch.randn(U, d, device=dev) / d, torch.randn(I, d, device=dev) / d, torch.zeros(U, device=dev),
             torch.zeros(I, device=dev)]
-    m = types.SimpleNamespace(_kind="mf", _num_items=I,
-                              _engine=types.SimpleNamespace(device=dev, params=lambda: tabs))
-    for name in ("_device_scores", "score_users", "topk_users"):
-        setattr(m, name, types.MethodType(getattr(ImplicitFactorizationModel, name), m))
+    m = eval_model(tabs, I, dev)
     csr = test.tocsr()
     n_users = int((np.diff(csr.indptr) > 0).sum())
     evaluation.precision_recall_score(m, Interactions(data.test_u[:2000], data.test_i[:2000], num_users=U,

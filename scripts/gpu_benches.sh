@@ -14,3 +14,4 @@ run mf128 --steps 50 --warmup 5 --dim 128 --no-cpu-baseline || exit $?
 run ncf --model ncf --steps 30 --warmup 5 --cpu-baseline-seconds 10 || exit $?
 run neumf --model neumf --steps 30 --warmup 5 --no-cpu-baseline || exit $?
 run gan --model gan --steps 20 --warmup 3 --no-cpu-baseline || exit $?
+run eval --model eval || exit $?

@@ -51,3 +51,21 @@ def test_failed_rank_fails_the_launch():
                        timeout=240, env=_env(), cwd=ROOT)
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_eval_model_stand_in_scores_like_the_tables():
+    """bench.py --model eval ranks through the drop-in's own evaluation methods bound to a
+    stand-in model (bench.eval_model): every attribute they read must exist (a missing one
+    broke the eval line once); scores = sigmoid(U I^T + ub + ib), checked on the CPU."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    g = torch.Generator().manual_seed(0)
+    tabs = [torch.randn(7, 4, generator=g), torch.randn(5, 4, generator=g), torch.randn(7, generator=g),
+            torch.randn(5, generator=g)]
+    m = bench.eval_model(tabs, 5, torch.device("cpu"))
+    got = m.score_users([0, 3, 6])
+    U, I, ub, ib = tabs
+    want = torch.sigmoid(U[[0, 3, 6]] @ I.T + ub[[0, 3, 6]][:, None] + ib[None, :]).numpy()
+    np.testing.assert_array_equal(got, want)
