@@ -422,7 +422,7 @@ struct RowLayoutV {
 };
 
 // The dense pass's layout for a dim's pair-pass layout L (mf_back_kernel, single-GPU MF):
-// RG_BACK_V64 / RG_BACK_V128 = lanes per row of a RowLayoutV for d = 64 / 128 (0: L itself).
+// RG_BACK_V32 / _V64 / _V128 = lanes per row of a RowLayoutV for d = 32 / 64 / 128 (0: L itself).
 // Measured (round 5, profiles/r5/attr/): d = 64 on 8 lanes x 2 float4 (8 rows per wave) instead of
 // 16 lanes x 1 float4: 55.1 -> 51.2 us per dense pass; d = 128 on 16 lanes x 2 float4 instead of
 // 32 x 1: 111.7 -> 104.3 us -- twice the bytes in flight per wave at a similar occupancy.
@@ -432,6 +432,9 @@ struct RowLayoutV {
 #ifndef RG_BACK_V128
 #define RG_BACK_V128 16
 #endif
+#ifndef RG_BACK_V32
+#define RG_BACK_V32 4   // d = 32 on 4 lanes x 2 float4 (16 rows per wave) instead of 8 x 1: dense pass
+#endif                  // 34.0-34.5 -> 31.5-32.0 us, 140.6-142.0 -> 146.5-146.8 M/s (profiles/r6/mf/attr_r6m_d32.txt)
 template <class L>
 struct BackLayout {
     using type = L;
@@ -446,6 +449,12 @@ struct BackLayout<RowLayout<16, 4, true>> {
 template <>
 struct BackLayout<RowLayout<32, 4, true>> {
     using type = RowLayoutV<RG_BACK_V128, 128 / (4 * RG_BACK_V128)>;
+};
+#endif
+#if RG_BACK_V32
+template <>
+struct BackLayout<RowLayout<8, 4, true>> {
+    using type = RowLayoutV<RG_BACK_V32, 32 / (4 * RG_BACK_V32)>;
 };
 #endif
 
