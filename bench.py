@@ -555,14 +555,15 @@ def bench_eval(args):
     m = eval_model(tabs, I, dev)
     csr = test.tocsr()
     n_users = int((np.diff(csr.indptr) > 0).sum())
-    evaluation.precision_recall_score(m, Interactions(data.test_u[:2000], data.test_i[:2000], num_users=U,
-                                                      num_items=I), k=k)       # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    p, r = evaluation.precision_recall_score(m, test, k=k)
-    mp = evaluation.map_at_k(m, test, k=k)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    with stdout_to_stderr():          # the metrics print the reference's cold-start count
+        evaluation.precision_recall_score(m, Interactions(data.test_u[:2000], data.test_i[:2000], num_users=U,
+                                                          num_items=I), k=k)       # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p, r = evaluation.precision_recall_score(m, test, k=k)
+        mp = evaluation.map_at_k(m, test, k=k)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
     out = {"metric": "evaluation test users/sec (precision/recall@5 + MAP@5), MF dim=64 MovieLens-20M",
            "value": 2 * n_users / el, "unit": "users/s", "n_gpus": 1, "steps": 2, "warmup": 1,
            "ms_per_step": el / 2 * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -576,10 +577,11 @@ def bench_eval(args):
         users = np.flatnonzero(np.diff(csr.indptr) > 0)
         sel = np.isin(data.test_u, users[:1000])
         sub = Interactions(data.test_u[sel], data.test_i[sel], num_users=U, num_items=I)
-        t0 = time.perf_counter()
-        evaluation.precision_recall_score(host, sub, k=k)
-        evaluation.map_at_k(host, sub, k=k)
-        elc = time.perf_counter() - t0
+        with stdout_to_stderr():
+            t0 = time.perf_counter()
+            evaluation.precision_recall_score(host, sub, k=k)
+            evaluation.map_at_k(host, sub, k=k)
+            elc = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": 2 * 1000 / elc, "unit": "users/s", "cores": 1, "kind": "port",
                                "sample": "1000 test users x 2 passes: scores from the device block, then the "
                                          "reference's per-user numpy argsort over all items on the host"}
