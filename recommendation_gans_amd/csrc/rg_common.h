@@ -421,6 +421,67 @@ struct RowLayoutV {
     }
 };
 
+// A row of an EVEN runtime D <= 2 * LPU * K floats over LPU lanes in float2 pairs: pair c of lane
+// `sub` holds floats (c * LPU + sub) * 2 and + 1 (rows 8-B aligned when D is even), masked past D.
+// The dense pass's layout for even dims that are not a power of two (NeuMF's GMF width 50): one
+// 8-B load per lane and pair instead of a dword per element (element-wise arithmetic, same bits).
+template <int LPU_, int K_>
+struct RowLayoutP {
+    static constexpr int LPU = LPU_;
+    static constexpr int EPL = 2 * K_;
+    static constexpr bool VEC = false;
+    static constexpr int UPW = kWave / LPU;
+    __device__ static __forceinline__ int elem(int sub, int e) { return ((e >> 1) * LPU + sub) * 2 + (e & 1); }
+    __device__ static __forceinline__ void load_strided(float (&v)[EPL], const float *__restrict__ base, int64_t row,
+                                                        int64_t stride, int D, int sub) {
+#pragma unroll
+        for (int c = 0; c < K_; ++c) {
+            const int f = (c * LPU + sub) * 2;
+            float2 t = make_float2(0.0f, 0.0f);
+            if (f < D) t = *reinterpret_cast<const float2 *>(base + row * stride + f);
+            v[2 * c] = t.x; v[2 * c + 1] = t.y;
+        }
+    }
+    __device__ static __forceinline__ void load(float (&v)[EPL], const float *__restrict__ base, int64_t row, int D,
+                                                int sub) {
+        load_strided(v, base, row, D, D, sub);
+    }
+    __device__ static __forceinline__ void load_nt(float (&v)[EPL], const float *__restrict__ base, int64_t row, int D,
+                                                   int sub) {
+        load(v, base, row, D, sub);
+    }
+    __device__ static __forceinline__ void load_sc1(float (&v)[EPL], const float *__restrict__ base, int64_t row,
+                                                    int D, int sub) {
+        load(v, base, row, D, sub);   // only the pipelined step (A/B build, d = 64) reads past L1
+    }
+    __device__ static __forceinline__ void store(float *__restrict__ base, int64_t row, int D, int sub,
+                                                 const float (&v)[EPL]) {
+#pragma unroll
+        for (int c = 0; c < K_; ++c) {
+            const int f = (c * LPU + sub) * 2;
+            if (f < D) *reinterpret_cast<float2 *>(base + row * (int64_t)D + f) = make_float2(v[2 * c], v[2 * c + 1]);
+        }
+    }
+    __device__ static __forceinline__ void store_nt(float *__restrict__ base, int64_t row, int D, int sub,
+                                                    const float (&v)[EPL]) {
+        store(base, row, D, sub, v);
+    }
+    __device__ static __forceinline__ void store_wt(float *__restrict__ base, int64_t row, int D, int sub,
+                                                    const float (&v)[EPL]) {
+        store(base, row, D, sub, v);  // only the pipelined step (A/B build, d = 64) writes through
+    }
+    __device__ static __forceinline__ void store1_wt(float *p, float v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static __forceinline__ float load1_sc1(const float *p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static __forceinline__ void zero(float (&v)[EPL]) {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) v[e] = 0.0f;
+    }
+};
+
 // The dense pass's layout for a dim's pair-pass layout L (mf_back_kernel, single-GPU MF):
 // RG_BACK_V32 / _V64 / _V128 = lanes per row of a RowLayoutV for d = 32 / 64 / 128 (0: L itself).
 // Measured (round 5, profiles/r5/attr/): d = 64 on 8 lanes x 2 float4 (8 rows per wave) instead of
@@ -431,6 +492,12 @@ struct RowLayoutV {
 #endif
 #ifndef RG_BACK_V128
 #define RG_BACK_V128 16
+#endif
+#ifndef RG_BACK_V16
+#define RG_BACK_V16 0   // d = 16 on 2 lanes x 2 float4 / 1 x 4: 28.4-30.5 / 33.2-33.5 vs 26.7-28.9 us in the NeuMF
+#endif                  // step (its tower's tables), not kept (profiles/r6/ncf/neumf_dense_layouts_r6.txt)
+#ifndef RG_BACK_P
+#define RG_BACK_P 0     // even dims 33..64 that are not 64 (NeuMF's GMF 50) on RowLayoutP<8, 4> (float2 pairs)
 #endif
 #ifndef RG_BACK_V32
 #define RG_BACK_V32 4   // d = 32 on 4 lanes x 2 float4 (16 rows per wave) instead of 8 x 1: dense pass
@@ -449,6 +516,18 @@ struct BackLayout<RowLayout<16, 4, true>> {
 template <>
 struct BackLayout<RowLayout<32, 4, true>> {
     using type = RowLayoutV<RG_BACK_V128, 128 / (4 * RG_BACK_V128)>;
+};
+#endif
+#if RG_BACK_V16
+template <>
+struct BackLayout<RowLayout<4, 4, true>> {
+    using type = RowLayoutV<RG_BACK_V16, 16 / (4 * RG_BACK_V16)>;
+};
+#endif
+#if RG_BACK_P
+template <>
+struct BackLayout<RowLayout<16, 4, false>> {
+    using type = RowLayoutP<8, 4>;   // even D only: the caller checks (BackLaunchF)
 };
 #endif
 #if RG_BACK_V32

@@ -2342,7 +2342,9 @@ struct BackLaunchF {
             // the dense pass (MF single-GPU, an owner rank's user rows, the NCF tail's embedding
             // tables pulling their per-example gradient rows) on its own row layout (RG_BACK_V64 /
             // _V128); element-wise arithmetic, so the same bits as the dispatch layout
-            if (!lazy && (a->contrib == nullptr || RG_BACK_V_NCF)) return run<LB, true>();
+            constexpr bool pairs = !LB::VEC;   // RowLayoutP: float2 pairs, even dims only
+            if (!lazy && (a->contrib == nullptr || RG_BACK_V_NCF) && (!pairs || a->dim % 2 == 0))
+                return run<LB, true>();
         }
         return run<L, false>();
     }

@@ -2,7 +2,7 @@
 # --only rg_ncf.hip ...).  The NCF / NeuMF GPU tests against every non-base variant first, then per
 # variant, interleaved twice: the NCF bench line and a rocprofv3 kernel-trace of it (average
 # ncf_wave_kernel and tail-launch durations).
-# Usage: bash scripts/gpu_ncf_lib_ab.sh TAG base NAME ...
+# Usage: [NCFMODEL=neumf] bash scripts/gpu_ncf_lib_ab.sh TAG base NAME ...
 set -o pipefail
 TAG=${1:-run}; shift
 mkdir -p gpurun_out
@@ -14,16 +14,16 @@ for name in "$@"; do
   lib=$(libof $name); [ -f "$lib" ] || { echo "missing $lib"; exit 1; }
   [ "$name" = base ] && continue
   RG_LIB=$lib timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
-    -m gpu tests/test_ncf_wave_gpu.py tests/test_ncf_gpu.py tests/test_neumf_gpu.py > gpurun_out/ncf_ab_tests_${TAG}_$name.log 2>&1
+    -m gpu tests/test_ncf_wave_gpu.py tests/test_ncf_gpu.py tests/test_neumf_gpu.py tests/test_mf_gpu.py > gpurun_out/ncf_ab_tests_${TAG}_$name.log 2>&1
   rc=$?; echo "$name tests exit=$rc" | tee -a $OUT; tail -2 gpurun_out/ncf_ab_tests_${TAG}_$name.log
   [ $rc -eq 0 ] || exit $rc
 done
 for rep in 1 2; do
   for name in "$@"; do
     lib=$(libof $name)
-    RG_LIB=$lib timeout -k 10 200 python3 bench.py --model ncf --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/ncf_ab_${TAG}_$name.json 2>gpurun_out/ncf_ab_${TAG}_$name.err || exit $?
+    RG_LIB=$lib timeout -k 10 200 python3 bench.py --model ${NCFMODEL:-ncf} --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/ncf_ab_${TAG}_$name.json 2>gpurun_out/ncf_ab_${TAG}_$name.err || exit $?
     python3 -c "import json;d=json.load(open('gpurun_out/ncf_ab_${TAG}_$name.json'));print('$name', 'bench', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step']*1e3,1), 'us/step')" | tee -a $OUT
-    (cd /tmp && RG_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ncf_ab_prof_${TAG}_${name}_$rep -o run -- python3 $R/bench.py --model ncf --steps 40 --warmup 5 --no-cpu-baseline > /dev/null 2>$R/gpurun_out/ncf_ab_prof_${TAG}_$name.err) || exit $?
+    (cd /tmp && RG_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ncf_ab_prof_${TAG}_${name}_$rep -o run -- python3 $R/bench.py --model ${NCFMODEL:-ncf} --steps 40 --warmup 5 --no-cpu-baseline > /dev/null 2>$R/gpurun_out/ncf_ab_prof_${TAG}_$name.err) || exit $?
     python3 - "$R/gpurun_out/ncf_ab_prof_${TAG}_${name}_$rep" "$name" <<'EOF' | tee -a $OUT
 import csv, glob, sys
 out = []
