@@ -497,7 +497,9 @@ struct RowLayoutP {
 #define RG_BACK_V16 0   // d = 16 on 2 lanes x 2 float4 / 1 x 4: 28.4-30.5 / 33.2-33.5 vs 26.7-28.9 us in the NeuMF
 #endif                  // step (its tower's tables), not kept (profiles/r6/ncf/neumf_dense_layouts_r6.txt)
 #ifndef RG_BACK_P
-#define RG_BACK_P 0     // even dims 33..64 that are not 64 (NeuMF's GMF 50) on RowLayoutP<8, 4> (float2 pairs)
+#define RG_BACK_P 0     // even dims 33..64 that are not 64 (NeuMF's GMF 50) on RowLayoutP<RG_BACK_P, 32 / RG_BACK_P>
+                        // (float2 pairs; lanes per row): 8 lanes measured slower in the NeuMF step, 47.7-47.8 vs
+                        // 45.8-46.2 us (profiles/r6/ncf/neumf_dense_layouts_r6.txt)
 #endif
 #ifndef RG_BACK_V32
 #define RG_BACK_V32 4   // d = 32 on 4 lanes x 2 float4 (16 rows per wave) instead of 8 x 1: dense pass
@@ -527,7 +529,7 @@ struct BackLayout<RowLayout<4, 4, true>> {
 #if RG_BACK_P
 template <>
 struct BackLayout<RowLayout<16, 4, false>> {
-    using type = RowLayoutP<8, 4>;   // even D only: the caller checks (BackLaunchF)
+    using type = RowLayoutP<RG_BACK_P, 32 / RG_BACK_P>;   // even D only: the caller checks (BackLaunchF)
 };
 #endif
 #if RG_BACK_V32
