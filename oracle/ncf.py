@@ -29,6 +29,9 @@ import math
 
 import torch
 
+from . import mf as omf
+from . import rng as orng
+
 U32 = 2.0 ** -24          # fp32 unit roundoff
 
 
@@ -51,8 +54,6 @@ def _decide(z, a, W, b, flip):
     amb = z64.abs() <= band
     return torch.where(amb, z64 <= 0, z > 0), amb
 
-from . import mf as omf
-from . import rng as orng
 
 LRELU = 0.1
 DROP_SCALE = 2.0
